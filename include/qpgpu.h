@@ -1,0 +1,102 @@
+/*
+ * qpgpu.h — C ABI of the MI355X (gfx950) Plonky2 prover backend.
+ *
+ * The reference (aletheia-labs/qp-zk-circuits-rm) has no FFI: its hot path is
+ * the Rust crate qp-plonky2 1.1.1 called from qp-wormhole-prover.  Each entry
+ * point below names the plonky2 routine it replaces and the reference call
+ * site that reaches it.  A Rust binding is a
+ * `[patch.crates-io]` qp-plonky2 whose routines call these functions
+ * (INTEGRATION.md).
+ *
+ * Conventions
+ *   - Field elements are canonical Goldilocks u64 (p = 2^64 - 2^32 + 1);
+ *     extension elements are (c0, c1) pairs, X^2 = 7.
+ *   - Host buffers are caller-owned and only borrowed for the call.  Device
+ *     objects (qp_ctx, qp_batch, qp_prover) are opaque handles released by
+ *     their _free / _destroy function.
+ *   - `_dev` variants take device pointers and run on the context's stream
+ *     without synchronising (inputs already resident in HBM).
+ *   - Every function returns a qp_status; it never aborts or throws across
+ *     the ABI.  qp_ctx_last_error() gives the message of the last failure.
+ *   - A qp_ctx is single-thread-affine (one HIP stream); concurrent callers
+ *     use distinct contexts, which are independent.
+ */
+#ifndef QPGPU_H
+#define QPGPU_H
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+typedef enum {
+    QP_OK = 0,
+    QP_ERR_ARG = 1,      /* bad shape / null pointer / out-of-range index */
+    QP_ERR_HIP = 2,      /* HIP runtime error (no device, launch failure) */
+    QP_ERR_OOM = 3,      /* device allocation failed */
+    QP_ERR_STATE = 4,    /* call order violated (e.g. prove before commit) */
+    QP_ERR_WITNESS = 5,  /* witness conflict ("set twice with different values") or unsatisfied */
+    QP_ERR_FORMAT = 6    /* malformed serialized input */
+} qp_status;
+
+typedef struct qp_ctx qp_ctx;
+typedef struct qp_batch qp_batch;
+
+/* ---- context ---------------------------------------------------------- */
+int qp_ctx_create(int device, qp_ctx **out);
+void qp_ctx_destroy(qp_ctx *ctx);
+const char *qp_ctx_last_error(const qp_ctx *ctx);
+/* run subsequent work on an external HIP stream (e.g. torch's); NULL = own stream */
+int qp_ctx_set_stream(qp_ctx *ctx, void *hip_stream);
+int qp_ctx_synchronize(qp_ctx *ctx);
+/* library build/version string */
+const char *qp_version(void);
+
+/* ---- PolynomialBatch (plonky2 fri/oracle.rs) ----------------------------
+ * Replaces PolynomialBatch::from_values (ifft -> coset LDE -> transpose ->
+ * reverse_index_bits -> MerkleTree::new).  Reached from
+ * WormholeProver::prove (wormhole/prover/src/lib.rs:233-237) for the wires,
+ * zs/partial-products and quotient commitments, and from
+ * WormholeProver::new -> CircuitBuilder::build (lib.rs:190-202) for the
+ * constants/sigmas commitment.
+ *   values: column-major [npolys][2^log_n]; salt: row-major [N][nsalt] (may be
+ *   NULL when nsalt == 0), N = 2^(log_n+rate_bits).
+ *   coeffs_out (optional): [npolys][2^log_n]; cap_out: [2^cap_height][4].
+ *   out (optional): keeps the LDE matrix + tree resident for openings.     */
+int qp_commit_values(qp_ctx *ctx, const uint64_t *values, uint32_t npolys, uint32_t log_n, uint32_t rate_bits,
+                     uint32_t cap_height, const uint64_t *salt, uint32_t nsalt, uint64_t *coeffs_out,
+                     uint64_t *cap_out, qp_batch **out);
+/* PolynomialBatch::from_coeffs (quotient chunks) — same, from coefficients */
+int qp_commit_coeffs(qp_ctx *ctx, const uint64_t *coeffs, uint32_t npolys, uint32_t log_n, uint32_t rate_bits,
+                     uint32_t cap_height, const uint64_t *salt, uint32_t nsalt, uint64_t *cap_out, qp_batch **out);
+/* device-resident variant: d_values [nbat][npolys][n] on the device; d_cap_out
+ * [nbat][2^cap_h][4] on the device; no host sync.  Batches are independent
+ * polynomial batches of identical shape (one per proof).                   */
+int qp_commit_values_dev(qp_ctx *ctx, const uint64_t *d_values, uint32_t nbat, uint32_t npolys, uint32_t log_n,
+                         uint32_t rate_bits, uint32_t cap_height, uint64_t *d_cap_out, qp_batch **out);
+
+/* MerkleTree::get + MerkleTree::prove for a list of leaf indices:
+ * leaves_out [nidx][npolys+nsalt], siblings_out [nidx][log_N - cap_h][4]    */
+int qp_batch_open(qp_batch *b, const uint32_t *leaf_idx, uint32_t nidx, uint64_t *leaves_out,
+                  uint64_t *siblings_out);
+/* copies the LDE matrix, leaf order, column-major [npolys][N] (tests) */
+int qp_batch_lde(qp_batch *b, uint64_t *out);
+/* copies the coefficients [npolys][n] */
+int qp_batch_coeffs(qp_batch *b, uint64_t *out);
+void qp_batch_free(qp_batch *b);
+
+/* ---- primitives (plonky2 field/fft.rs, hash/poseidon.rs) ----------------- */
+/* PolynomialValues::ifft for ncols columns, in place, column-major          */
+int qp_ifft(qp_ctx *ctx, uint64_t *data, uint32_t ncols, uint32_t log_n);
+/* PolynomialCoeffs::lde(rate_bits).coset_fft(shift), output in Merkle-leaf
+ * (bit-reversed) row order, column-major [ncols][N]                         */
+int qp_lde(qp_ctx *ctx, const uint64_t *coeffs, uint32_t ncols, uint32_t log_n, uint32_t rate_bits, uint64_t shift,
+           uint64_t *out);
+/* Poseidon permutation of n 12-element states, in place                   */
+int qp_poseidon_permute(qp_ctx *ctx, uint64_t *states, uint64_t n);
+
+#ifdef __cplusplus
+}
+#endif
+#endif

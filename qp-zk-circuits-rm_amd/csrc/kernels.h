@@ -1,0 +1,65 @@
+// kernels.h — launchers for the gfx950 kernels of the prover hot path.
+// Layouts (device, all canonical u64):
+//   polynomial matrices are column-major [col][len] with a column stride;
+//   an LDE matrix holds column c at rows in Merkle-leaf order: row i is the
+//   evaluation at g*w_N^{rev(i)} (plonky2 fri/oracle.rs reverse_index_bits);
+//   digests of a tree: level 0 (N leaf digests) followed by each parent level
+//   down to the 2^cap_h cap, 4 felts per digest.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+namespace qpk {
+
+constexpr unsigned TW_LOG = 16;  // twiddle tables cover sizes up to 2^16
+
+struct Twiddles {
+  uint64_t *fwd = nullptr;  // fwd[j] = w_{2^TW_LOG}^j,   j < 2^(TW_LOG-1)
+  uint64_t *inv = nullptr;  // inv[j] = w_{2^TW_LOG}^-j
+};
+
+hipError_t twiddles_init(Twiddles &t, hipStream_t s);
+void twiddles_free(Twiddles &t);
+
+// values -> coefficients (plonky2 PolynomialValues::ifft), natural order in/out.
+// batch: nbat independent matrices at in + b*in_bstride etc.
+void intt(const Twiddles &t, const uint64_t *in, uint64_t in_stride, uint64_t *out, uint64_t out_stride,
+          uint32_t ncols, uint32_t log_n, uint32_t nbat, uint64_t in_bstride, uint64_t out_bstride, hipStream_t s);
+
+// coefficients (n) -> coset LDE (N = n << rate_bits) at shift*w_N^j, written in
+// Merkle-leaf (bit-reversed) order.  (plonky2 PolynomialBatch::lde_values)
+void lde(const Twiddles &t, const uint64_t *coeffs, uint64_t c_stride, uint64_t *out, uint64_t o_stride,
+         uint32_t ncols, uint32_t log_n, uint32_t rate_bits, uint64_t shift, uint32_t nbat,
+         uint64_t c_bstride, uint64_t o_bstride, hipStream_t s);
+
+// leaf digests: hash_or_noop(row i of [ncols] ++ salt[i][nsalt])
+void leaf_hash(const uint64_t *cols, uint64_t stride, uint32_t ncols, const uint64_t *salt, uint32_t nsalt,
+               uint64_t *digests, uint32_t N, uint32_t nbat, uint64_t c_bstride, uint64_t s_bstride,
+               uint64_t d_bstride, hipStream_t s);
+
+// parent levels down to the cap (two_to_one), appended after the N leaf digests
+void merkle_tree(uint64_t *digests, uint32_t log_N, uint32_t cap_h, uint32_t nbat, uint64_t d_bstride,
+                 hipStream_t s);
+
+inline uint64_t tree_digest_count(uint32_t log_N, uint32_t cap_h) {
+  uint64_t n = 0;
+  for (uint32_t k = 0; k <= log_N - cap_h; k++) n += (uint64_t)1 << (log_N - k);
+  return n;
+}
+inline uint64_t tree_level_offset(uint32_t log_N, uint32_t level) {  // in digests
+  uint64_t o = 0;
+  for (uint32_t k = 0; k < level; k++) o += (uint64_t)1 << (log_N - k);
+  return o;
+}
+
+// row gather for query openings: out[q][c] = cols[c*stride + idx[q]]
+void gather_rows(const uint64_t *cols, uint64_t stride, uint32_t ncols, const uint32_t *idx, uint32_t nidx,
+                 uint64_t *out, hipStream_t s);
+// Merkle paths: out[q][k][4] = sibling digest at level k of leaf idx[q]
+void gather_paths(const uint64_t *digests, uint32_t log_N, uint32_t cap_h, const uint32_t *idx, uint32_t nidx,
+                  uint64_t *out, hipStream_t s);
+
+// bulk Poseidon permutations (states [n][12], in place)
+void permute_batch(uint64_t *states, uint64_t n, hipStream_t s);
+
+}  // namespace qpk

@@ -1,0 +1,11 @@
+"""qp_wormhole — host-side mirror of the reference's prover API over the
+MI355X-native C ABI (include/qpgpu.h, libqpgpu.so).
+
+Mirrors qp-wormhole-prover's WormholeProver (wormhole/prover/src/lib.rs:74-237)
+and plonky2's PolynomialBatch for the parity tests.  The HIP library is the
+only backend: importing the native pieces raises if it is not built.
+"""
+from ._native import (Context, PolynomialBatch, QpError, header_symbols, ifft, lde, lib,  # noqa: F401
+                      poseidon_permute)
+
+__all__ = ["Context", "PolynomialBatch", "QpError", "ifft", "lde", "poseidon_permute", "lib", "header_symbols"]

@@ -1,0 +1,193 @@
+"""ctypes binding of libqpgpu.so (include/qpgpu.h).
+
+The product path is the HIP library only: if libqpgpu.so is missing or cannot
+be loaded this module raises, there is no CPU fallback.
+"""
+import ctypes
+import os
+import re
+
+import numpy as np
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(HERE, "libqpgpu.so")
+HEADER = os.path.join(os.path.dirname(os.path.dirname(HERE)), "include", "qpgpu.h")
+
+U64P = np.ctypeslib.ndpointer(np.uint64, flags="C_CONTIGUOUS")
+U32P = np.ctypeslib.ndpointer(np.uint32, flags="C_CONTIGUOUS")
+VP = ctypes.c_void_p
+PP = ctypes.POINTER(ctypes.c_void_p)
+
+STATUS = {0: "QP_OK", 1: "QP_ERR_ARG", 2: "QP_ERR_HIP", 3: "QP_ERR_OOM", 4: "QP_ERR_STATE",
+          5: "QP_ERR_WITNESS", 6: "QP_ERR_FORMAT"}
+
+
+class QpError(RuntimeError):
+    def __init__(self, code, msg=""):
+        self.code = code
+        super().__init__(f"{STATUS.get(code, code)}: {msg}")
+
+
+_lib = None
+
+
+def header_symbols():
+    """Function names declared in include/qpgpu.h."""
+    txt = open(HEADER).read()
+    return sorted(set(re.findall(r"^\s*(?:const\s+)?\w+\s+\*?\s*(qp_\w+)\s*\(", txt, re.M)))
+
+
+def lib():
+    global _lib
+    if _lib is not None:
+        return _lib
+    if not os.path.exists(LIB_PATH):
+        raise ImportError(f"{LIB_PATH} not built: run `python -c 'import __graft_entry__ as g; g.build()'`")
+    L = ctypes.CDLL(LIB_PATH)
+    sig = {
+        "qp_version": (ctypes.c_char_p, []),
+        "qp_ctx_create": (ctypes.c_int, [ctypes.c_int, PP]),
+        "qp_ctx_destroy": (None, [VP]),
+        "qp_ctx_last_error": (ctypes.c_char_p, [VP]),
+        "qp_ctx_set_stream": (ctypes.c_int, [VP, VP]),
+        "qp_ctx_synchronize": (ctypes.c_int, [VP]),
+        "qp_commit_values": (ctypes.c_int, [VP, U64P, ctypes.c_uint32, ctypes.c_uint32, ctypes.c_uint32,
+                                            ctypes.c_uint32, VP, ctypes.c_uint32, VP, U64P, PP]),
+        "qp_commit_coeffs": (ctypes.c_int, [VP, U64P, ctypes.c_uint32, ctypes.c_uint32, ctypes.c_uint32,
+                                            ctypes.c_uint32, VP, ctypes.c_uint32, U64P, PP]),
+        "qp_commit_values_dev": (ctypes.c_int, [VP, VP, ctypes.c_uint32, ctypes.c_uint32, ctypes.c_uint32,
+                                                ctypes.c_uint32, ctypes.c_uint32, VP, PP]),
+        "qp_batch_open": (ctypes.c_int, [VP, U32P, ctypes.c_uint32, U64P, U64P]),
+        "qp_batch_lde": (ctypes.c_int, [VP, U64P]),
+        "qp_batch_coeffs": (ctypes.c_int, [VP, U64P]),
+        "qp_batch_free": (None, [VP]),
+        "qp_ifft": (ctypes.c_int, [VP, U64P, ctypes.c_uint32, ctypes.c_uint32]),
+        "qp_lde": (ctypes.c_int, [VP, U64P, ctypes.c_uint32, ctypes.c_uint32, ctypes.c_uint32, ctypes.c_uint64,
+                                  U64P]),
+        "qp_poseidon_permute": (ctypes.c_int, [VP, U64P, ctypes.c_uint64]),
+    }
+    for name, (res, args) in sig.items():
+        f = getattr(L, name)
+        f.restype = res
+        f.argtypes = args
+    _lib = L
+    return L
+
+
+class Context:
+    """One HIP stream on one device (qp_ctx)."""
+
+    def __init__(self, device=0):
+        L = lib()
+        h = ctypes.c_void_p()
+        rc = L.qp_ctx_create(device, ctypes.byref(h))
+        if rc:
+            raise QpError(rc, f"qp_ctx_create(device={device})")
+        self.h = h
+
+    def check(self, rc, what=""):
+        if rc:
+            raise QpError(rc, f"{what}: {lib().qp_ctx_last_error(self.h).decode()}")
+
+    def close(self):
+        if self.h:
+            lib().qp_ctx_destroy(self.h)
+            self.h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def set_stream(self, stream_ptr):
+        self.check(lib().qp_ctx_set_stream(self.h, stream_ptr), "set_stream")
+
+    def synchronize(self):
+        self.check(lib().qp_ctx_synchronize(self.h), "synchronize")
+
+
+class PolynomialBatch:
+    """Device-resident committed polynomial batch (plonky2 PolynomialBatch)."""
+
+    def __init__(self, ctx, handle, npolys, nsalt, log_n, rate_bits, cap_height, cap, coeffs=None):
+        self.ctx, self.h = ctx, handle
+        self.npolys, self.nsalt, self.log_n, self.rate_bits, self.cap_height = npolys, nsalt, log_n, rate_bits, cap_height
+        self.cap, self.coeffs = cap, coeffs
+
+    @classmethod
+    def from_values(cls, ctx, values, rate_bits, cap_height, salt=None, keep=True):
+        values = np.ascontiguousarray(values, dtype=np.uint64)
+        npolys, n = values.shape
+        log_n = n.bit_length() - 1
+        nsalt = 0 if salt is None else salt.shape[1]
+        salt_c = None if salt is None else np.ascontiguousarray(salt, dtype=np.uint64)
+        coeffs = np.zeros_like(values)
+        cap = np.zeros(((1 << cap_height), 4), np.uint64)
+        h = ctypes.c_void_p()
+        rc = lib().qp_commit_values(ctx.h, values, npolys, log_n, rate_bits, cap_height,
+                                    None if salt_c is None else salt_c.ctypes.data, nsalt, coeffs.ctypes.data, cap,
+                                    ctypes.byref(h) if keep else None)
+        ctx.check(rc, "qp_commit_values")
+        return cls(ctx, h if keep else None, npolys, nsalt, log_n, rate_bits, cap_height, cap, coeffs)
+
+    @classmethod
+    def from_coeffs(cls, ctx, coeffs, rate_bits, cap_height, salt=None, keep=True):
+        coeffs = np.ascontiguousarray(coeffs, dtype=np.uint64)
+        npolys, n = coeffs.shape
+        log_n = n.bit_length() - 1
+        nsalt = 0 if salt is None else salt.shape[1]
+        salt_c = None if salt is None else np.ascontiguousarray(salt, dtype=np.uint64)
+        cap = np.zeros(((1 << cap_height), 4), np.uint64)
+        h = ctypes.c_void_p()
+        rc = lib().qp_commit_coeffs(ctx.h, coeffs, npolys, log_n, rate_bits, cap_height,
+                                    None if salt_c is None else salt_c.ctypes.data, nsalt, cap,
+                                    ctypes.byref(h) if keep else None)
+        ctx.check(rc, "qp_commit_coeffs")
+        return cls(ctx, h if keep else None, npolys, nsalt, log_n, rate_bits, cap_height, cap, coeffs)
+
+    def open(self, indices):
+        idx = np.ascontiguousarray(indices, dtype=np.uint32)
+        W = self.npolys + self.nsalt
+        depth = self.log_n + self.rate_bits - self.cap_height
+        leaves = np.zeros((len(idx), W), np.uint64)
+        sibs = np.zeros((len(idx), depth, 4), np.uint64)
+        self.ctx.check(lib().qp_batch_open(self.h, idx, len(idx), leaves, sibs), "qp_batch_open")
+        return leaves, sibs
+
+    def lde(self):
+        out = np.zeros((self.npolys, 1 << (self.log_n + self.rate_bits)), np.uint64)
+        self.ctx.check(lib().qp_batch_lde(self.h, out), "qp_batch_lde")
+        return out
+
+    def free(self):
+        if self.h:
+            lib().qp_batch_free(self.h)
+            self.h = None
+
+    def __del__(self):
+        try:
+            self.free()
+        except Exception:
+            pass
+
+
+def ifft(ctx, data):
+    a = np.ascontiguousarray(data, dtype=np.uint64).copy()
+    ncols, n = a.shape
+    ctx.check(lib().qp_ifft(ctx.h, a, ncols, n.bit_length() - 1), "qp_ifft")
+    return a
+
+
+def lde(ctx, coeffs, rate_bits, shift=0xC65C18B67785D900):
+    c = np.ascontiguousarray(coeffs, dtype=np.uint64)
+    ncols, n = c.shape
+    out = np.zeros((ncols, n << rate_bits), np.uint64)
+    ctx.check(lib().qp_lde(ctx.h, c, ncols, n.bit_length() - 1, rate_bits, shift, out), "qp_lde")
+    return out
+
+
+def poseidon_permute(ctx, states):
+    s = np.ascontiguousarray(states, dtype=np.uint64).copy()
+    ctx.check(lib().qp_poseidon_permute(ctx.h, s, s.shape[0]), "qp_poseidon_permute")
+    return s
