@@ -96,6 +96,50 @@ int qp_lde(qp_ctx *ctx, const uint64_t *coeffs, uint32_t ncols, uint32_t log_n, 
 /* Poseidon permutation of n 12-element states, in place                   */
 int qp_poseidon_permute(qp_ctx *ctx, uint64_t *states, uint64_t n);
 
+
+/* ---- circuits and witnesses (host; no device needed) ---------------------
+ * Native equivalent of plonky2's CircuitBuilder::build / build_prover and
+ * generate_partial_witness for the reference circuits.                     */
+typedef struct qp_circuit qp_circuit;
+typedef struct qp_witness qp_witness;
+
+/* CircuitInputs (wormhole/circuit/src/inputs.rs:25-52) in byte form */
+typedef struct {
+    uint8_t funding_amount[16];        /* u128, little-endian */
+    uint8_t nullifier[32];
+    uint8_t root_hash[32];
+    uint8_t exit_account[32];
+    uint8_t secret[32];
+    uint64_t transfer_count;
+    uint8_t funding_account[32];
+    uint8_t unspendable_account[32];
+    uint32_t num_nodes;                /* storage proof length (<= 20) */
+    const uint8_t *const *nodes;       /* node byte strings */
+    const uint32_t *node_lens;
+    const uint64_t *indices;           /* hex-character child-hash indices */
+} qp_wormhole_inputs;
+
+/* WormholeCircuit::new(config) + build_prover (wormhole/circuit/src/circuit.rs:76-108,
+ * wormhole/prover/src/lib.rs:190-202) — host part.  zero_knowledge selects
+ * standard_recursion_zk_config (salted commitments) vs standard_recursion_config. */
+int qp_wormhole_circuit_new(int zero_knowledge, qp_circuit **out);
+void qp_circuit_free(qp_circuit *c);
+/* info[0..6] = degree_bits, num_wires, num_routed_wires, num_constants,
+ *              num_public_inputs, gates used (before padding), num_gate_constraints */
+int qp_circuit_info(const qp_circuit *c, uint32_t *info);
+/* CommonCircuitData::to_bytes (plonky2 util/serialization.rs) */
+int qp_circuit_common_data(const qp_circuit *c, uint8_t *out, size_t cap, size_t *len);
+/* preprocessed constants||sigmas values over H, [num_constants+num_routed][n] */
+int qp_circuit_constants_sigmas(const qp_circuit *c, uint64_t *out);
+/* WormholeProver::commit (lib.rs:209-225) + witness generation.  On a witness
+ * conflict returns QP_ERR_WITNESS with the reference's message in err.     */
+int qp_wormhole_commit(const qp_circuit *c, const qp_wormhole_inputs *in, qp_witness **out, char *err,
+                       size_t errcap);
+/* full wire matrix, column-major [num_wires][n] */
+int qp_witness_wires(const qp_witness *w, uint64_t *out);
+int qp_witness_public_inputs(const qp_witness *w, uint64_t *out, uint32_t cap, uint32_t *n);
+void qp_witness_free(qp_witness *w);
+
 #ifdef __cplusplus
 }
 #endif

@@ -13,10 +13,12 @@ or_merkle_t *or_merkle_build(const gl_t *leaves, unsigned log_n, size_t width, u
     memcpy(t->leaves, leaves, n * width * sizeof(gl_t));
     t->levels = calloc(log_n + 1, sizeof(gl_t *));
     t->levels[0] = malloc(n * 4 * sizeof(gl_t));
+#pragma omp parallel for schedule(static)
     for (size_t i = 0; i < n; i++) ps_hash_or_noop(leaves + i * width, width, t->levels[0] + 4 * i);
     for (unsigned k = 1; k <= log_n - cap_height; k++) {
         size_t m = n >> k;
         t->levels[k] = malloc(m * 4 * sizeof(gl_t));
+#pragma omp parallel for schedule(static) if (m > 1024)
         for (size_t i = 0; i < m; i++)
             ps_two_to_one(t->levels[k - 1] + 8 * i, t->levels[k - 1] + 8 * i + 4, t->levels[k] + 4 * i);
     }

@@ -160,3 +160,46 @@ long ora_merkle_find_index(const uint64_t *leaf, size_t width, const uint64_t *s
     }
     return -1;
 }
+
+int or_prove(const uint8_t *common_bytes, size_t clen, const gl_t *consts_sigmas, const gl_t *wires,
+             const gl_t *pis, size_t npis, uint8_t *proof_out, size_t out_cap, size_t *out_len,
+             gl_t *cs_cap_out, gl_t *digest_out);
+/* full CPU prove; also returns the verifier-only data (cap, digest) */
+int ora_prove(const uint8_t *cb, size_t clen, const uint64_t *cs, const uint64_t *wires, const uint64_t *pis,
+              size_t npis, uint8_t *out, size_t cap, size_t *len, uint64_t *cs_cap, uint64_t *digest) {
+    return or_prove(cb, clen, cs, wires, pis, npis, out, cap, len, cs_cap, digest);
+}
+
+/* Witness check on H: every filtered gate constraint vanishes at every row,
+ * and the copy constraints hold (permutation grand product == 1 for fixed
+ * pseudo-random beta, gamma).  Returns -1 if satisfied, the first failing
+ * row, or -2 for a failed permutation check, -3 for bad input. */
+long ora_check_witness(const uint8_t *cb, size_t clen, const uint64_t *cs, const uint64_t *wires,
+                       const uint64_t *pis, size_t npis) {
+    or_common_t c;
+    size_t used;
+    if (or_parse_common(cb, clen, &used, &c) || used != clen) return -3;
+    size_t n = (size_t)1 << c.degree_bits;
+    unsigned W = (unsigned)c.num_wires, R = (unsigned)c.num_routed_wires, NC = (unsigned)c.num_constants;
+    gl_t pih[4];
+    ps_hash_no_pad(pis, npis, pih);
+    gl_t lc[64], lw[256], out[512];
+    for (size_t i = 0; i < n; i++) {
+        for (unsigned k = 0; k < NC + R; k++) lc[k] = cs[(size_t)k * n + i];
+        for (unsigned k = 0; k < W; k++) lw[k] = wires[(size_t)k * n + i];
+        or_eval_gate_constraints_base(&c, lc, lw, pih, out);
+        for (unsigned k = 0; k < c.num_gate_constraints; k++)
+            if (out[k]) return (long)i;
+    }
+    gl_t beta = 0x1234567890abcdefULL % GL_P, gamma = 0x0fedcba987654321ULL % GL_P;
+    gl_t w = gl_root_of_unity((unsigned)c.degree_bits), x = 1, num = 1, den = 1;
+    for (size_t i = 0; i < n; i++) {
+        for (unsigned j = 0; j < R; j++) {
+            gl_t wv = wires[(size_t)j * n + i];
+            num = gl_mul(num, gl_add(gl_add(wv, gl_mul(beta, gl_mul(c.k_is[j], x))), gamma));
+            den = gl_mul(den, gl_add(gl_add(wv, gl_mul(beta, cs[(size_t)(NC + j) * n + i])), gamma));
+        }
+        x = gl_mul(x, w);
+    }
+    return num == den ? -1 : -2;
+}

@@ -108,13 +108,17 @@ static inline gl_t sbox(gl_t x) {
 }
 
 static void mds(gl_t s[PS_WIDTH]) {
+    /* s < 2^64, constants < 2^6: split into 32-bit halves so each partial
+     * sum fits a u64 (13 terms * 2^38), then one 128-bit reduction */
     gl_t o[PS_WIDTH];
+    uint64_t lo[PS_WIDTH * 2], hi[PS_WIDTH * 2];
+    for (int i = 0; i < PS_WIDTH; i++) { lo[i] = lo[i + PS_WIDTH] = s[i] & 0xFFFFFFFFULL; hi[i] = hi[i + PS_WIDTH] = s[i] >> 32; }
     for (int r = 0; r < PS_WIDTH; r++) {
-        unsigned __int128 acc = 0;
-        for (int i = 0; i < PS_WIDTH; i++)
-            acc += (unsigned __int128)s[(i + r) % PS_WIDTH] * PS_MDS_CIRC[i];
-        acc += (unsigned __int128)s[r] * PS_MDS_DIAG[r];
-        o[r] = gl_reduce128(acc);
+        uint64_t al = 0, ah = 0;
+        for (int i = 0; i < PS_WIDTH; i++) { al += lo[i + r] * PS_MDS_CIRC[i]; ah += hi[i + r] * PS_MDS_CIRC[i]; }
+        al += lo[r] * PS_MDS_DIAG[r];
+        ah += hi[r] * PS_MDS_DIAG[r];
+        o[r] = gl_reduce128((unsigned __int128)al + ((unsigned __int128)ah << 32));
     }
     memcpy(s, o, sizeof(o));
 }

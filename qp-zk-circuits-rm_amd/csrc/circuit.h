@@ -1,0 +1,217 @@
+// circuit.h — native Plonky2-compatible circuit builder, preprocessing and
+// witness generation (host side of the prover).
+//
+// Replaces qp-plonky2 1.1.1 plonk/circuit_builder.rs (CircuitBuilder::build,
+// SURVEY.md a0/a1), iop/generator.rs (generate_partial_witness, a3) and the
+// gadgets the reference circuits use (arithmetic.rs, split_base.rs,
+// hash/hashing.rs hash_n_to_m_no_pad, select, is_equal).  Gate set: Noop,
+// Constant, PublicInput, BaseSum<2>, Arithmetic, Poseidon — exactly the
+// Wormhole circuit's ([FIX] common.bin).
+//
+// Witness generation is schedule-driven: build() resolves the generator
+// dependency order once (generators are structural, values are not), so a
+// proof's witness is one linear pass over the schedule — cheap enough to run
+// 256 proofs per batch on the host threads.
+#pragma once
+#include <stdint.h>
+#include <map>
+#include <string>
+#include <unordered_map>
+#include <vector>
+
+namespace qc {
+
+using F = uint64_t;
+
+struct Target {
+  uint32_t v = 0xFFFFFFFFu;
+  static constexpr uint32_t VIRT = 0x80000000u;
+  static Target wire(uint32_t row, uint32_t col) { return Target{(row << 8) | col}; }
+  static Target virt(uint32_t idx) { return Target{VIRT | idx}; }
+  bool is_virtual() const { return v & VIRT; }
+  uint32_t row() const { return v >> 8; }
+  uint32_t col() const { return v & 0xFF; }
+  bool operator==(const Target &o) const { return v == o.v; }
+  bool operator!=(const Target &o) const { return v != o.v; }
+  bool operator<(const Target &o) const { return v < o.v; }
+};
+
+enum GateKind : uint8_t { G_NOOP = 0, G_CONSTANT, G_PUBLIC_INPUT, G_BASE_SUM, G_ARITHMETIC, G_POSEIDON, G_NKINDS };
+
+// plonky2 DefaultGateSerializer ids
+inline uint32_t gate_serial_id(GateKind k) {
+  switch (k) {
+    case G_NOOP: return 9;
+    case G_CONSTANT: return 3;
+    case G_PUBLIC_INPUT: return 12;
+    case G_BASE_SUM: return 2;
+    case G_ARITHMETIC: return 0;
+    case G_POSEIDON: return 11;
+    default: return 0xFFFFFFFF;
+  }
+}
+
+struct CircuitConfig {
+  uint32_t num_wires = 135, num_routed_wires = 80, num_constants = 2;
+  bool use_base_arithmetic_gate = true;
+  uint32_t security_bits = 100, num_challenges = 2;
+  bool zero_knowledge = false;
+  uint32_t max_quotient_degree_factor = 8;
+  uint32_t rate_bits = 3, cap_height = 4, pow_bits = 16, num_query_rounds = 28;
+  uint32_t arity_bits = 4, final_poly_bits = 5;  // ConstantArityBits(4, 5)
+  static CircuitConfig standard_recursion_config() { return CircuitConfig(); }
+  static CircuitConfig standard_recursion_zk_config() {
+    CircuitConfig c;
+    c.zero_knowledge = true;
+    return c;
+  }
+};
+
+struct GateInst {
+  GateKind kind;
+  F c0 = 0, c1 = 0;
+};
+
+// generator record: run by witness generation in schedule order
+enum GenKind : uint8_t { GEN_CONSTANT = 0, GEN_ARITH, GEN_POSEIDON, GEN_BASE_SPLIT, GEN_EQUALITY };
+struct Gen {
+  GenKind kind;
+  uint32_t row = 0, op = 0;             // gate row / arithmetic op index
+  Target a, b, c, d;                    // EQUALITY: x, y, equal, inv
+};
+
+// everything the prover needs about a built circuit (plonky2 ProverCircuitData
+// + CommonCircuitData), kept in host memory
+struct CircuitData {
+  CircuitConfig config;
+  uint32_t degree_bits = 0, n = 0;
+  uint32_t num_constants = 0;           // selectors + gate constants
+  uint32_t num_gate_constraints = 0, quotient_degree_factor = 0, num_partial_products = 0;
+  uint32_t num_public_inputs = 0;
+  std::vector<GateKind> gate_kinds;     // common-data gate order
+  std::vector<uint32_t> gate_params;    // parameter per gate kind (num_ops / num_limbs / num_consts)
+  std::vector<uint32_t> selector_indices;
+  std::vector<std::pair<uint32_t, uint32_t>> groups;
+  std::vector<F> k_is;
+  std::vector<uint32_t> fri_arity_bits;
+  // preprocessed polynomials, column-major values over H (natural row order)
+  std::vector<F> constants_sigmas;      // [num_constants + num_routed][n]
+  std::vector<GateInst> rows;
+  // witness layout
+  uint32_t num_slots = 0;
+  std::vector<uint32_t> wire_slot;      // [n * num_wires] row-major: slot of wire (row, col) or ~0u
+  std::vector<Gen> schedule;            // generators in dependency order
+  std::vector<uint32_t> pi_slots;       // public input slots (in order)
+  std::map<uint32_t, uint32_t> target_slot_virtual;  // virtual target -> slot
+  // commitments (filled by the prover backend at setup)
+  F constants_sigmas_cap[64 * 4] = {0};
+  F circuit_digest[4] = {0};
+  bool digest_ready = false;
+
+  uint32_t slot_of(Target t) const;
+  // plonky2 CommonCircuitData::to_bytes (util/serialization.rs)
+  std::vector<uint8_t> common_bytes() const;
+};
+
+class Witness;
+
+class CircuitBuilder {
+ public:
+  explicit CircuitBuilder(const CircuitConfig &cfg);
+
+  Target add_virtual_target();
+  std::vector<Target> add_virtual_targets(size_t n);
+  std::vector<Target> add_virtual_hash() { return add_virtual_targets(4); }
+  Target add_virtual_public_input();
+  std::vector<Target> add_virtual_hash_public_input();
+  void register_public_input(Target t) { public_inputs_.push_back(t); }
+
+  Target constant(F c);
+  Target zero() { return constant(0); }
+  Target one() { return constant(1); }
+  Target _false() { return zero(); }
+  Target _true() { return one(); }
+  Target constant_bool(bool b) { return constant(b ? 1 : 0); }
+
+  void connect(Target a, Target b);
+  void connect_hashes(const std::vector<Target> &a, const std::vector<Target> &b);
+  void assert_zero(Target t) { connect(t, zero()); }
+
+  // plonky2 gadgets/arithmetic.rs
+  Target arithmetic(F c0, F c1, Target m0, Target m1, Target addend);
+  Target add(Target x, Target y);
+  Target sub(Target x, Target y);
+  Target mul(Target x, Target y);
+  Target mul_add(Target x, Target y, Target z);
+  Target mul_sub(Target x, Target y, Target z);
+  Target mul_const(F c, Target x);
+  Target mul_const_add(F c, Target x, Target y);
+  Target _not(Target b);
+  Target _and(Target a, Target b) { return mul(a, b); }
+  Target _or(Target a, Target b);
+  Target select(Target b, Target x, Target y);
+  Target is_equal(Target x, Target y);
+
+  // gadgets/split_base.rs / range_check.rs
+  std::vector<Target> split_le(Target x, uint32_t num_bits);
+  void range_check(Target x, uint32_t n_log) { split_le(x, n_log); }
+
+  // hash/hashing.rs hash_n_to_m_no_pad (Poseidon, overwrite mode)
+  std::vector<Target> hash_n_to_hash_no_pad(const std::vector<Target> &inputs);
+
+  // targets whose values the caller sets before witness generation (fill_targets)
+  void mark_input(Target t) { inputs_.push_back(t); }
+  void mark_inputs(const std::vector<Target> &ts) { inputs_.insert(inputs_.end(), ts.begin(), ts.end()); }
+
+  size_t num_gates() const { return rows_.size(); }
+  // CircuitBuilder::build: PI hash + PublicInputGate, constant gates, padding,
+  // selectors, sigmas, generator schedule.  Throws std::runtime_error on failure.
+  CircuitData build();
+
+ private:
+  uint32_t add_gate(GateKind k, F c0 = 0, F c1 = 0);
+  bool as_const(Target t, F &v) const;
+  std::vector<Target> permute(const std::vector<Target> &state);
+
+  CircuitConfig cfg_;
+  std::vector<GateInst> rows_;
+  uint32_t nvirt_ = 0;
+  std::vector<std::pair<Target, Target>> copies_;
+  std::vector<Gen> gens_;
+  std::vector<Target> public_inputs_;
+  std::vector<Target> inputs_;
+  std::unordered_map<F, Target> const_to_target_;
+  std::unordered_map<uint32_t, F> target_to_const_;
+  std::map<std::pair<F, F>, std::pair<uint32_t, uint32_t>> arith_open_;  // (c0,c1) -> (row, next op)
+  std::map<std::tuple<F, F, uint32_t, uint32_t, uint32_t>, Target> arith_cache_;
+  uint32_t arith_ops_, base_sum_limbs_;
+};
+
+// Per-proof witness: values per partition slot.
+class Witness {
+ public:
+  explicit Witness(const CircuitData &cd);
+  // PartialWitness::set_target; returns false on "set twice with different values"
+  bool set(Target t, F v);
+  bool set_slot(uint32_t s, F v);
+  bool get_slot(uint32_t s, F &v) const {
+    v = val_[s];
+    return known_[s];
+  }
+  // run the generator schedule; returns false (and a message) on conflict / missing input
+  bool generate(std::string &err);
+  // full wire matrix, column-major [num_wires][n]
+  void wires_matrix(F *out) const;
+  std::vector<F> public_inputs() const;
+
+ private:
+  bool set_wire(uint32_t row, uint32_t col, F v);
+  F wire(uint32_t row, uint32_t col) const;
+  const CircuitData &cd_;
+  std::vector<F> val_;
+  std::vector<uint8_t> known_;
+  std::vector<F> nonrouted_;  // values of wires that are not in any slot
+  bool conflict_ = false;
+};
+
+}  // namespace qc

@@ -1,0 +1,125 @@
+// circuit_api.cpp — C ABI (include/qpgpu.h) for circuits and witnesses.
+// Host only: builds the native circuit and generates witnesses; the device
+// side of a circuit (constants/sigmas commitment) lives in prover.cpp.
+#include <string.h>
+#include <exception>
+#include <memory>
+#include <new>
+#include "../../include/qpgpu.h"
+#include "circuit_obj.h"
+
+extern "C" {
+
+int qp_wormhole_circuit_new(int zk, qp_circuit **out) {
+  if (!out) return QP_ERR_ARG;
+  *out = nullptr;
+  try {
+    auto c = std::make_unique<qp_circuit>();
+    c->kind = qp_circuit::WORMHOLE;
+    qc::CircuitBuilder b(zk ? qc::CircuitConfig::standard_recursion_zk_config()
+                            : qc::CircuitConfig::standard_recursion_config());
+    c->wormhole = qw::build_wormhole(b);
+    c->gates_used = (uint32_t)b.num_gates();
+    c->cd = b.build();
+    *out = c.release();
+    return QP_OK;
+  } catch (const std::bad_alloc &) {
+    return QP_ERR_OOM;
+  } catch (const std::exception &) {
+    return QP_ERR_STATE;
+  }
+}
+
+void qp_circuit_free(qp_circuit *c) { delete c; }
+
+int qp_circuit_info(const qp_circuit *c, uint32_t *info) {
+  if (!c || !info) return QP_ERR_ARG;
+  info[0] = c->cd.degree_bits;
+  info[1] = c->cd.config.num_wires;
+  info[2] = c->cd.config.num_routed_wires;
+  info[3] = c->cd.num_constants;
+  info[4] = c->cd.num_public_inputs;
+  info[5] = c->gates_used;
+  info[6] = c->cd.num_gate_constraints;
+  return QP_OK;
+}
+
+int qp_circuit_common_data(const qp_circuit *c, uint8_t *out, size_t cap, size_t *len) {
+  if (!c) return QP_ERR_ARG;
+  auto b = c->cd.common_bytes();
+  if (len) *len = b.size();
+  if (out) {
+    if (cap < b.size()) return QP_ERR_ARG;
+    memcpy(out, b.data(), b.size());
+  }
+  return QP_OK;
+}
+
+int qp_circuit_constants_sigmas(const qp_circuit *c, uint64_t *out) {
+  if (!c || !out) return QP_ERR_ARG;
+  memcpy(out, c->cd.constants_sigmas.data(), c->cd.constants_sigmas.size() * 8);
+  return QP_OK;
+}
+
+static void put_err(char *err, size_t cap, const std::string &m) {
+  if (err && cap) {
+    size_t k = m.size() < cap - 1 ? m.size() : cap - 1;
+    memcpy(err, m.data(), k);
+    err[k] = 0;
+  }
+}
+
+int qp_wormhole_commit(const qp_circuit *c, const qp_wormhole_inputs *in, qp_witness **out, char *err, size_t errcap) {
+  if (!c || !in || !out || c->kind != qp_circuit::WORMHOLE) return QP_ERR_ARG;
+  *out = nullptr;
+  if (in->num_nodes && (!in->nodes || !in->node_lens || !in->indices)) return QP_ERR_ARG;
+  try {
+    qw::CircuitInputs ci;
+    memcpy(&ci.funding_amount_lo, in->funding_amount, 8);
+    memcpy(&ci.funding_amount_hi, in->funding_amount + 8, 8);
+    memcpy(ci.nullifier, in->nullifier, 32);
+    memcpy(ci.root_hash, in->root_hash, 32);
+    memcpy(ci.exit_account, in->exit_account, 32);
+    memcpy(ci.secret, in->secret, 32);
+    ci.transfer_count = in->transfer_count;
+    memcpy(ci.funding_account, in->funding_account, 32);
+    memcpy(ci.unspendable_account, in->unspendable_account, 32);
+    for (uint32_t i = 0; i < in->num_nodes; i++) {
+      ci.storage_proof.emplace_back(in->nodes[i], in->nodes[i] + in->node_lens[i]);
+      ci.storage_indices.push_back(in->indices[i]);
+    }
+    auto w = std::make_unique<qp_witness>(c);
+    std::string e = qw::commit(c->wormhole, ci, w->w);
+    if (e.empty() && !w->w.generate(e)) {
+    }
+    if (!e.empty()) {
+      put_err(err, errcap, e);
+      return e.find("set twice") != std::string::npos ? QP_ERR_WITNESS : QP_ERR_ARG;
+    }
+    *out = w.release();
+    return QP_OK;
+  } catch (const std::bad_alloc &) {
+    return QP_ERR_OOM;
+  }
+}
+
+int qp_witness_wires(const qp_witness *w, uint64_t *out) {
+  if (!w || !out) return QP_ERR_ARG;
+  w->w.wires_matrix(out);
+  return QP_OK;
+}
+
+int qp_witness_public_inputs(const qp_witness *w, uint64_t *out, uint32_t cap, uint32_t *n) {
+  if (!w) return QP_ERR_ARG;
+  auto pi = w->w.public_inputs();
+  if (n) *n = (uint32_t)pi.size();
+  if (out) {
+    if (cap < pi.size()) return QP_ERR_ARG;
+    memcpy(out, pi.data(), pi.size() * 8);
+  }
+  return QP_OK;
+}
+
+void qp_witness_free(qp_witness *w) { delete w; }
+
+}  // extern "C"

@@ -1,0 +1,18 @@
+// circuit_obj.h — definitions behind qp_circuit / qp_witness handles.
+#pragma once
+#include <stdint.h>
+#include "circuit.h"
+#include "wormhole.h"
+
+struct qp_circuit {
+  enum Kind { WORMHOLE = 1, VOTING = 2 } kind = WORMHOLE;
+  qc::CircuitData cd;
+  qw::WormholeTargets wormhole;
+  uint32_t gates_used = 0;
+};
+
+struct qp_witness {
+  explicit qp_witness(const qp_circuit *c) : circuit(c), w(c->cd) {}
+  const qp_circuit *circuit;
+  qc::Witness w;
+};

@@ -65,6 +65,16 @@ def lib():
         "qp_lde": (ctypes.c_int, [VP, U64P, ctypes.c_uint32, ctypes.c_uint32, ctypes.c_uint32, ctypes.c_uint64,
                                   U64P]),
         "qp_poseidon_permute": (ctypes.c_int, [VP, U64P, ctypes.c_uint64]),
+        "qp_wormhole_circuit_new": (ctypes.c_int, [ctypes.c_int, PP]),
+        "qp_circuit_free": (None, [VP]),
+        "qp_circuit_info": (ctypes.c_int, [VP, ctypes.POINTER(ctypes.c_uint32)]),
+        "qp_circuit_common_data": (ctypes.c_int, [VP, ctypes.c_char_p, ctypes.c_size_t,
+                                                  ctypes.POINTER(ctypes.c_size_t)]),
+        "qp_circuit_constants_sigmas": (ctypes.c_int, [VP, U64P]),
+        "qp_wormhole_commit": (ctypes.c_int, [VP, VP, PP, ctypes.c_char_p, ctypes.c_size_t]),
+        "qp_witness_wires": (ctypes.c_int, [VP, U64P]),
+        "qp_witness_public_inputs": (ctypes.c_int, [VP, U64P, ctypes.c_uint32, ctypes.POINTER(ctypes.c_uint32)]),
+        "qp_witness_free": (None, [VP]),
     }
     for name, (res, args) in sig.items():
         f = getattr(L, name)

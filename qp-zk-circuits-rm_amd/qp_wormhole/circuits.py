@@ -1,0 +1,161 @@
+"""Host-side mirror of the reference's circuit / prover input types.
+
+CircuitInputs mirrors wormhole/circuit/src/inputs.rs:21-52 (public +
+private inputs); WormholeCircuit builds the native circuit
+(wormhole/circuit/src/circuit.rs:63-109) through the C ABI; Witness is the
+result of WormholeProver::commit (wormhole/prover/src/lib.rs:209-225).
+"""
+import ctypes
+from dataclasses import dataclass, field
+from typing import List
+
+import numpy as np
+
+from ._native import QpError, lib
+
+U8_32 = ctypes.c_uint8 * 32
+
+
+class _Inputs(ctypes.Structure):
+    _fields_ = [("funding_amount", ctypes.c_uint8 * 16), ("nullifier", U8_32), ("root_hash", U8_32),
+                ("exit_account", U8_32), ("secret", U8_32), ("transfer_count", ctypes.c_uint64),
+                ("funding_account", U8_32), ("unspendable_account", U8_32), ("num_nodes", ctypes.c_uint32),
+                ("nodes", ctypes.POINTER(ctypes.c_char_p)), ("node_lens", ctypes.POINTER(ctypes.c_uint32)),
+                ("indices", ctypes.POINTER(ctypes.c_uint64))]
+
+
+@dataclass
+class ProcessedStorageProof:
+    """storage_proof/mod.rs:58-76: node byte strings + hex-char child-hash indices."""
+    proof: List[bytes] = field(default_factory=list)
+    indices: List[int] = field(default_factory=list)
+
+
+@dataclass
+class PublicCircuitInputs:
+    funding_amount: int
+    nullifier: bytes
+    root_hash: bytes
+    exit_account: bytes
+
+
+@dataclass
+class PrivateCircuitInputs:
+    secret: bytes
+    storage_proof: ProcessedStorageProof
+    transfer_count: int
+    funding_account: bytes
+    unspendable_account: bytes
+
+
+@dataclass
+class CircuitInputs:
+    public: PublicCircuitInputs
+    private: PrivateCircuitInputs
+
+    def to_c(self):
+        s = _Inputs()
+        s.funding_amount[:] = list(int(self.public.funding_amount).to_bytes(16, "little"))
+        s.nullifier[:] = list(self.public.nullifier)
+        s.root_hash[:] = list(self.public.root_hash)
+        s.exit_account[:] = list(self.public.exit_account)
+        s.secret[:] = list(self.private.secret)
+        s.transfer_count = self.private.transfer_count
+        s.funding_account[:] = list(self.private.funding_account)
+        s.unspendable_account[:] = list(self.private.unspendable_account)
+        sp = self.private.storage_proof
+        n = len(sp.proof)
+        s.num_nodes = n
+        keep = [bytes(p) for p in sp.proof]
+        s.nodes = (ctypes.c_char_p * max(n, 1))(*keep) if n else None
+        s.node_lens = (ctypes.c_uint32 * max(n, 1))(*[len(p) for p in keep]) if n else None
+        s.indices = (ctypes.c_uint64 * max(len(sp.indices), 1))(*sp.indices) if n else None
+        s._keep = keep
+        return s
+
+
+class Witness:
+    def __init__(self, circuit, handle):
+        self.circuit, self.h = circuit, handle
+
+    def wires(self):
+        out = np.zeros((self.circuit.num_wires, self.circuit.n), np.uint64)
+        rc = lib().qp_witness_wires(self.h, out)
+        if rc:
+            raise QpError(rc, "qp_witness_wires")
+        return out
+
+    def public_inputs(self):
+        out = np.zeros(256, np.uint64)
+        n = ctypes.c_uint32()
+        rc = lib().qp_witness_public_inputs(self.h, out, 256, ctypes.byref(n))
+        if rc:
+            raise QpError(rc, "qp_witness_public_inputs")
+        return out[:n.value].copy()
+
+    def free(self):
+        if self.h:
+            lib().qp_witness_free(self.h)
+            self.h = None
+
+    def __del__(self):
+        try:
+            self.free()
+        except Exception:
+            pass
+
+
+class Circuit:
+    """A built circuit (plonky2 ProverCircuitData + CommonCircuitData)."""
+
+    def __init__(self, handle, kind):
+        self.h, self.kind = handle, kind
+        info = (ctypes.c_uint32 * 8)()
+        lib().qp_circuit_info(self.h, info)
+        (self.degree_bits, self.num_wires, self.num_routed_wires, self.num_constants, self.num_public_inputs,
+         self.gates_used, self.num_gate_constraints) = list(info)[:7]
+        self.n = 1 << self.degree_bits
+
+    @classmethod
+    def wormhole(cls, zero_knowledge=False):
+        h = ctypes.c_void_p()
+        rc = lib().qp_wormhole_circuit_new(int(zero_knowledge), ctypes.byref(h))
+        if rc:
+            raise QpError(rc, "qp_wormhole_circuit_new")
+        return cls(h, "wormhole")
+
+    def common_data(self):
+        ln = ctypes.c_size_t()
+        lib().qp_circuit_common_data(self.h, None, 0, ctypes.byref(ln))
+        buf = ctypes.create_string_buffer(ln.value)
+        rc = lib().qp_circuit_common_data(self.h, buf, ln.value, ctypes.byref(ln))
+        if rc:
+            raise QpError(rc, "qp_circuit_common_data")
+        return buf.raw[:ln.value]
+
+    def constants_sigmas(self):
+        out = np.zeros((self.num_constants + self.num_routed_wires, self.n), np.uint64)
+        rc = lib().qp_circuit_constants_sigmas(self.h, out)
+        if rc:
+            raise QpError(rc, "qp_circuit_constants_sigmas")
+        return out
+
+    def commit(self, inputs: CircuitInputs) -> Witness:
+        s = inputs.to_c()
+        h = ctypes.c_void_p()
+        err = ctypes.create_string_buffer(512)
+        rc = lib().qp_wormhole_commit(self.h, ctypes.byref(s), ctypes.byref(h), err, 512)
+        if rc:
+            raise QpError(rc, err.value.decode())
+        return Witness(self, h)
+
+    def free(self):
+        if self.h:
+            lib().qp_circuit_free(self.h)
+            self.h = None
+
+    def __del__(self):
+        try:
+            self.free()
+        except Exception:
+            pass
