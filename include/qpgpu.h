@@ -95,6 +95,9 @@ int qp_lde(qp_ctx *ctx, const uint64_t *coeffs, uint32_t ncols, uint32_t log_n, 
            uint64_t *out);
 /* Poseidon permutation of n 12-element states, in place                   */
 int qp_poseidon_permute(qp_ctx *ctx, uint64_t *states, uint64_t n);
+/* PoseidonHash::hash_no_pad on the host (no device): used to build circuit
+ * inputs (nullifier, unspendable account, storage-proof roots)            */
+int qp_hash_no_pad(const uint64_t *in, size_t n, uint64_t *out4);
 
 
 /* ---- circuits and witnesses (host; no device needed) ---------------------
@@ -139,6 +142,32 @@ int qp_wormhole_commit(const qp_circuit *c, const qp_wormhole_inputs *in, qp_wit
 int qp_witness_wires(const qp_witness *w, uint64_t *out);
 int qp_witness_public_inputs(const qp_witness *w, uint64_t *out, uint32_t cap, uint32_t *n);
 void qp_witness_free(qp_witness *w);
+
+/* ---- prover (device) -------------------------------------------------------
+ * plonky2 prove() (plonk/prover.rs) for B proofs of one circuit at a time,
+ * replacing ProverCircuitData::prove as called by WormholeProver::prove
+ * (wormhole/prover/src/lib.rs:233-237) and by the aggregator
+ * (wormhole/aggregator/src/circuits/tree.rs:136).  qp_prover_new runs the
+ * circuit's device preprocessing (constants/sigmas LDE + Merkle cap, circuit
+ * digest: CircuitBuilder::build) and sizes the workspace for max_batch proofs.
+ * Proof bytes follow ProofWithPublicInputs::to_bytes; the PoW witness is the
+ * minimal one, so proofs are a deterministic function of the witness.      */
+typedef struct qp_prover qp_prover;
+int qp_prover_new(qp_ctx *ctx, const qp_circuit *c, uint32_t max_batch, qp_prover **out);
+void qp_prover_free(qp_prover *p);
+int qp_prover_proof_size(const qp_prover *p, size_t *len);
+/* VerifierOnlyCircuitData || CommonCircuitData bytes (cap height, constants/sigmas
+ * cap, circuit digest, common data) — the wormhole/bench-data/verifier.bin layout */
+int qp_prover_verifier_data(const qp_prover *p, uint8_t *out, size_t cap, size_t *len);
+/* prove from witnesses made by qp_wormhole_commit; proof b at out + b*stride */
+int qp_prover_prove(qp_prover *p, const qp_witness *const *w, uint32_t nproofs, uint8_t *out, size_t stride,
+                    size_t *lens);
+/* prove from raw wire matrices [nproofs][num_wires][n] + public inputs [nproofs][npis] */
+int qp_prover_prove_wires(qp_prover *p, const uint64_t *wires, const uint64_t *pis, uint32_t nproofs, uint8_t *out,
+                          size_t stride, size_t *lens);
+/* accumulated host wall time per stage (ms): commit wires, zs, quotient, openings,
+ * FRI, PoW, queries, serialize; reset != 0 clears */
+int qp_prover_stage_times(qp_prover *p, double *ms, uint32_t n, int reset);
 
 #ifdef __cplusplus
 }

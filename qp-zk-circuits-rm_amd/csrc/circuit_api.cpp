@@ -7,6 +7,7 @@
 #include <new>
 #include "../../include/qpgpu.h"
 #include "circuit_obj.h"
+#include "host_util.h"
 
 extern "C" {
 
@@ -121,5 +122,13 @@ int qp_witness_public_inputs(const qp_witness *w, uint64_t *out, uint32_t cap, u
 }
 
 void qp_witness_free(qp_witness *w) { delete w; }
+
+int qp_hash_no_pad(const uint64_t *in, size_t n, uint64_t *out4) {
+  if ((!in && n) || !out4) return QP_ERR_ARG;
+  std::vector<uint64_t> v(in, in + n);
+  for (auto &x : v) x = gl::canon(x);
+  qh::hash_no_pad(v.data(), n, out4);
+  return QP_OK;
+}
 
 }  // extern "C"

@@ -11,6 +11,7 @@
 //   * ifft is a DIF with inverse twiddles and a bit-reversed LDS read on store.
 #include "field.h"
 #include "kernels.h"
+#include "ntt_device.h"
 
 namespace qpk {
 
@@ -37,23 +38,6 @@ void twiddles_free(Twiddles &t) {
   if (t.fwd) (void)hipFree(t.fwd);
   if (t.inv) (void)hipFree(t.inv);
   t.fwd = t.inv = nullptr;
-}
-
-// DIF over LDS a[0..2^log_n): after it, a[p] = sum_k x_k w^{rev(p) k}
-__device__ void dif_lds(uint64_t *a, uint32_t log_n, const uint64_t *__restrict__ tw) {
-  const uint32_t half_n = 1u << (log_n - 1);
-  for (int s = (int)log_n - 1; s >= 0; s--) {
-    const uint32_t h = 1u << s;
-    const uint32_t tsh = TW_LOG - 1 - s;
-    for (uint32_t b = threadIdx.x; b < half_n; b += blockDim.x) {
-      uint32_t j = b & (h - 1);
-      uint32_t k = ((b >> s) << (s + 1)) + j;
-      uint64_t u = a[k], v = a[k + h];
-      a[k] = gl::add(u, v);
-      a[k + h] = gl::mul(gl::sub(u, v), tw[j << tsh]);
-    }
-    __syncthreads();
-  }
 }
 
 __global__ void __launch_bounds__(512) k_intt(const uint64_t *__restrict__ in, uint64_t in_stride,

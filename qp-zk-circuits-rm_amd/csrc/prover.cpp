@@ -1,0 +1,777 @@
+// prover.cpp — batched Plonky2 prove() on one MI355X (plonky2 plonk/prover.rs
+// `prove` + fri/oracle.rs `prove_openings` + fri/prover.rs `fri_proof`,
+// SURVEY.md 3.2), called from WormholeProver::prove
+// (wormhole/prover/src/lib.rs:233-237) and the aggregator's
+// CircuitData::prove (wormhole/aggregator/src/circuits/tree.rs:136).
+//
+// B proofs of one circuit move through every stage together: each stage is
+// one batched kernel launch (blockIdx.y/z = proof), so a 256-proof batch
+// fills the chip even where one proof alone would not.  The matrices stay
+// resident in HBM between stages; only caps, openings, the final polynomial
+// and the query openings cross PCIe.  The transcript (Challenger) runs on the
+// host, per proof, on a thread pool, between stages.
+#include <string.h>
+#include <algorithm>
+#include <chrono>
+#include <memory>
+#include <new>
+#include <stdexcept>
+#include <vector>
+#include "../../include/qpgpu.h"
+#include "circuit_obj.h"
+#include "ctx.h"
+#include "field.h"
+#include "host_util.h"
+#include "kernels.h"
+#include "prover_kernels.h"
+
+namespace {
+
+using gl::ext;
+
+struct DevBuf {
+  uint64_t *p = nullptr;
+  size_t words = 0;
+  hipError_t alloc(size_t w) {
+    words = w;
+    return hipMalloc(&p, (w ? w : 1) * 8);
+  }
+  ~DevBuf() {
+    if (p) (void)hipFree(p);
+  }
+};
+
+struct Tree {  // one Merkle-committed matrix per proof
+  uint32_t npolys = 0, log_n = 0, rate_bits = 0, cap_h = 0;
+  DevBuf vals, coeffs, lde, dig;
+  uint64_t n() const { return 1ull << log_n; }
+  uint64_t N() const { return 1ull << (log_n + rate_bits); }
+  uint64_t ndig() const { return qpk::tree_digest_count(log_n + rate_bits, cap_h); }
+  uint64_t cbs() const { return (uint64_t)npolys * n(); }
+  uint64_t lbs() const { return (uint64_t)npolys * N(); }
+  uint64_t dbs() const { return ndig() * 4; }
+  hipError_t alloc(uint32_t np, uint32_t ln, uint32_t rb, uint32_t ch, uint32_t b, bool with_vals) {
+    npolys = np; log_n = ln; rate_bits = rb; cap_h = ch;
+    hipError_t e = with_vals ? vals.alloc((size_t)b * cbs()) : hipSuccess;
+    if (!e) e = coeffs.alloc((size_t)b * cbs());
+    if (!e) e = lde.alloc((size_t)b * lbs());
+    if (!e) e = dig.alloc((size_t)b * dbs());
+    return e;
+  }
+  // coefficients in `coeffs`: LDE + leaves + tree
+  void build(qp_ctx *c, uint32_t nbat) {
+    qpk::lde(c->tw, coeffs.p, n(), lde.p, N(), npolys, log_n, rate_bits, gl::GEN, nbat, cbs(), lbs(), c->stream);
+    qpk::leaf_hash(lde.p, N(), npolys, nullptr, 0, dig.p, (uint32_t)N(), nbat, lbs(), 0, dbs(), c->stream);
+    qpk::merkle_tree(dig.p, log_n + rate_bits, cap_h, nbat, dbs(), c->stream);
+  }
+  // values in `vals` ([nb][npolys][n]): ifft then build
+  void build_from_values(qp_ctx *c, uint32_t nbat) {
+    qpk::intt(c->tw, vals.p, n(), coeffs.p, n(), npolys, log_n, nbat, cbs(), cbs(), c->stream);
+    build(c, nbat);
+  }
+};
+
+inline unsigned cdiv(uint64_t a, unsigned b) { return (unsigned)((a + b - 1) / b); }
+
+}  // namespace
+
+struct qp_prover {
+  qp_ctx *ctx = nullptr;
+  const qp_circuit *circuit = nullptr;
+  uint32_t max_batch = 0;
+  uint32_t log_n = 0, rate_bits = 0, cap_h = 0, W = 0, R = 0, NC = 0, nc = 0, npp = 0, qdf = 0, nchunks = 0;
+  uint32_t nq = 0, pow_bits = 0, npis = 0;
+  std::vector<uint32_t> arity;
+  uint32_t final_len = 0;
+  uint64_t cs_cap[64 * 4] = {0};
+  uint64_t digest[4] = {0};
+  qpk::GateDesc gdesc;
+  std::vector<uint8_t> common;
+  Tree cs;
+  DevBuf sigmas, kis;
+  Tree wires, zs, quot;
+  DevBuf chal, prods, qvals, cbuf, openings, comp, fin, pow_state, pow_found, pow_pos, qidx, qout;
+  std::vector<DevBuf> fvals, fdig, fcoef;
+  size_t qout_words = 0;
+  std::unique_ptr<qh::ThreadPool> pool;
+  std::vector<uint64_t> h_chal, h_caps, h_open, h_final, h_qout, h_powst, h_found;
+  std::vector<uint32_t> h_qidx, h_pos;
+  size_t proof_len = 0;
+  double stage_ms[16] = {0};
+};
+
+namespace {
+
+#define TRY(expr)                                                              \
+  do {                                                                         \
+    hipError_t _e = (expr);                                                    \
+    if (_e != hipSuccess) {                                                    \
+      P->ctx->err = std::string(#expr) + ": " + hipGetErrorString(_e);         \
+      return _e == hipErrorOutOfMemory ? QP_ERR_OOM : QP_ERR_HIP;              \
+    }                                                                          \
+  } while (0)
+
+uint32_t oracle_width(const qp_prover *p, int o) {
+  switch (o) {
+    case 0: return p->NC + p->R;
+    case 1: return p->W;
+    case 2: return p->nc * p->nchunks;
+    default: return p->nc * p->qdf;
+  }
+}
+
+size_t proof_size(const qp_prover *p) {
+  const size_t caps = ((size_t)4 << p->cap_h) * 8;
+  size_t s = 3 * caps;
+  s += (size_t)(p->NC + p->R + p->W + p->nc * p->nchunks + p->nc * p->qdf + p->nc) * 16;
+  s += p->arity.size() * caps;
+  const uint32_t logN = p->log_n + p->rate_bits;
+  size_t q = 0;
+  for (int o = 0; o < 4; o++) q += oracle_width(p, o) * 8 + 1 + (size_t)(logN - p->cap_h) * 32;
+  uint32_t lg = logN;
+  for (uint32_t ab : p->arity) {
+    lg -= ab;
+    q += (16ull << ab) + 1 + (size_t)(lg - p->cap_h) * 32;
+  }
+  s += q * p->nq;
+  s += (size_t)p->final_len * 16 + 8 + 8 + (size_t)p->npis * 8;
+  return s;
+}
+
+int setup(qp_prover *P) {
+  qp_ctx *c = P->ctx;
+  const qc::CircuitData &cd = P->circuit->cd;
+  P->log_n = cd.degree_bits;
+  P->rate_bits = cd.config.rate_bits;
+  P->cap_h = cd.config.cap_height;
+  P->W = cd.config.num_wires;
+  P->R = cd.config.num_routed_wires;
+  P->NC = cd.num_constants;
+  P->nc = cd.config.num_challenges;
+  P->npp = cd.num_partial_products;
+  P->qdf = cd.quotient_degree_factor;
+  P->nchunks = P->npp + 1;
+  P->nq = cd.config.num_query_rounds;
+  P->pow_bits = cd.config.pow_bits;
+  P->npis = cd.num_public_inputs;
+  P->arity = cd.fri_arity_bits;
+  uint32_t tot = 0;
+  for (auto a : P->arity) tot += a;
+  P->final_len = 1u << (P->log_n - tot);
+  P->common = cd.common_bytes();
+  if (P->nc != 2 || cd.config.zero_knowledge || (1u << P->rate_bits) != P->qdf || P->log_n > 14 ||
+      P->log_n < 10 || P->nchunks > 16 || P->NC > 8 || P->arity.size() > 8 || P->nq > 64) {
+    c->err = "unsupported circuit shape for the GPU prover (need 2 challenges, non-zk, qdf = blowup, 2^10 <= n <= 2^14)";
+    return QP_ERR_ARG;
+  }
+  qpk::GateDesc &g = P->gdesc;
+  g.ngates = (uint32_t)cd.gate_kinds.size();
+  g.nsel = (uint32_t)cd.groups.size();
+  for (uint32_t i = 0; i < g.ngates; i++) {
+    switch (cd.gate_kinds[i]) {
+      case qc::G_NOOP: g.kind[i] = qpk::GK_NOOP; break;
+      case qc::G_CONSTANT: g.kind[i] = qpk::GK_CONSTANT; break;
+      case qc::G_PUBLIC_INPUT: g.kind[i] = qpk::GK_PUBLIC_INPUT; break;
+      case qc::G_BASE_SUM: g.kind[i] = qpk::GK_BASE_SUM; break;
+      case qc::G_ARITHMETIC: g.kind[i] = qpk::GK_ARITHMETIC; break;
+      case qc::G_POSEIDON: g.kind[i] = qpk::GK_POSEIDON; break;
+      default: break;
+    }
+    g.param[i] = cd.gate_params[i];
+    g.sel_index[i] = cd.selector_indices[i];
+  }
+  for (uint32_t s = 0; s < g.nsel; s++) {
+    g.grp_lo[s] = cd.groups[s].first;
+    g.grp_hi[s] = cd.groups[s].second;
+  }
+  const uint64_t n = 1ull << P->log_n;
+  const uint64_t N = n << P->rate_bits;
+  TRY(hipSetDevice(c->device));
+  // constants || sigmas commitment (CircuitBuilder::build preprocessing) + circuit digest
+  TRY(P->cs.alloc(P->NC + P->R, P->log_n, P->rate_bits, P->cap_h, 1, true));
+  TRY(hipMemcpyAsync(P->cs.vals.p, cd.constants_sigmas.data(), cd.constants_sigmas.size() * 8, hipMemcpyHostToDevice,
+                     c->stream));
+  P->cs.build_from_values(c, 1);
+  TRY(hipGetLastError());
+  TRY(P->sigmas.alloc((size_t)P->R * n));
+  TRY(hipMemcpyAsync(P->sigmas.p, cd.constants_sigmas.data() + (size_t)P->NC * n, (size_t)P->R * n * 8,
+                     hipMemcpyHostToDevice, c->stream));
+  TRY(P->kis.alloc(P->R));
+  TRY(hipMemcpyAsync(P->kis.p, cd.k_is.data(), P->R * 8ull, hipMemcpyHostToDevice, c->stream));
+  const uint32_t logN = P->log_n + P->rate_bits;
+  TRY(hipMemcpyAsync(P->cs_cap, P->cs.dig.p + qpk::tree_level_offset(logN, logN - P->cap_h) * 4,
+                     (size_t)32 << P->cap_h, hipMemcpyDeviceToHost, c->stream));
+  TRY(hipStreamSynchronize(c->stream));
+  {
+    std::vector<uint64_t> buf(P->cs_cap, P->cs_cap + (4u << P->cap_h));
+    uint64_t dsep[4];
+    qh::hash_pad(nullptr, 0, dsep);
+    buf.insert(buf.end(), dsep, dsep + 4);
+    buf.push_back(P->log_n);
+    qh::hash_no_pad(buf.data(), buf.size(), P->digest);
+  }
+  const uint32_t B = P->max_batch;
+  TRY(P->wires.alloc(P->W, P->log_n, P->rate_bits, P->cap_h, B, true));
+  TRY(P->zs.alloc(P->nc * P->nchunks, P->log_n, P->rate_bits, P->cap_h, B, true));
+  TRY(P->quot.alloc(P->nc * P->qdf, P->log_n, P->rate_bits, P->cap_h, B, false));
+  TRY(P->chal.alloc((size_t)B * qpk::CHAL_STRIDE));
+  TRY(P->prods.alloc((size_t)B * P->nc * P->nchunks * n));
+  TRY(P->qvals.alloc((size_t)B * P->nc * N));
+  TRY(P->cbuf.alloc((size_t)B * P->nc * N));
+  TRY(P->openings.alloc((size_t)B * qpk::OPEN_STRIDE));
+  TRY(P->comp.alloc((size_t)B * 4 * n));
+  TRY(P->fin.alloc((size_t)B * 2 * N));
+  TRY(hipMemsetAsync(P->fin.p, 0, (size_t)B * 2 * N * 8, c->stream));
+  P->fvals.resize(P->arity.size());
+  P->fdig.resize(P->arity.size());
+  P->fcoef.resize(P->arity.size());
+  uint32_t lg = logN;
+  for (size_t l = 0; l < P->arity.size(); l++) {
+    TRY(P->fvals[l].alloc(((size_t)B * 2) << lg));
+    TRY(P->fdig[l].alloc((size_t)B * qpk::tree_digest_count(lg - P->arity[l], P->cap_h) * 4));
+    lg -= P->arity[l];
+    TRY(P->fcoef[l].alloc(((size_t)B * 2) << lg));
+  }
+  TRY(P->pow_state.alloc((size_t)B * 12));
+  TRY(P->pow_found.alloc(B));
+  TRY(P->pow_pos.alloc((B + 1) / 2));
+  TRY(P->qidx.alloc(((size_t)B * P->nq + 1) / 2));
+  {
+    size_t w = 0;
+    for (int o = 0; o < 4; o++) w += (size_t)P->nq * (oracle_width(P, o) + (logN - P->cap_h) * 4);
+    uint32_t lg2 = logN;
+    for (uint32_t ab : P->arity) {
+      lg2 -= ab;
+      w += (size_t)P->nq * ((2u << ab) + (lg2 - P->cap_h) * 4);
+    }
+    P->qout_words = w;
+    TRY(P->qout.alloc((size_t)B * w));
+  }
+  P->h_chal.assign((size_t)B * qpk::CHAL_STRIDE, 0);
+  P->h_caps.assign((size_t)B * (4u << P->cap_h), 0);
+  P->h_open.assign((size_t)B * qpk::OPEN_STRIDE, 0);
+  P->h_final.assign((size_t)B * 2 * P->final_len, 0);
+  P->h_qout.assign((size_t)B * P->qout_words, 0);
+  P->h_qidx.assign((size_t)B * P->nq, 0);
+  P->h_pos.assign(B, 0);
+  P->h_powst.assign((size_t)B * 12, 0);
+  P->h_found.assign(B, 0);
+  TRY(hipStreamSynchronize(c->stream));
+  P->proof_len = proof_size(P);
+  unsigned hw = std::thread::hardware_concurrency();
+  unsigned nthreads = std::min<unsigned>(hw ? hw : 4, 16);
+  P->pool.reset(new qh::ThreadPool(nthreads > 1 ? nthreads - 1 : 0));
+  return QP_OK;
+}
+
+int fetch_caps(qp_prover *P, const uint64_t *dig_base, uint64_t dbs, uint32_t log_leaves, uint32_t nb) {
+  qp_ctx *c = P->ctx;
+  const uint64_t off = qpk::tree_level_offset(log_leaves, log_leaves - P->cap_h) * 4;
+  const size_t cw = 4u << P->cap_h;
+  TRY(hipMemcpy2DAsync(P->h_caps.data(), cw * 8, dig_base + off, dbs * 8, cw * 8, nb, hipMemcpyDeviceToHost,
+                       c->stream));
+  TRY(hipStreamSynchronize(c->stream));
+  return QP_OK;
+}
+
+int push_chal(qp_prover *P, uint32_t nb) {
+  TRY(hipMemcpyAsync(P->chal.p, P->h_chal.data(), (size_t)nb * qpk::CHAL_STRIDE * 8, hipMemcpyHostToDevice,
+                     P->ctx->stream));
+  return QP_OK;
+}
+
+struct ProofState {
+  qh::Challenger t;
+  uint64_t pih[4];
+  std::vector<uint64_t> caps[3];
+  std::vector<uint64_t> fri_caps;
+  uint64_t pow_witness = 0;
+};
+
+using Clock = std::chrono::steady_clock;
+
+int prove_batch(qp_prover *P, const uint64_t *const *wires_host, const uint64_t *const *pis_host, uint32_t nb,
+                uint8_t *out, size_t stride, size_t *lens) {
+  qp_ctx *c = P->ctx;
+  hipStream_t s = c->stream;
+  const uint64_t n = 1ull << P->log_n;
+  const uint32_t logN = P->log_n + P->rate_bits;
+  const uint64_t N = 1ull << logN;
+  const size_t capw = 4u << P->cap_h;
+  const uint32_t nc = P->nc;
+  std::vector<ProofState> st(nb);
+  auto T0 = Clock::now();
+  auto lap = [&](int k) {
+    auto t = Clock::now();
+    P->stage_ms[k] += std::chrono::duration<double, std::milli>(t - T0).count();
+    T0 = t;
+  };
+  TRY(hipSetDevice(c->device));
+  int rc;
+
+  // ---- 1. wires commitment
+  for (uint32_t b = 0; b < nb; b++)
+    TRY(hipMemcpyAsync(P->wires.vals.p + b * P->wires.cbs(), wires_host[b], P->wires.cbs() * 8, hipMemcpyHostToDevice, s));
+  P->wires.build_from_values(c, nb);
+  TRY(hipGetLastError());
+  if ((rc = fetch_caps(P, P->wires.dig.p, P->wires.dbs(), logN, nb))) return rc;
+  P->pool->parallel_for(nb, [&](size_t b) {
+    ProofState &S = st[b];
+    qh::hash_no_pad(pis_host[b], P->npis, S.pih);
+    S.caps[0].assign(P->h_caps.begin() + b * capw, P->h_caps.begin() + (b + 1) * capw);
+    S.t.observe(P->digest, 4);
+    S.t.observe(S.pih, 4);
+    S.t.observe(S.caps[0].data(), capw);
+    uint64_t *ch = P->h_chal.data() + b * qpk::CHAL_STRIDE;
+    for (uint32_t i = 0; i < nc; i++) ch[qpk::CH_BETA + i] = S.t.get();
+    for (uint32_t i = 0; i < nc; i++) ch[qpk::CH_GAMMA + i] = S.t.get();
+    for (int i = 0; i < 4; i++) ch[qpk::CH_PIH + i] = S.pih[i];
+  });
+  if ((rc = push_chal(P, nb))) return rc;
+  lap(0);
+
+  // ---- 2. partial products + Z (a9), commitment
+  const uint64_t pbs = (uint64_t)nc * P->nchunks * n;
+  qpk::k_pp_rows<<<dim3(cdiv(n, 256), nb), 256, 0, s>>>(P->wires.vals.p, P->sigmas.p, P->kis.p, P->chal.p, P->prods.p,
+                                                         P->log_n, P->R, P->qdf, nc, P->wires.cbs(), pbs, c->tw.fwd);
+  qpk::k_z_scan<<<dim3(nc, nb), 1024, 0, s>>>(P->prods.p, P->zs.vals.p, P->log_n, nc, P->nchunks, pbs, P->zs.cbs());
+  P->zs.build_from_values(c, nb);
+  TRY(hipGetLastError());
+  if ((rc = fetch_caps(P, P->zs.dig.p, P->zs.dbs(), logN, nb))) return rc;
+  P->pool->parallel_for(nb, [&](size_t b) {
+    ProofState &S = st[b];
+    S.caps[1].assign(P->h_caps.begin() + b * capw, P->h_caps.begin() + (b + 1) * capw);
+    S.t.observe(S.caps[1].data(), capw);
+    uint64_t *ch = P->h_chal.data() + b * qpk::CHAL_STRIDE;
+    for (uint32_t i = 0; i < nc; i++) ch[qpk::CH_ALPHA + i] = S.t.get();
+  });
+  if ((rc = push_chal(P, nb))) return rc;
+  lap(1);
+
+  // ---- 3. quotient polynomials (a8)
+  {
+    qpk::QuotientArgs a;
+    a.cs_lde = P->cs.lde.p;
+    a.w_lde = P->wires.lde.p;
+    a.z_lde = P->zs.lde.p;
+    a.w_bstride = P->wires.lbs();
+    a.z_bstride = P->zs.lbs();
+    a.chal = P->chal.p;
+    a.tw = c->tw.fwd;
+    const uint32_t B = 1u << P->rate_bits;
+    const uint64_t wN = gl::root_of_unity(logN);
+    for (uint32_t k = 0; k < B; k++) {
+      uint64_t xn = gl::pow(gl::mul(gl::GEN, gl::pow(wN, k)), n);
+      a.zh[k] = gl::sub(xn, 1);
+      a.zh_inv[k] = gl::inv(a.zh[k]);
+    }
+    a.q_out = P->qvals.p;
+    a.q_bstride = (uint64_t)nc * N;
+    a.log_n = P->log_n;
+    a.rate_bits = P->rate_bits;
+    a.R = P->R;
+    a.qdf = P->qdf;
+    a.num_constants = P->NC;
+    a.g = P->gdesc;
+    qpk::k_quotient<<<dim3(cdiv(N, 256), nb), 256, 0, s>>>(a);
+    const uint64_t n_inv = gl::inv(n);
+    qpk::k_qintt_blocks<<<dim3(B, nc, nb), 512, 8u << P->log_n, s>>>(P->qvals.p, P->cbuf.p, P->log_n, P->rate_bits,
+                                                                     (uint64_t)nc * N, (uint64_t)nc * N, c->tw.fwd,
+                                                                     c->tw.inv, n_inv, gl::inv(gl::GEN));
+    const uint64_t winv_r = gl::inv(gl::root_of_unity(P->rate_bits));
+    const uint64_t gninv = gl::inv(gl::pow(gl::GEN, n));
+    qpk::k_qintt_radix<<<dim3(cdiv(n, 256), nc, nb), 256, 0, s>>>(P->cbuf.p, P->quot.coeffs.p, P->log_n, P->rate_bits,
+                                                                 (uint64_t)nc * N, P->quot.cbs(), winv_r,
+                                                                 gl::inv(B), gninv);
+    P->quot.build(c, nb);
+    TRY(hipGetLastError());
+  }
+  if ((rc = fetch_caps(P, P->quot.dig.p, P->quot.dbs(), logN, nb))) return rc;
+  const uint64_t g_n = gl::root_of_unity(P->log_n);
+  P->pool->parallel_for(nb, [&](size_t b) {
+    ProofState &S = st[b];
+    S.caps[2].assign(P->h_caps.begin() + b * capw, P->h_caps.begin() + (b + 1) * capw);
+    S.t.observe(S.caps[2].data(), capw);
+    ext z = S.t.get_ext();
+    ext zn = gl::ext_scale(z, g_n);
+    ext zi = gl::ext_inv(z), zni = gl::ext_inv(zn);
+    uint64_t *ch = P->h_chal.data() + b * qpk::CHAL_STRIDE;
+    ch[qpk::CH_ZETA] = z.c0; ch[qpk::CH_ZETA + 1] = z.c1;
+    ch[qpk::CH_ZETA_NEXT] = zn.c0; ch[qpk::CH_ZETA_NEXT + 1] = zn.c1;
+    ch[qpk::CH_ZETA_INV] = zi.c0; ch[qpk::CH_ZETA_INV + 1] = zi.c1;
+    ch[qpk::CH_ZETA_NEXT_INV] = zni.c0; ch[qpk::CH_ZETA_NEXT_INV + 1] = zni.c1;
+  });
+  if ((rc = push_chal(P, nb))) return rc;
+  lap(2);
+
+  // ---- 4. openings (a10)
+  {
+    const uint32_t ncs = P->NC + P->R, nzs = nc * P->nchunks, nq = nc * P->qdf;
+    qpk::k_openings<<<dim3(ncs, nb), 256, 0, s>>>(P->cs.coeffs.p, 0, ncs, P->log_n, P->chal.p, qpk::CH_ZETA,
+                                                  P->openings.p, 0);
+    qpk::k_openings<<<dim3(P->W, nb), 256, 0, s>>>(P->wires.coeffs.p, P->wires.cbs(), P->W, P->log_n, P->chal.p,
+                                                   qpk::CH_ZETA, P->openings.p, ncs);
+    qpk::k_openings<<<dim3(nzs, nb), 256, 0, s>>>(P->zs.coeffs.p, P->zs.cbs(), nzs, P->log_n, P->chal.p, qpk::CH_ZETA,
+                                                  P->openings.p, ncs + P->W);
+    qpk::k_openings<<<dim3(nq, nb), 256, 0, s>>>(P->quot.coeffs.p, P->quot.cbs(), nq, P->log_n, P->chal.p,
+                                                 qpk::CH_ZETA, P->openings.p, ncs + P->W + nzs);
+    qpk::k_openings<<<dim3(nc, nb), 256, 0, s>>>(P->zs.coeffs.p, P->zs.cbs(), nc, P->log_n, P->chal.p,
+                                                 qpk::CH_ZETA_NEXT, P->openings.p, ncs + P->W + nzs + nq);
+    TRY(hipGetLastError());
+    TRY(hipMemcpyAsync(P->h_open.data(), P->openings.p, (size_t)nb * qpk::OPEN_STRIDE * 8, hipMemcpyDeviceToHost, s));
+    TRY(hipStreamSynchronize(s));
+  }
+  const uint32_t nopen = P->NC + P->R + P->W + nc * P->nchunks + nc * P->qdf;
+  P->pool->parallel_for(nb, [&](size_t b) {
+    ProofState &S = st[b];
+    const uint64_t *o = P->h_open.data() + b * qpk::OPEN_STRIDE;
+    S.t.observe(o, 2 * (size_t)nopen);           // zeta batch in oracle order
+    S.t.observe(o + 2 * (size_t)nopen, 2 * nc);  // g*zeta batch
+    ext al = S.t.get_ext();
+    ext ap = gl::ext_pow(al, nc);
+    uint64_t *ch = P->h_chal.data() + b * qpk::CHAL_STRIDE;
+    ch[qpk::CH_FRI_ALPHA] = al.c0; ch[qpk::CH_FRI_ALPHA + 1] = al.c1;
+    ch[qpk::CH_ALPHA_POW_NC] = ap.c0; ch[qpk::CH_ALPHA_POW_NC + 1] = ap.c1;
+  });
+  if ((rc = push_chal(P, nb))) return rc;
+  lap(3);
+
+  // ---- 5. FRI (a11)
+  {
+    qpk::FriComposeArgs fa;
+    fa.coeffs[0] = P->cs.coeffs.p; fa.bstride[0] = 0; fa.npolys[0] = P->NC + P->R;
+    fa.coeffs[1] = P->wires.coeffs.p; fa.bstride[1] = P->wires.cbs(); fa.npolys[1] = P->W;
+    fa.coeffs[2] = P->zs.coeffs.p; fa.bstride[2] = P->zs.cbs(); fa.npolys[2] = nc * P->nchunks;
+    fa.coeffs[3] = P->quot.coeffs.p; fa.bstride[3] = P->quot.cbs(); fa.npolys[3] = nc * P->qdf;
+    fa.noracles = 4; fa.nnext = nc; fa.log_n = P->log_n;
+    fa.chal = P->chal.p;
+    fa.comp = P->comp.p;
+    qpk::k_fri_compose<<<dim3(cdiv(n, 256), nb), 256, 0, s>>>(fa);
+    qpk::k_fri_divide<<<nb, (unsigned)std::min<uint64_t>(1024, n / 8), 0, s>>>(P->comp.p, P->fin.p, P->log_n,
+                                                                             P->chal.p, 2 * N, N);
+    TRY(hipGetLastError());
+  }
+  {
+    uint32_t lg = logN;
+    const uint64_t *coef = P->fin.p;  // layer-0 coefficients: final poly zero-padded to N, [2][N]
+    uint64_t coef_bs = 2 * N, coef_cs = N;
+    uint32_t coef_log = P->log_n;     // number of (possibly) nonzero coefficients
+    uint64_t shift = gl::GEN;
+    for (size_t l = 0; l < P->arity.size(); l++) {
+      const uint32_t ab = P->arity[l];
+      // values of this layer: coset_fft(coef, shift) of size 2^lg, leaf order
+      qpk::lde(c->tw, coef, coef_cs, P->fvals[l].p, 1ull << lg, 2, coef_log, lg - coef_log, shift, nb, coef_bs,
+               2ull << lg, s);
+      const uint64_t dbs = qpk::tree_digest_count(lg - ab, P->cap_h) * 4;
+      qpk::k_fri_leaf<<<dim3(cdiv(1ull << (lg - ab), 256), nb), 256, 0, s>>>(P->fvals[l].p, P->fdig[l].p, lg, ab,
+                                                                            2ull << lg, dbs);
+      qpk::merkle_tree(P->fdig[l].p, lg - ab, P->cap_h, nb, dbs, s);
+      TRY(hipGetLastError());
+      if ((rc = fetch_caps(P, P->fdig[l].p, dbs, lg - ab, nb))) return rc;
+      P->pool->parallel_for(nb, [&](size_t b) {
+        ProofState &S = st[b];
+        const uint64_t *cp = P->h_caps.data() + b * capw;
+        S.fri_caps.insert(S.fri_caps.end(), cp, cp + capw);
+        S.t.observe(cp, capw);
+        ext beta = S.t.get_ext();
+        uint64_t *ch = P->h_chal.data() + b * qpk::CHAL_STRIDE;
+        ch[qpk::CH_FRI_BETA + 2 * l] = beta.c0;
+        ch[qpk::CH_FRI_BETA + 2 * l + 1] = beta.c1;
+      });
+      if ((rc = push_chal(P, nb))) return rc;
+      // fold: next coefficients (length 2^(lg-ab)); only the low 2^(coef_log-ab) can be nonzero
+      qpk::k_fold<<<dim3(cdiv(1ull << (lg - ab), 256), nb), 256, 0, s>>>(coef, P->fcoef[l].p, lg, ab, (uint32_t)l,
+                                                                        P->chal.p, coef_bs, 2ull << (lg - ab));
+      TRY(hipGetLastError());
+      coef = P->fcoef[l].p;
+      lg -= ab;
+      coef_bs = 2ull << lg;
+      coef_cs = 1ull << lg;
+      coef_log = coef_log > ab ? coef_log - ab : 0;
+      shift = gl::pow(shift, 1ull << ab);
+    }
+    // final polynomial: the first final_len folded coefficients
+    TRY(hipMemcpy2DAsync(P->h_final.data(), (size_t)P->final_len * 8, coef, coef_cs * 8, (size_t)P->final_len * 8,
+                         (size_t)2 * nb, hipMemcpyDeviceToHost, s));
+    TRY(hipStreamSynchronize(s));
+  }
+  lap(4);
+
+  // ---- 6. proof of work (a12): minimal witness
+  P->pool->parallel_for(nb, [&](size_t b) {
+    ProofState &S = st[b];
+    const uint64_t *f0 = P->h_final.data() + (size_t)b * 2 * P->final_len;
+    const uint64_t *f1 = f0 + P->final_len;
+    for (uint32_t i = 0; i < P->final_len; i++) {
+      S.t.observe(f0[i]);
+      S.t.observe(f1[i]);
+    }
+    uint64_t *ps_ = P->h_powst.data() + b * 12;
+    memcpy(ps_, S.t.state, 96);
+    for (uint32_t i = 0; i < S.t.nin; i++) ps_[i] = S.t.in[i];
+    P->h_pos[b] = S.t.nin;
+  });
+  TRY(hipMemcpyAsync(P->pow_state.p, P->h_powst.data(), (size_t)nb * 96, hipMemcpyHostToDevice, s));
+  TRY(hipMemcpyAsync(P->pow_pos.p, P->h_pos.data(), (size_t)nb * 4, hipMemcpyHostToDevice, s));
+  TRY(hipMemsetAsync(P->pow_found.p, 0xFF, (size_t)nb * 8, s));
+  {
+    const uint64_t window = 1ull << 16;
+    for (uint64_t base = 0;; base += window) {
+      qpk::k_pow<<<dim3((uint32_t)(window / 256), nb), 256, 0, s>>>(P->pow_state.p, (const uint32_t *)P->pow_pos.p,
+                                                                    P->pow_found.p, base, P->pow_bits);
+      TRY(hipGetLastError());
+      TRY(hipMemcpyAsync(P->h_found.data(), P->pow_found.p, (size_t)nb * 8, hipMemcpyDeviceToHost, s));
+      TRY(hipStreamSynchronize(s));
+      bool all = true;
+      for (uint32_t b = 0; b < nb; b++) all &= P->h_found[b] != ~0ull;
+      if (all) break;
+      if (base > (1ull << 40)) {
+        c->err = "proof of work not found";
+        return QP_ERR_STATE;
+      }
+    }
+  }
+  P->pool->parallel_for(nb, [&](size_t b) {
+    ProofState &S = st[b];
+    S.pow_witness = P->h_found[b];
+    S.t.observe(S.pow_witness);
+    (void)S.t.get();
+    for (uint32_t q = 0; q < P->nq; q++) P->h_qidx[b * P->nq + q] = (uint32_t)(S.t.get() % N);
+  });
+  lap(5);
+
+  // ---- 7. query rounds: gather leaves + Merkle paths
+  TRY(hipMemcpyAsync(P->qidx.p, P->h_qidx.data(), (size_t)nb * P->nq * 4, hipMemcpyHostToDevice, s));
+  {
+    const uint32_t *qi = (const uint32_t *)P->qidx.p;
+    uint64_t off = 0;
+    const uint64_t obs = P->qout_words;
+    Tree *trees[4] = {&P->cs, &P->wires, &P->zs, &P->quot};
+    for (int o = 0; o < 4; o++) {
+      Tree *t = trees[o];
+      const uint32_t w = t->npolys;
+      const uint64_t bs = o == 0 ? 0 : t->lbs(), dbs = o == 0 ? 0 : t->dbs();
+      qpk::k_gather_rows_b<<<dim3(cdiv((uint64_t)w * P->nq, 256), nb), 256, 0, s>>>(t->lde.p, N, bs, w, qi, P->nq, 0,
+                                                                                   P->qout.p + off, obs);
+      off += (uint64_t)w * P->nq;
+      const uint32_t depth = logN - P->cap_h;
+      qpk::k_gather_paths_b<<<dim3(cdiv((uint64_t)P->nq * depth * 4, 256), nb), 256, 0, s>>>(
+          t->dig.p, dbs, logN, P->cap_h, qi, P->nq, 0, P->qout.p + off, obs);
+      off += (uint64_t)P->nq * depth * 4;
+    }
+    uint32_t lg = logN, shift = 0;
+    for (size_t l = 0; l < P->arity.size(); l++) {
+      const uint32_t ab = P->arity[l];
+      shift += ab;
+      qpk::k_gather_fri_leaf<<<dim3(cdiv((uint64_t)P->nq * (2u << ab), 256), nb), 256, 0, s>>>(
+          P->fvals[l].p, 2ull << lg, lg, ab, qi, P->nq, shift, P->qout.p + off, obs);
+      off += (uint64_t)P->nq * (2u << ab);
+      const uint32_t depth = lg - ab - P->cap_h;
+      const uint64_t dbs = qpk::tree_digest_count(lg - ab, P->cap_h) * 4;
+      qpk::k_gather_paths_b<<<dim3(cdiv((uint64_t)P->nq * depth * 4, 256), nb), 256, 0, s>>>(
+          P->fdig[l].p, dbs, lg - ab, P->cap_h, qi, P->nq, shift, P->qout.p + off, obs);
+      off += (uint64_t)P->nq * depth * 4;
+      lg -= ab;
+    }
+    TRY(hipGetLastError());
+    TRY(hipMemcpyAsync(P->h_qout.data(), P->qout.p, (size_t)nb * obs * 8, hipMemcpyDeviceToHost, s));
+    TRY(hipStreamSynchronize(s));
+  }
+  lap(6);
+
+  // ---- 8. serialize (ProofWithPublicInputs::to_bytes)
+  P->pool->parallel_for(nb, [&](size_t b) {
+    ProofState &S = st[b];
+    qh::ByteWriter w(out + b * stride);
+    for (int k = 0; k < 3; k++) w.u64s(S.caps[k].data(), capw);
+    const uint64_t *o = P->h_open.data() + b * qpk::OPEN_STRIDE;
+    const uint32_t ncs = P->NC + P->R, nzs = nc * P->nchunks;
+    // constants, sigmas, wires, zs, zs_next, partial products, quotient
+    w.u64s(o, 2 * (size_t)(ncs + P->W));
+    w.u64s(o + 2 * (size_t)(ncs + P->W), 2 * nc);
+    w.u64s(o + 2 * (size_t)nopen, 2 * nc);
+    w.u64s(o + 2 * (size_t)(ncs + P->W + nc), 2 * (size_t)(nzs - nc));
+    w.u64s(o + 2 * (size_t)(ncs + P->W + nzs), 2 * (size_t)(nc * P->qdf));
+    w.u64s(S.fri_caps.data(), S.fri_caps.size());
+    const uint64_t *qo = P->h_qout.data() + b * P->qout_words;
+    const uint32_t depth = logN - P->cap_h;
+    std::vector<const uint64_t *> leafp(4), pathp(4);
+    uint64_t off = 0;
+    for (int oo = 0; oo < 4; oo++) {
+      leafp[oo] = qo + off;
+      off += (uint64_t)oracle_width(P, oo) * P->nq;
+      pathp[oo] = qo + off;
+      off += (uint64_t)P->nq * depth * 4;
+    }
+    std::vector<const uint64_t *> lleaf(P->arity.size()), lpath(P->arity.size());
+    std::vector<uint32_t> ldepth(P->arity.size());
+    uint32_t lg = logN;
+    for (size_t l = 0; l < P->arity.size(); l++) {
+      lleaf[l] = qo + off;
+      off += (uint64_t)P->nq * (2u << P->arity[l]);
+      ldepth[l] = lg - P->arity[l] - P->cap_h;
+      lpath[l] = qo + off;
+      off += (uint64_t)P->nq * ldepth[l] * 4;
+      lg -= P->arity[l];
+    }
+    for (uint32_t q = 0; q < P->nq; q++) {
+      for (int oo = 0; oo < 4; oo++) {
+        const uint32_t wd = oracle_width(P, oo);
+        w.u64s(leafp[oo] + (size_t)q * wd, wd);
+        w.u8((uint8_t)depth);
+        w.u64s(pathp[oo] + (size_t)q * depth * 4, (size_t)depth * 4);
+      }
+      for (size_t l = 0; l < P->arity.size(); l++) {
+        const uint32_t lw = 2u << P->arity[l];
+        w.u64s(lleaf[l] + (size_t)q * lw, lw);
+        w.u8((uint8_t)ldepth[l]);
+        w.u64s(lpath[l] + (size_t)q * ldepth[l] * 4, (size_t)ldepth[l] * 4);
+      }
+    }
+    const uint64_t *f0 = P->h_final.data() + (size_t)b * 2 * P->final_len;
+    for (uint32_t i = 0; i < P->final_len; i++) {
+      w.u64(f0[i]);
+      w.u64(f0[P->final_len + i]);
+    }
+    w.u64(S.pow_witness);
+    w.u64(P->npis);
+    w.u64s(pis_host[b], P->npis);
+    if (lens) lens[b] = w.pos;
+  });
+  lap(7);
+  return QP_OK;
+}
+
+}  // namespace
+
+extern "C" {
+
+int qp_prover_new(qp_ctx *c, const qp_circuit *circuit, uint32_t max_batch, qp_prover **out) {
+  if (!c || !circuit || !out || !max_batch) return QP_ERR_ARG;
+  *out = nullptr;
+  qp_prover *P = new (std::nothrow) qp_prover();
+  if (!P) return QP_ERR_OOM;
+  P->ctx = c;
+  P->circuit = circuit;
+  P->max_batch = max_batch;
+  int rc;
+  try {
+    rc = setup(P);
+  } catch (const std::bad_alloc &) {
+    rc = QP_ERR_OOM;
+  }
+  if (rc) {
+    delete P;
+    return rc;
+  }
+  *out = P;
+  return QP_OK;
+}
+
+void qp_prover_free(qp_prover *P) {
+  if (!P) return;
+  (void)hipSetDevice(P->ctx->device);
+  (void)hipStreamSynchronize(P->ctx->stream);
+  delete P;
+}
+
+int qp_prover_proof_size(const qp_prover *P, size_t *len) {
+  if (!P || !len) return QP_ERR_ARG;
+  *len = P->proof_len;
+  return QP_OK;
+}
+
+int qp_prover_verifier_data(const qp_prover *P, uint8_t *out, size_t cap, size_t *len) {
+  if (!P) return QP_ERR_ARG;
+  const size_t capw = 4u << P->cap_h;
+  const size_t total = 8 + capw * 8 + 32 + P->common.size();
+  if (len) *len = total;
+  if (!out) return QP_OK;
+  if (cap < total) return QP_ERR_ARG;
+  qh::ByteWriter w(out);
+  w.u64(P->cap_h);
+  w.u64s(P->cs_cap, capw);
+  w.u64s(P->digest, 4);
+  memcpy(out + w.pos, P->common.data(), P->common.size());
+  return QP_OK;
+}
+
+int qp_prover_prove_wires(qp_prover *P, const uint64_t *wires, const uint64_t *pis, uint32_t nproofs, uint8_t *out,
+                          size_t stride, size_t *lens) {
+  if (!P || !wires || !pis || !out || !nproofs) return QP_ERR_ARG;
+  if (stride < P->proof_len) {
+    P->ctx->err = "output stride smaller than the proof size";
+    return QP_ERR_ARG;
+  }
+  const uint64_t wsz = (uint64_t)P->W << P->log_n;
+  for (uint32_t done = 0; done < nproofs;) {
+    const uint32_t nb = std::min(P->max_batch, nproofs - done);
+    std::vector<const uint64_t *> wp(nb), pp(nb);
+    for (uint32_t b = 0; b < nb; b++) {
+      wp[b] = wires + (uint64_t)(done + b) * wsz;
+      pp[b] = pis + (uint64_t)(done + b) * P->npis;
+    }
+    int rc;
+    try {
+      rc = prove_batch(P, wp.data(), pp.data(), nb, out + (size_t)done * stride, stride, lens ? lens + done : nullptr);
+    } catch (const std::bad_alloc &) {
+      rc = QP_ERR_OOM;
+    }
+    if (rc) return rc;
+    done += nb;
+  }
+  return QP_OK;
+}
+
+int qp_prover_prove(qp_prover *P, const qp_witness *const *w, uint32_t nproofs, uint8_t *out, size_t stride,
+                    size_t *lens) {
+  if (!P || !w || !out || !nproofs) return QP_ERR_ARG;
+  if (stride < P->proof_len) {
+    P->ctx->err = "output stride smaller than the proof size";
+    return QP_ERR_ARG;
+  }
+  const uint64_t wsz = (uint64_t)P->W << P->log_n;
+  for (uint32_t done = 0; done < nproofs;) {
+    const uint32_t nb = std::min(P->max_batch, nproofs - done);
+    std::vector<uint64_t> wires((size_t)nb * wsz), pis((size_t)nb * P->npis);
+    bool bad = false;
+    P->pool->parallel_for(nb, [&](size_t b) {
+      const qp_witness *wt = w[done + b];
+      if (!wt || wt->circuit != P->circuit) {
+        bad = true;
+        return;
+      }
+      wt->w.wires_matrix(wires.data() + b * wsz);
+      auto pi = wt->w.public_inputs();
+      memcpy(pis.data() + b * P->npis, pi.data(), P->npis * 8);
+    });
+    if (bad) {
+      P->ctx->err = "witness belongs to a different circuit";
+      return QP_ERR_ARG;
+    }
+    std::vector<const uint64_t *> wp(nb), pp(nb);
+    for (uint32_t b = 0; b < nb; b++) {
+      wp[b] = wires.data() + b * wsz;
+      pp[b] = pis.data() + b * P->npis;
+    }
+    int rc;
+    try {
+      rc = prove_batch(P, wp.data(), pp.data(), nb, out + (size_t)done * stride, stride, lens ? lens + done : nullptr);
+    } catch (const std::bad_alloc &) {
+      rc = QP_ERR_OOM;
+    }
+    if (rc) return rc;
+    done += nb;
+  }
+  return QP_OK;
+}
+
+int qp_prover_stage_times(qp_prover *P, double *ms, uint32_t n, int reset) {
+  if (!P) return QP_ERR_ARG;
+  for (uint32_t i = 0; i < n && i < 16; i++) ms[i] = P->stage_ms[i];
+  if (reset)
+    for (double &x : P->stage_ms) x = 0;
+  return QP_OK;
+}
+
+}  // extern "C"

@@ -1,0 +1,72 @@
+// prover_kernels.h — argument layouts and launchers of prover_kernels.hip.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+#include "kernels.h"
+#include "ntt_device.h"
+
+namespace qpk {
+
+// per-proof challenge block (device, u64 words)
+enum : uint32_t {
+  CH_BETA = 0, CH_GAMMA = 2, CH_ALPHA = 4, CH_PIH = 6, CH_ZETA = 10, CH_ZETA_NEXT = 12, CH_ZETA_INV = 14,
+  CH_ZETA_NEXT_INV = 16, CH_FRI_ALPHA = 18, CH_ALPHA_POW_NC = 20, CH_FRI_BETA = 22, CHAL_STRIDE = 40
+};
+constexpr uint32_t OPEN_STRIDE = 520;  // 257 ext openings per proof (+pad)
+
+enum GateKindDev : uint32_t { GK_NOOP = 0, GK_CONSTANT, GK_PUBLIC_INPUT, GK_BASE_SUM, GK_ARITHMETIC, GK_POSEIDON };
+
+struct GateDesc {
+  uint32_t ngates = 0, nsel = 0;
+  uint32_t kind[8] = {0}, param[8] = {0}, sel_index[8] = {0}, grp_lo[8] = {0}, grp_hi[8] = {0};
+};
+
+struct QuotientArgs {
+  const uint64_t *cs_lde, *w_lde, *z_lde;
+  uint64_t w_bstride, z_bstride;
+  const uint64_t *chal, *tw;
+  uint64_t zh[16], zh_inv[16];
+  uint64_t *q_out;
+  uint64_t q_bstride;
+  uint32_t log_n, rate_bits, R, qdf, num_constants;
+  GateDesc g;
+};
+
+struct FriComposeArgs {
+  const uint64_t *coeffs[4];
+  uint64_t bstride[4];
+  uint32_t npolys[4];
+  uint32_t noracles, nnext, log_n;
+  const uint64_t *chal;
+  uint64_t *comp;
+};
+
+__global__ void k_pp_rows(const uint64_t *wires, const uint64_t *sigmas, const uint64_t *k_is, const uint64_t *chal,
+                          uint64_t *prods, uint32_t log_n, uint32_t R, uint32_t qdf, uint32_t nc, uint64_t w_bstride,
+                          uint64_t p_bstride, const uint64_t *tw);
+__global__ void k_z_scan(const uint64_t *prods, uint64_t *zs, uint32_t log_n, uint32_t nc, uint32_t nchunks,
+                         uint64_t p_bstride, uint64_t z_bstride);
+__global__ void k_quotient(QuotientArgs a);
+__global__ void k_qintt_blocks(const uint64_t *vals, uint64_t *out, uint32_t log_n, uint32_t rate_bits,
+                               uint64_t v_bstride, uint64_t o_bstride, const uint64_t *tw, const uint64_t *tw_inv,
+                               uint64_t n_inv, uint64_t ginv);
+__global__ void k_qintt_radix(const uint64_t *cbuf, uint64_t *coeffs, uint32_t log_n, uint32_t rate_bits,
+                              uint64_t c_bstride, uint64_t o_bstride, uint64_t winv_r, uint64_t r_inv, uint64_t gninv);
+__global__ void k_openings(const uint64_t *coeffs, uint64_t c_bstride, uint32_t npolys, uint32_t log_n,
+                           const uint64_t *pts, uint32_t pt_off, uint64_t *out, uint32_t out_off);
+__global__ void k_fri_compose(FriComposeArgs a);
+__global__ void k_fri_divide(const uint64_t *comp, uint64_t *fin, uint32_t log_n, const uint64_t *chal,
+                             uint64_t f_bstride, uint64_t f_cstride);
+__global__ void k_fri_leaf(const uint64_t *vals, uint64_t *dig, uint32_t log_len, uint32_t ab, uint64_t v_bstride,
+                           uint64_t d_bstride);
+__global__ void k_fold(const uint64_t *cin, uint64_t *cout, uint32_t log_len, uint32_t ab, uint32_t layer,
+                       const uint64_t *chal, uint64_t i_bstride, uint64_t o_bstride);
+__global__ void k_pow(const uint64_t *states, const uint32_t *pos, uint64_t *found, uint64_t base, uint32_t bits);
+__global__ void k_gather_rows_b(const uint64_t *cols, uint64_t stride, uint64_t bstride, uint32_t ncols,
+                                const uint32_t *idx, uint32_t nq, uint32_t shift, uint64_t *out, uint64_t o_bstride);
+__global__ void k_gather_paths_b(const uint64_t *dig, uint64_t d_bstride, uint32_t log_leaves, uint32_t cap_h,
+                                 const uint32_t *idx, uint32_t nq, uint32_t shift, uint64_t *out, uint64_t o_bstride);
+__global__ void k_gather_fri_leaf(const uint64_t *vals, uint64_t v_bstride, uint32_t log_len, uint32_t ab,
+                                  const uint32_t *idx, uint32_t nq, uint32_t shift, uint64_t *out, uint64_t o_bstride);
+
+}  // namespace qpk

@@ -1,0 +1,567 @@
+// prover_kernels.hip — gfx950 kernels for the proof stages after the
+// commitments, batched over
+// proofs of one circuit (blockIdx.y / .z = proof index, per-proof strides).
+//
+//   k_pp_rows / k_z_scan   wires_permutation_partial_products_and_zs (a9)
+//   k_quotient             compute_quotient_polys: vanishing poly at every
+//                          LDE point, alpha-reduced, / Z_H (a8)
+//   k_qintt_blocks/_radix  coset_ifft of size N as 2^r size-n LDS iNTTs + a
+//                          radix-2^r cross-block pass (a8, second half)
+//   k_openings             OpeningSet::new: Horner at zeta / g*zeta (a10)
+//   k_fri_compose/_divide  prove_openings: alpha-reduce + divide by (X - z) (a11)
+//   k_fri_leaf, k_fold     fri_committed_trees: leaves of 2^a ext, folding (a11)
+//   k_pow                  fri_proof_of_work: minimal witness (a12)
+//   k_gather_*             query-round openings (a11)
+#include "field.h"
+#include "poseidon.h"
+#include "prover_kernels.h"
+
+namespace qpk {
+
+using gl::ext;
+
+__device__ __forceinline__ uint64_t wpow_N(const uint64_t *__restrict__ tw, uint32_t j, uint32_t logN) {
+  // w_N^j from the half table of w_{2^TW_LOG}: w_N^j = w_T^{j << (TW_LOG-logN)}
+  uint32_t e = j << (TW_LOG - logN);
+  const uint32_t half = 1u << (TW_LOG - 1);
+  return e < half ? tw[e] : gl::neg(tw[e - half]);
+}
+
+// ---------------------------------------------------------------- a9
+
+// per row: P_j = prod_{k<=j} num_k/den_k over chunks of qdf routed wires
+__global__ void __launch_bounds__(256) k_pp_rows(const uint64_t *__restrict__ wires, const uint64_t *__restrict__ sigmas,
+                                                 const uint64_t *__restrict__ k_is, const uint64_t *__restrict__ chal,
+                                                 uint64_t *__restrict__ prods, uint32_t log_n, uint32_t R, uint32_t qdf,
+                                                 uint32_t nc, uint64_t w_bstride, uint64_t p_bstride,
+                                                 const uint64_t *__restrict__ tw) {
+  const uint32_t n = 1u << log_n;
+  const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  const uint32_t b = blockIdx.y;
+  wires += b * w_bstride;
+  prods += b * p_bstride;
+  const uint64_t *ch = chal + b * CHAL_STRIDE;
+  const uint64_t x = wpow_N(tw, i, log_n);
+  const uint32_t nchunks = (R + qdf - 1) / qdf;
+  for (uint32_t c = 0; c < nc; c++) {
+    const uint64_t beta = ch[CH_BETA + c], gamma = ch[CH_GAMMA + c];
+    uint64_t num[16], den[16];
+    for (uint32_t k = 0; k < nchunks; k++) {
+      uint64_t nn = 1, dd = 1;
+      for (uint32_t j = k * qdf; j < (k + 1) * qdf && j < R; j++) {
+        uint64_t wv = wires[(uint64_t)j * n + i];
+        nn = gl::mul(nn, gl::add(gl::add(wv, gl::mul(beta, gl::mul(k_is[j], x))), gamma));
+        dd = gl::mul(dd, gl::add(gl::add(wv, gl::mul(beta, sigmas[(uint64_t)j * n + i])), gamma));
+      }
+      num[k] = nn;
+      den[k] = dd;
+    }
+    // batch inversion of den[0..nchunks)
+    uint64_t pre[16], acc = 1;
+    for (uint32_t k = 0; k < nchunks; k++) {
+      pre[k] = acc;
+      acc = gl::mul(acc, den[k]);
+    }
+    uint64_t inv = gl::inv(acc);
+    for (uint32_t k = nchunks; k-- > 0;) {
+      uint64_t t = gl::mul(inv, pre[k]);
+      inv = gl::mul(inv, den[k]);
+      den[k] = t;
+    }
+    uint64_t run = 1;
+    for (uint32_t k = 0; k < nchunks; k++) {
+      run = gl::mul(run, gl::mul(num[k], den[k]));
+      prods[((uint64_t)c * nchunks + k) * n + i] = run;
+    }
+  }
+}
+
+// exclusive prefix product of the full-row products -> Z; pp_j = Z * P_j
+__global__ void __launch_bounds__(1024) k_z_scan(const uint64_t *__restrict__ prods, uint64_t *__restrict__ zs,
+                                                 uint32_t log_n, uint32_t nc, uint32_t nchunks, uint64_t p_bstride,
+                                                 uint64_t z_bstride) {
+  __shared__ uint64_t sh[1024];
+  const uint32_t n = 1u << log_n;
+  const uint32_t c = blockIdx.x, b = blockIdx.y;
+  prods += b * p_bstride + (uint64_t)c * nchunks * n;
+  zs += b * z_bstride;
+  const uint64_t *full = prods + (uint64_t)(nchunks - 1) * n;
+  const uint32_t T = blockDim.x, per = (n + T - 1) / T;
+  const uint32_t lo = threadIdx.x * per, hi = min(lo + per, n);
+  uint64_t local = 1;
+  for (uint32_t i = lo; i < hi; i++) local = gl::mul(local, full[i]);
+  sh[threadIdx.x] = local;
+  __syncthreads();
+  // inclusive Hillis-Steele scan over T partial products
+  for (uint32_t off = 1; off < T; off <<= 1) {
+    uint64_t v = threadIdx.x >= off ? sh[threadIdx.x - off] : 1;
+    __syncthreads();
+    sh[threadIdx.x] = gl::mul(sh[threadIdx.x], v);
+    __syncthreads();
+  }
+  uint64_t z = threadIdx.x ? sh[threadIdx.x - 1] : 1;
+  const uint32_t npp = nchunks - 1;
+  for (uint32_t i = lo; i < hi; i++) {
+    zs[(uint64_t)c * n + i] = z;
+    for (uint32_t j = 0; j < npp; j++)
+      zs[((uint64_t)nc + c * npp + j) * n + i] = gl::mul(z, prods[(uint64_t)j * n + i]);
+    z = gl::mul(z, full[i]);
+  }
+}
+
+// ---------------------------------------------------------------- a8
+
+struct Acc2 {
+  uint64_t acc0, acc1, p0, p1, a0, a1;
+  __device__ __forceinline__ void emit(uint64_t t) {
+    acc0 = gl::add(acc0, gl::mul(t, p0));
+    acc1 = gl::add(acc1, gl::mul(t, p1));
+    p0 = gl::mul(p0, a0);
+    p1 = gl::mul(p1, a1);
+  }
+  __device__ __forceinline__ void emitf(uint64_t f, uint64_t t) { emit(gl::mul(f, t)); }
+};
+
+#define WV(j) wl[(uint64_t)(j) * N]
+
+__device__ __forceinline__ void poseidon_gate(const uint64_t *__restrict__ wl, uint64_t N, uint64_t f, Acc2 &A) {
+  const uint64_t swap = WV(24);
+  A.emitf(f, gl::mul(swap, gl::sub(swap, 1)));
+  uint64_t s[12];
+#pragma unroll
+  for (int i = 0; i < 4; i++) {
+    const uint64_t delta = WV(25 + i), a = WV(i), c = WV(i + 4);
+    A.emitf(f, gl::sub(gl::mul(swap, gl::sub(c, a)), delta));
+    s[i] = gl::add(a, delta);
+    s[i + 4] = gl::sub(c, delta);
+  }
+#pragma unroll
+  for (int i = 8; i < 12; i++) s[i] = WV(i);
+  int rc = 0;
+  for (int r = 0; r < 4; r++, rc++) {
+#pragma unroll
+    for (int i = 0; i < 12; i++) s[i] = gl::add(s[i], ps::rc(rc * 12 + i));
+    if (r) {
+#pragma unroll
+      for (int i = 0; i < 12; i++) {
+        const uint64_t sb = WV(29 + (r - 1) * 12 + i);
+        A.emitf(f, gl::sub(s[i], sb));
+        s[i] = sb;
+      }
+    }
+#pragma unroll
+    for (int i = 0; i < 12; i++) s[i] = ps::sbox(s[i]);
+    ps::mds(s);
+  }
+  for (int r = 0; r < 22; r++, rc++) {
+#pragma unroll
+    for (int i = 0; i < 12; i++) s[i] = gl::add(s[i], ps::rc(rc * 12 + i));
+    const uint64_t sb = WV(65 + r);
+    A.emitf(f, gl::sub(s[0], sb));
+    s[0] = ps::sbox(sb);
+    ps::mds(s);
+  }
+  for (int r = 0; r < 4; r++, rc++) {
+#pragma unroll
+    for (int i = 0; i < 12; i++) s[i] = gl::add(s[i], ps::rc(rc * 12 + i));
+#pragma unroll
+    for (int i = 0; i < 12; i++) {
+      const uint64_t sb = WV(87 + r * 12 + i);
+      A.emitf(f, gl::sub(s[i], sb));
+      s[i] = sb;
+    }
+#pragma unroll
+    for (int i = 0; i < 12; i++) s[i] = ps::sbox(s[i]);
+    ps::mds(s);
+  }
+#pragma unroll
+  for (int i = 0; i < 12; i++) A.emitf(f, gl::sub(s[i], WV(12 + i)));
+}
+
+__global__ void __launch_bounds__(256) k_quotient(QuotientArgs a) {
+  const uint32_t logN = a.log_n + a.rate_bits;
+  const uint64_t N = 1ull << logN, n = 1ull << a.log_n;
+  const uint32_t t = blockIdx.x * blockDim.x + threadIdx.x;
+  if (t >= N) return;
+  const uint32_t b = blockIdx.y;
+  const uint64_t *ch = a.chal + b * CHAL_STRIDE;
+  const uint64_t *cs = a.cs_lde + t;                       // [ncs][N]
+  const uint64_t *wl = a.w_lde + b * a.w_bstride + t;      // [W][N]
+  const uint64_t *zl = a.z_lde + b * a.z_bstride;          // [nzs][N]
+  const uint32_t j = gl::rev_bits(t, logN);                // natural point index
+  const uint32_t tn = gl::rev_bits((j + (1u << a.rate_bits)) & (uint32_t)(N - 1), logN);
+  const uint64_t x = gl::mul(gl::GEN, wpow_N(a.tw, j, logN));
+  const uint64_t zh = a.zh[j & ((1u << a.rate_bits) - 1)];
+  const uint64_t zh_inv = a.zh_inv[j & ((1u << a.rate_bits) - 1)];
+  Acc2 A;
+  A.acc0 = A.acc1 = 0;
+  A.p0 = A.p1 = 1;
+  A.a0 = ch[CH_ALPHA + 0];
+  A.a1 = ch[CH_ALPHA + 1];
+  // L_0(x) (Z_c - 1)
+  const uint64_t l0 = gl::mul(zh, gl::inv(gl::mul(gl::sub(x, 1), n % gl::P)));
+  for (uint32_t c = 0; c < 2; c++) A.emit(gl::mul(l0, gl::sub(zl[(uint64_t)c * N + t], 1)));
+  // partial-product checks
+  const uint32_t R = a.R, qdf = a.qdf, nchunks = (R + qdf - 1) / qdf, npp = nchunks - 1;
+  for (uint32_t c = 0; c < 2; c++) {
+    const uint64_t beta = ch[CH_BETA + c], gamma = ch[CH_GAMMA + c];
+    uint64_t kx = x;  // k_j * x with k_j = g^j
+    for (uint32_t k = 0; k < nchunks; k++) {
+      uint64_t num = 1, den = 1;
+      for (uint32_t jj = k * qdf; jj < (k + 1) * qdf && jj < R; jj++) {
+        const uint64_t wv = WV(jj);
+        num = gl::mul(num, gl::add(gl::add(wv, gl::mul(beta, kx)), gamma));
+        den = gl::mul(den, gl::add(gl::add(wv, gl::mul(beta, cs[(uint64_t)(a.num_constants + jj) * N])), gamma));
+        kx = gl::mul(kx, gl::GEN);
+      }
+      const uint64_t prev = k == 0 ? zl[(uint64_t)c * N + t] : zl[((uint64_t)2 + c * npp + k - 1) * N + t];
+      const uint64_t next = k == nchunks - 1 ? zl[(uint64_t)c * N + tn] : zl[((uint64_t)2 + c * npp + k) * N + t];
+      A.emit(gl::sub(gl::mul(prev, num), gl::mul(next, den)));
+    }
+  }
+  // gate constraints: every gate restarts at alpha^(#pre-terms)
+  const uint64_t base0 = A.p0, base1 = A.p1;
+  uint64_t consts[8];
+  for (uint32_t k = 0; k < a.num_constants && k < 8; k++) consts[k] = cs[(uint64_t)k * N];
+  const uint32_t nsel = a.g.nsel;
+  for (uint32_t gi = 0; gi < a.g.ngates; gi++) {
+    const uint32_t si = a.g.sel_index[gi];
+    const uint64_t s = consts[si];
+    uint64_t f = 1;
+    for (uint32_t jj = a.g.grp_lo[si]; jj < a.g.grp_hi[si]; jj++)
+      if (jj != gi) f = gl::mul(f, gl::sub(jj, s));
+    if (nsel > 1) f = gl::mul(f, gl::sub(0xFFFFFFFFull, s));
+    A.p0 = base0;
+    A.p1 = base1;
+    const uint64_t *gc = consts + nsel;
+    switch (a.g.kind[gi]) {
+      case GK_CONSTANT:
+        for (uint32_t i = 0; i < a.g.param[gi]; i++) A.emitf(f, gl::sub(gc[i], WV(i)));
+        break;
+      case GK_PUBLIC_INPUT:
+        for (uint32_t i = 0; i < 4; i++) A.emitf(f, gl::sub(WV(i), ch[CH_PIH + i]));
+        break;
+      case GK_BASE_SUM: {
+        const uint32_t L = a.g.param[gi];
+        uint64_t acc = 0;
+        for (uint32_t i = L; i-- > 0;) acc = gl::add(gl::add(acc, acc), WV(1 + i));
+        A.emitf(f, gl::sub(acc, WV(0)));
+        for (uint32_t i = 0; i < L; i++) {
+          const uint64_t l = WV(1 + i);
+          A.emitf(f, gl::mul(l, gl::sub(l, 1)));
+        }
+        break;
+      }
+      case GK_ARITHMETIC:
+        for (uint32_t i = 0; i < a.g.param[gi]; i++) {
+          const uint64_t comp = gl::add(gl::mul(gl::mul(WV(4 * i), WV(4 * i + 1)), gc[0]), gl::mul(WV(4 * i + 2), gc[1]));
+          A.emitf(f, gl::sub(WV(4 * i + 3), comp));
+        }
+        break;
+      case GK_POSEIDON:
+        poseidon_gate(wl, N, f, A);
+        break;
+      default:
+        break;
+    }
+  }
+  uint64_t *q = a.q_out + b * a.q_bstride;
+  q[t] = gl::mul(A.acc0, zh_inv);
+  q[N + t] = gl::mul(A.acc1, zh_inv);
+}
+#undef WV
+
+// coset iNTT, stage 1: block s' holds coset s = rev_r(s') values in bit-reversed
+// order; produce C^s_k = iNTT_n(block)_k * (g w_N^s)^-k   (scaled by 1/n)
+__global__ void __launch_bounds__(512) k_qintt_blocks(const uint64_t *__restrict__ vals, uint64_t *__restrict__ out,
+                                                      uint32_t log_n, uint32_t rate_bits, uint64_t v_bstride,
+                                                      uint64_t o_bstride, const uint64_t *__restrict__ tw,
+                                                      const uint64_t *__restrict__ tw_inv, uint64_t n_inv,
+                                                      uint64_t ginv) {
+  extern __shared__ __attribute__((aligned(16))) uint64_t lds[];
+  const uint32_t n = 1u << log_n, logN = log_n + rate_bits;
+  const uint32_t sp = blockIdx.x, c = blockIdx.y, b = blockIdx.z;
+  const uint32_t s = gl::rev_bits(sp, rate_bits);
+  const uint64_t N = (uint64_t)n << rate_bits;
+  const uint64_t *src = vals + b * v_bstride + c * N + ((uint64_t)sp << log_n);
+  for (uint32_t p = threadIdx.x; p < n; p += blockDim.x) lds[gl::rev_bits(p, log_n)] = src[p];
+  __syncthreads();
+  dif_lds(lds, log_n, tw_inv);
+  // base^-1 = g^-1 w_N^-s
+  const uint64_t wNs = wpow_N(tw, s, logN);
+  const uint64_t binv = gl::mul(ginv, gl::inv(wNs));
+  uint64_t f = gl::mul(gl::pow(binv, threadIdx.x), n_inv);
+  const uint64_t step = gl::pow(binv, blockDim.x);
+  uint64_t *dst = out + b * o_bstride + ((uint64_t)c << rate_bits) * n + (uint64_t)s * n;
+  for (uint32_t k = threadIdx.x; k < n; k += blockDim.x) {
+    dst[k] = gl::mul(lds[gl::rev_bits(k, log_n)], f);
+    f = gl::mul(f, step);
+  }
+}
+
+// coset iNTT, stage 2: e_j = (1/2^r) sum_s C^s_k w_{2^r}^{-sj}; a_{k+jn} = e_j g^{-jn}
+__global__ void __launch_bounds__(256) k_qintt_radix(const uint64_t *__restrict__ cbuf, uint64_t *__restrict__ coeffs,
+                                                     uint32_t log_n, uint32_t rate_bits, uint64_t c_bstride,
+                                                     uint64_t o_bstride, uint64_t winv_r, uint64_t r_inv,
+                                                     uint64_t gninv) {
+  const uint32_t n = 1u << log_n, B = 1u << rate_bits;
+  const uint32_t k = blockIdx.x * blockDim.x + threadIdx.x;
+  if (k >= n) return;
+  const uint32_t c = blockIdx.y, b = blockIdx.z;
+  const uint64_t *src = cbuf + b * c_bstride + (uint64_t)c * B * n + k;
+  uint64_t C[16];
+  for (uint32_t s = 0; s < B; s++) C[s] = src[(uint64_t)s * n];
+  uint64_t *dst = coeffs + b * o_bstride + (uint64_t)c * B * n + k;
+  uint64_t gj = r_inv;  // (1/B) g^{-jn}
+  uint64_t wj = 1;      // w_B^{-j}
+  for (uint32_t jj = 0; jj < B; jj++) {
+    uint64_t e = 0, wsj = 1;
+    for (uint32_t s = 0; s < B; s++) {
+      e = gl::add(e, gl::mul(C[s], wsj));
+      wsj = gl::mul(wsj, wj);
+    }
+    dst[(uint64_t)jj * n] = gl::mul(e, gj);
+    gj = gl::mul(gj, gninv);
+    wj = gl::mul(wj, winv_r);
+  }
+}
+
+// ---------------------------------------------------------------- a10
+
+// value of each coefficient column at an extension point: out[b][poly]
+__global__ void __launch_bounds__(256) k_openings(const uint64_t *__restrict__ coeffs, uint64_t c_bstride,
+                                                  uint32_t npolys, uint32_t log_n, const uint64_t *__restrict__ pts,
+                                                  uint32_t pt_off, uint64_t *__restrict__ out, uint32_t out_off) {
+  __shared__ ext red[256];
+  const uint32_t n = 1u << log_n;
+  const uint32_t p = blockIdx.x, b = blockIdx.y;
+  const uint64_t *cf = coeffs + b * c_bstride + (uint64_t)p * n;
+  const ext z = ext{pts[b * CHAL_STRIDE + pt_off], pts[b * CHAL_STRIDE + pt_off + 1]};
+  ext zp = gl::ext_pow(z, threadIdx.x);
+  const ext zs = gl::ext_pow(z, blockDim.x);
+  ext acc{0, 0};
+  for (uint32_t k = threadIdx.x; k < n; k += blockDim.x) {
+    acc = gl::ext_add(acc, gl::ext_scale(zp, cf[k]));
+    zp = gl::ext_mul(zp, zs);
+  }
+  red[threadIdx.x] = acc;
+  __syncthreads();
+  for (uint32_t o = blockDim.x / 2; o; o >>= 1) {
+    if (threadIdx.x < o) red[threadIdx.x] = gl::ext_add(red[threadIdx.x], red[threadIdx.x + o]);
+    __syncthreads();
+  }
+  if (!threadIdx.x) {
+    uint64_t *dst = out + b * OPEN_STRIDE + 2 * (out_off + p);
+    dst[0] = red[0].c0;
+    dst[1] = red[0].c1;
+  }
+}
+
+// ---------------------------------------------------------------- a11
+
+// comp[k] = sum_j alpha^j c_j[k] over the listed oracles (Horner, reverse order)
+__global__ void __launch_bounds__(256) k_fri_compose(FriComposeArgs a) {
+  const uint32_t n = 1u << a.log_n;
+  const uint32_t k = blockIdx.x * blockDim.x + threadIdx.x;
+  if (k >= n) return;
+  const uint32_t b = blockIdx.y;
+  const uint64_t *ch = a.chal + b * CHAL_STRIDE;
+  const ext al{ch[CH_FRI_ALPHA], ch[CH_FRI_ALPHA + 1]};
+  ext acc{0, 0};
+  for (int o = (int)a.noracles - 1; o >= 0; o--) {
+    const uint64_t *base = a.coeffs[o] + b * a.bstride[o] + k;
+    for (uint32_t p = a.npolys[o]; p-- > 0;) acc = gl::ext_add(gl::ext_mul(acc, al), ext{base[(uint64_t)p * n], 0});
+  }
+  ext acc2{0, 0};
+  const uint64_t *zb = a.coeffs[2] + b * a.bstride[2] + k;
+  for (uint32_t p = a.nnext; p-- > 0;) acc2 = gl::ext_add(gl::ext_mul(acc2, al), ext{zb[(uint64_t)p * n], 0});
+  uint64_t *o1 = a.comp + b * (4ull * n);
+  o1[k] = acc.c0;
+  o1[n + k] = acc.c1;
+  o1[2 * n + k] = acc2.c0;
+  o1[3 * n + k] = acc2.c1;
+}
+
+// suffix-scan form of divide_by_linear: q_{k-1} = sum_{i>=k} c_i z^{i-k}
+//   = z^{-k} S_k with S_k = sum_{i>=k} c_i z^i; final = alpha^nc Q1 + Q2
+__global__ void __launch_bounds__(1024) k_fri_divide(const uint64_t *__restrict__ comp, uint64_t *__restrict__ fin,
+                                                     uint32_t log_n, const uint64_t *__restrict__ chal,
+                                                     uint64_t f_bstride, uint64_t f_cstride) {
+  __shared__ ext sh[1024];
+  const uint32_t n = 1u << log_n, b = blockIdx.x;
+  const uint64_t *ch = chal + b * CHAL_STRIDE;
+  const uint32_t T = blockDim.x, per = n / T;
+  const uint32_t lo = threadIdx.x * per;
+  ext res[16];
+  for (int pass = 0; pass < 2; pass++) {
+    const uint64_t *cc = comp + b * (4ull * n) + (uint64_t)pass * 2 * n;
+    const ext z{ch[pass ? CH_ZETA_NEXT : CH_ZETA], ch[(pass ? CH_ZETA_NEXT : CH_ZETA) + 1]};
+    const ext zi{ch[pass ? CH_ZETA_NEXT_INV : CH_ZETA_INV], ch[(pass ? CH_ZETA_NEXT_INV : CH_ZETA_INV) + 1]};
+    // local suffix sums within [lo, lo+per) of d_i = c_i z^i
+    ext zp = gl::ext_pow(z, lo);
+    ext d[16];
+    for (uint32_t i = 0; i < per; i++) {
+      d[i] = gl::ext_mul(ext{cc[lo + i], cc[n + lo + i]}, zp);
+      zp = gl::ext_mul(zp, z);
+    }
+    ext tot{0, 0};
+    for (uint32_t i = per; i-- > 0;) {
+      tot = gl::ext_add(tot, d[i]);
+      d[i] = tot;
+    }
+    sh[threadIdx.x] = tot;
+    __syncthreads();
+    // inclusive suffix scan across threads
+    for (uint32_t off = 1; off < T; off <<= 1) {
+      ext v = threadIdx.x + off < T ? sh[threadIdx.x + off] : ext{0, 0};
+      __syncthreads();
+      sh[threadIdx.x] = gl::ext_add(sh[threadIdx.x], v);
+      __syncthreads();
+    }
+    const ext after = threadIdx.x + 1 < T ? sh[threadIdx.x + 1] : ext{0, 0};
+    __syncthreads();
+    // q_{k-1} = z^{-k} (S_k) for k >= 1; output index m = k-1; q_{n-1} = 0 (padding)
+    ext zk = gl::ext_pow(zi, lo);
+    for (uint32_t i = 0; i < per; i++) {
+      const uint32_t k = lo + i;
+      ext q = gl::ext_mul(gl::ext_add(d[i], after), zk);  // S_k z^-k = q_{k-1}
+      zk = gl::ext_mul(zk, zi);
+      if (pass == 0) {
+        res[i] = q;
+      } else {
+        res[i] = gl::ext_add(res[i], q);
+      }
+      (void)k;
+    }
+    if (pass == 0) {
+      const ext ap{ch[CH_ALPHA_POW_NC], ch[CH_ALPHA_POW_NC + 1]};
+      for (uint32_t i = 0; i < per; i++) res[i] = gl::ext_mul(res[i], ap);
+    }
+  }
+  // res[i] at k = lo+i holds q_{k-1}; shift down by one, q_{n-1} = 0
+  uint64_t *o = fin + b * f_bstride;
+  for (uint32_t i = 0; i < per; i++) {
+    const uint32_t k = lo + i;
+    if (k == 0) continue;
+    o[k - 1] = res[i].c0;
+    o[f_cstride + k - 1] = res[i].c1;
+  }
+  if (threadIdx.x == T - 1) {
+    o[n - 1] = 0;
+    o[f_cstride + n - 1] = 0;
+  }
+}
+
+// FRI layer leaves: leaf i = 2^ab consecutive leaf-order ext values, interleaved c0,c1
+__global__ void __launch_bounds__(256) k_fri_leaf(const uint64_t *__restrict__ vals, uint64_t *__restrict__ dig,
+                                                  uint32_t log_len, uint32_t ab, uint64_t v_bstride, uint64_t d_bstride) {
+  const uint32_t nleaves = 1u << (log_len - ab);
+  const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= nleaves) return;
+  const uint32_t b = blockIdx.y;
+  const uint64_t L = 1ull << log_len;
+  const uint64_t *c0 = vals + b * v_bstride + ((uint64_t)i << ab);
+  const uint64_t *c1 = c0 + L;
+  const uint32_t W = 2u << ab;
+  uint64_t s[12] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0};
+  for (uint32_t off = 0; off < W; off += 8) {
+#pragma unroll
+    for (uint32_t k = 0; k < 8; k += 2) {
+      const uint32_t e = (off + k) >> 1;
+      if (off + k < W) {
+        s[k] = c0[e];
+        s[k + 1] = c1[e];
+      }
+    }
+    ps::permute(s);
+  }
+  uint64_t *o = dig + b * d_bstride + (uint64_t)i * 4;
+  o[0] = s[0]; o[1] = s[1]; o[2] = s[2]; o[3] = s[3];
+}
+
+// fold: out[k] = sum_{i<2^ab} beta^i c[2^ab k + i]  (coefficients, ext as 2 columns)
+__global__ void __launch_bounds__(256) k_fold(const uint64_t *__restrict__ cin, uint64_t *__restrict__ cout,
+                                              uint32_t log_len, uint32_t ab, uint32_t layer,
+                                              const uint64_t *__restrict__ chal, uint64_t i_bstride,
+                                              uint64_t o_bstride) {
+  const uint32_t nout = 1u << (log_len - ab);
+  const uint32_t k = blockIdx.x * blockDim.x + threadIdx.x;
+  if (k >= nout) return;
+  const uint32_t b = blockIdx.y;
+  const uint64_t *ch = chal + b * CHAL_STRIDE;
+  const ext beta{ch[CH_FRI_BETA + 2 * layer], ch[CH_FRI_BETA + 2 * layer + 1]};
+  const uint64_t L = 1ull << log_len;
+  const uint64_t *c0 = cin + b * i_bstride, *c1 = c0 + L;
+  ext acc{0, 0};
+  for (uint32_t i = 1u << ab; i-- > 0;) {
+    const uint64_t idx = ((uint64_t)k << ab) + i;
+    acc = gl::ext_add(gl::ext_mul(acc, beta), ext{c0[idx], c1[idx]});
+  }
+  uint64_t *o = cout + b * o_bstride;
+  o[k] = acc.c0;
+  o[nout + k] = acc.c1;
+}
+
+// ---------------------------------------------------------------- a12
+
+__global__ void __launch_bounds__(256) k_pow(const uint64_t *__restrict__ states, const uint32_t *__restrict__ pos,
+                                             uint64_t *__restrict__ found, uint64_t base, uint32_t bits) {
+  const uint32_t b = blockIdx.y;
+  if (found[b] != ~0ull && found[b] < base) return;
+  const uint64_t cand = base + (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  uint64_t s[12];
+#pragma unroll
+  for (int i = 0; i < 12; i++) s[i] = states[b * 12 + i];
+  const uint32_t ps_ = pos[b];
+#pragma unroll
+  for (int i = 0; i < 8; i++)
+    if ((uint32_t)i == ps_) s[i] = cand;
+  ps::permute(s);
+  if ((s[7] >> (64 - bits)) == 0) atomicMin((unsigned long long *)&found[b], (unsigned long long)cand);
+}
+
+// ---------------------------------------------------------------- gathers
+
+// out[b][q][c] = cols[b*bstride + c*stride + idx[b][q] >> shift]
+__global__ void k_gather_rows_b(const uint64_t *__restrict__ cols, uint64_t stride, uint64_t bstride, uint32_t ncols,
+                                const uint32_t *__restrict__ idx, uint32_t nq, uint32_t shift,
+                                uint64_t *__restrict__ out, uint64_t o_bstride) {
+  const uint32_t t = blockIdx.x * blockDim.x + threadIdx.x;
+  const uint32_t b = blockIdx.y;
+  if (t >= ncols * nq) return;
+  const uint32_t q = t / ncols, c = t % ncols;
+  out[b * o_bstride + t] = cols[b * bstride + (uint64_t)c * stride + (idx[b * nq + q] >> shift)];
+}
+
+// out[b][q][k][4] = sibling digest at level k of leaf idx[b][q] >> shift
+__global__ void k_gather_paths_b(const uint64_t *__restrict__ dig, uint64_t d_bstride, uint32_t log_leaves,
+                                 uint32_t cap_h, const uint32_t *__restrict__ idx, uint32_t nq, uint32_t shift,
+                                 uint64_t *__restrict__ out, uint64_t o_bstride) {
+  const uint32_t depth = log_leaves - cap_h;
+  const uint32_t t = blockIdx.x * blockDim.x + threadIdx.x;
+  const uint32_t b = blockIdx.y;
+  if (t >= nq * depth * 4) return;
+  const uint32_t q = t / (depth * 4), r = t % (depth * 4), k = r / 4, e = r % 4;
+  uint64_t off = 0;
+  for (uint32_t j = 0; j < k; j++) off += (uint64_t)1 << (log_leaves - j);
+  const uint64_t leaf = idx[b * nq + q] >> shift;
+  const uint64_t sib = (leaf >> k) ^ 1u;
+  out[b * o_bstride + t] = dig[b * d_bstride + (off + sib) * 4 + e];
+}
+
+// FRI layer leaves for queries: out[b][q][2*arity] interleaved from 2 columns
+__global__ void k_gather_fri_leaf(const uint64_t *__restrict__ vals, uint64_t v_bstride, uint32_t log_len, uint32_t ab,
+                                  const uint32_t *__restrict__ idx, uint32_t nq, uint32_t shift,
+                                  uint64_t *__restrict__ out, uint64_t o_bstride) {
+  const uint32_t W = 2u << ab;
+  const uint32_t t = blockIdx.x * blockDim.x + threadIdx.x;
+  const uint32_t b = blockIdx.y;
+  if (t >= nq * W) return;
+  const uint32_t q = t / W, e = t % W;
+  const uint64_t leaf = idx[b * nq + q] >> shift;
+  const uint64_t L = 1ull << log_len;
+  out[b * o_bstride + t] = vals[b * v_bstride + (e & 1) * L + (leaf << ab) + (e >> 1)];
+}
+
+}  // namespace qpk

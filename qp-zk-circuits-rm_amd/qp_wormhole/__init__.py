@@ -8,4 +8,9 @@ only backend: importing the native pieces raises if it is not built.
 from ._native import (Context, PolynomialBatch, QpError, header_symbols, ifft, lde, lib,  # noqa: F401
                       poseidon_permute)
 
-__all__ = ["Context", "PolynomialBatch", "QpError", "ifft", "lde", "poseidon_permute", "lib", "header_symbols"]
+from .circuits import (Circuit, CircuitInputs, PrivateCircuitInputs, ProcessedStorageProof,  # noqa: F401,E402
+                       PublicCircuitInputs, Witness)
+from .prover import Prover, ProofWithPublicInputs, WormholeProver  # noqa: F401,E402
+
+__all__ = ["Circuit", "CircuitInputs", "PrivateCircuitInputs", "ProcessedStorageProof", "PublicCircuitInputs",
+           "Witness", "Prover", "ProofWithPublicInputs", "WormholeProver", "Context", "PolynomialBatch", "QpError", "ifft", "lde", "poseidon_permute", "lib", "header_symbols"]

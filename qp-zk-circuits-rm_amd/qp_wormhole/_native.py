@@ -75,6 +75,17 @@ def lib():
         "qp_witness_wires": (ctypes.c_int, [VP, U64P]),
         "qp_witness_public_inputs": (ctypes.c_int, [VP, U64P, ctypes.c_uint32, ctypes.POINTER(ctypes.c_uint32)]),
         "qp_witness_free": (None, [VP]),
+        "qp_hash_no_pad": (ctypes.c_int, [U64P, ctypes.c_size_t, U64P]),
+        "qp_prover_new": (ctypes.c_int, [VP, VP, ctypes.c_uint32, PP]),
+        "qp_prover_free": (None, [VP]),
+        "qp_prover_proof_size": (ctypes.c_int, [VP, ctypes.POINTER(ctypes.c_size_t)]),
+        "qp_prover_verifier_data": (ctypes.c_int, [VP, ctypes.c_char_p, ctypes.c_size_t,
+                                                   ctypes.POINTER(ctypes.c_size_t)]),
+        "qp_prover_prove": (ctypes.c_int, [VP, ctypes.POINTER(ctypes.c_void_p), ctypes.c_uint32, ctypes.c_char_p,
+                                           ctypes.c_size_t, ctypes.POINTER(ctypes.c_size_t)]),
+        "qp_prover_prove_wires": (ctypes.c_int, [VP, U64P, U64P, ctypes.c_uint32, ctypes.c_char_p, ctypes.c_size_t,
+                                                 ctypes.POINTER(ctypes.c_size_t)]),
+        "qp_prover_stage_times": (ctypes.c_int, [VP, ctypes.POINTER(ctypes.c_double), ctypes.c_uint32, ctypes.c_int]),
     }
     for name, (res, args) in sig.items():
         f = getattr(L, name)
@@ -201,3 +212,13 @@ def poseidon_permute(ctx, states):
     s = np.ascontiguousarray(states, dtype=np.uint64).copy()
     ctx.check(lib().qp_poseidon_permute(ctx.h, s, s.shape[0]), "qp_poseidon_permute")
     return s
+
+
+def hash_no_pad(values):
+    """PoseidonHash::hash_no_pad on the host (libqpgpu host code)."""
+    a = np.ascontiguousarray(values, dtype=np.uint64)
+    out = np.zeros(4, np.uint64)
+    rc = lib().qp_hash_no_pad(a, len(a), out)
+    if rc:
+        raise QpError(rc, "qp_hash_no_pad")
+    return [int(x) for x in out]

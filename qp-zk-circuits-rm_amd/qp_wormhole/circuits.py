@@ -30,6 +30,11 @@ class ProcessedStorageProof:
     proof: List[bytes] = field(default_factory=list)
     indices: List[int] = field(default_factory=list)
 
+    def validate(self):
+        if len(self.proof) != len(self.indices):
+            raise ValueError("indices length must be equal to proof length, actual lengths: "
+                             f"{len(self.proof)}, {len(self.indices)}")
+
 
 @dataclass
 class PublicCircuitInputs:
@@ -64,6 +69,7 @@ class CircuitInputs:
         s.funding_account[:] = list(self.private.funding_account)
         s.unspendable_account[:] = list(self.private.unspendable_account)
         sp = self.private.storage_proof
+        sp.validate()
         n = len(sp.proof)
         s.num_nodes = n
         keep = [bytes(p) for p in sp.proof]

@@ -1,0 +1,122 @@
+"""Device prover and the WormholeProver mirror.
+
+`Prover` wraps qp_prover (include/qpgpu.h): B proofs of one circuit per call on
+one MI355X.  `WormholeProver` mirrors qp-wormhole-prover's API
+(wormhole/prover/src/lib.rs:74-237): new(config) -> commit(inputs) -> prove(),
+single use, commit twice is an error, prove before commit is an error.
+"""
+import ctypes
+import threading
+
+import numpy as np
+
+from ._native import Context, QpError, lib
+from .circuits import Circuit, CircuitInputs
+
+STAGES = ["commit_wires", "zs_pp", "quotient", "openings", "fri", "pow", "queries", "serialize"]
+
+
+class ProofWithPublicInputs:
+    """Serialized plonky2 ProofWithPublicInputs (ProofWithPublicInputs::to_bytes)."""
+
+    def __init__(self, data: bytes, public_inputs):
+        self.data = data
+        self.public_inputs = [int(x) for x in public_inputs]
+
+    def to_bytes(self):
+        return self.data
+
+
+class Prover:
+    def __init__(self, ctx: Context, circuit: Circuit, max_batch=1):
+        self.ctx, self.circuit, self.max_batch = ctx, circuit, max_batch
+        h = ctypes.c_void_p()
+        ctx.check(lib().qp_prover_new(ctx.h, circuit.h, max_batch, ctypes.byref(h)), "qp_prover_new")
+        self.h = h
+        ln = ctypes.c_size_t()
+        lib().qp_prover_proof_size(self.h, ctypes.byref(ln))
+        self.proof_size = ln.value
+
+    def verifier_data(self):
+        ln = ctypes.c_size_t()
+        lib().qp_prover_verifier_data(self.h, None, 0, ctypes.byref(ln))
+        buf = ctypes.create_string_buffer(ln.value)
+        self.ctx.check(lib().qp_prover_verifier_data(self.h, buf, ln.value, ctypes.byref(ln)), "verifier_data")
+        return buf.raw[:ln.value]
+
+    def prove_witnesses(self, witnesses):
+        nb = len(witnesses)
+        arr = (ctypes.c_void_p * nb)(*[w.h.value for w in witnesses])
+        out = ctypes.create_string_buffer(self.proof_size * nb)
+        lens = (ctypes.c_size_t * nb)()
+        self.ctx.check(lib().qp_prover_prove(self.h, arr, nb, out, self.proof_size, lens), "qp_prover_prove")
+        raw = out.raw
+        return [raw[i * self.proof_size:i * self.proof_size + lens[i]] for i in range(nb)]
+
+    def prove_wires(self, wires, pis):
+        wires = np.ascontiguousarray(wires, dtype=np.uint64)
+        pis = np.ascontiguousarray(pis, dtype=np.uint64)
+        nb = wires.shape[0]
+        out = ctypes.create_string_buffer(self.proof_size * nb)
+        lens = (ctypes.c_size_t * nb)()
+        self.ctx.check(lib().qp_prover_prove_wires(self.h, wires, pis, nb, out, self.proof_size, lens),
+                       "qp_prover_prove_wires")
+        raw = out.raw
+        return [raw[i * self.proof_size:i * self.proof_size + lens[i]] for i in range(nb)]
+
+    def stage_times(self, reset=False):
+        ms = (ctypes.c_double * 16)()
+        lib().qp_prover_stage_times(self.h, ms, 16, int(reset))
+        return dict(zip(STAGES, list(ms)[:len(STAGES)]))
+
+    def free(self):
+        if self.h:
+            lib().qp_prover_free(self.h)
+            self.h = None
+
+    def __del__(self):
+        try:
+            self.free()
+        except Exception:
+            pass
+
+
+_cache = {}
+_lock = threading.Lock()
+
+
+def _shared(config, device):
+    """Circuit + device prover per (config, device): the reference rebuilds in
+    WormholeProver::new; here the built circuit and its device preprocessing are
+    cached (the role of generated-bins/ in WormholeProver::default, lib.rs:81-101)."""
+    key = (config, device)
+    with _lock:
+        if key not in _cache:
+            ctx = Context(device)
+            circ = Circuit.wormhole(zero_knowledge=(config == "standard_recursion_zk_config"))
+            _cache[key] = (ctx, circ, Prover(ctx, circ, 1))
+        return _cache[key]
+
+
+class WormholeProver:
+    def __init__(self, config="standard_recursion_config", device=0):
+        if config not in ("standard_recursion_config", "standard_recursion_zk_config"):
+            raise ValueError(f"unknown circuit config {config!r}")
+        self.ctx, self.circuit, self.prover = _shared(config, device)
+        self._witness = None
+        self._committed = False
+
+    def commit(self, inputs: CircuitInputs):
+        if self._committed:
+            raise QpError(4, "prover has already commited to inputs")
+        self._witness = self.circuit.commit(inputs)
+        self._committed = True
+        return self
+
+    def prove(self) -> ProofWithPublicInputs:
+        if self._witness is None:
+            raise QpError(4, "prover has not commited to any inputs")
+        w = self._witness
+        self._witness = None
+        data = self.prover.prove_witnesses([w])[0]
+        return ProofWithPublicInputs(data, w.public_inputs())
