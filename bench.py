@@ -1,0 +1,178 @@
+"""bench.py — Wormhole proofs/sec on MI355X (BASELINE.json metric).
+
+One step = prove() of one batch of B synthetic Wormhole witnesses per GPU
+(BASELINE.json configs[2]: "Batch 256 Wormhole proofs on 1xMI355X").  The
+committed wire matrices (the output of WormholeProver::commit's witness
+generation) are resident in HBM before the timed region; each step runs the
+full prover (commitments, permutation argument, quotient, openings, FRI, PoW,
+query openings) and returns serialized proofs to the host.  With N GPUs each
+rank proves its own batch (independent proofs, weak scaling) and the leaf proof
+bytes are gathered to rank 0 over RCCL (the aggregator's input).
+
+Also reported (one JSON line, rank 0):
+  roofline      the wires LDE (NTT) kernel: algorithmic bytes 8*(n+N) per column
+                / its HIP-event-timed duration, vs the 8 TB/s HBM3E peak
+  cpu_baseline  the CPU restatement of the same prover (oracle/prover.c, "port";
+                the Rust reference cannot be built here) on a bounded sample
+"""
+import argparse
+import ctypes
+import json
+import os
+import sys
+import time
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, os.path.join(ROOT, "qp-zk-circuits-rm_amd"))
+sys.path.insert(0, os.path.join(ROOT, "tests"))
+
+HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec peak (MI355X_MICROARCH.md)
+
+
+def parse():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=3)
+    ap.add_argument("--warmup", type=int, default=1)
+    ap.add_argument("--batch", type=int, default=256, help="proofs per GPU per step")
+    ap.add_argument("--cpu-sample", type=int, default=2, help="proofs in the CPU baseline sample (0 = skip)")
+    return ap.parse_args()
+
+
+def make_witnesses(circuit, first, count):
+    from qp_wormhole.synthetic import synthetic_inputs
+    n, W = circuit.n, circuit.num_wires
+    wires = np.empty((count, W, n), np.uint64)
+    pis = np.empty((count, circuit.num_public_inputs), np.uint64)
+    for i in range(count):
+        w = circuit.commit(synthetic_inputs(first + i))
+        wires[i] = w.wires()
+        pis[i] = w.public_inputs()
+        w.free()
+    return wires, pis
+
+
+def cpu_baseline(circuit, wires, pis, sample):
+    """oracle/prover.c (C + OpenMP restatement of plonky2 prove) on `sample` proofs."""
+    from oracle_lib import U64P, lib as olib
+    L = olib()
+    L.ora_prove.argtypes = [ctypes.c_char_p, ctypes.c_size_t, U64P, U64P, U64P, ctypes.c_size_t, ctypes.c_char_p,
+                            ctypes.c_size_t, ctypes.POINTER(ctypes.c_size_t), U64P, U64P]
+    cb = circuit.common_data()
+    cs = circuit.constants_sigmas()
+    out = ctypes.create_string_buffer(400000)
+    ln = ctypes.c_size_t()
+    cap = np.zeros(64, np.uint64)
+    dig = np.zeros(4, np.uint64)
+    t = time.perf_counter()
+    for i in range(sample):
+        rc = L.ora_prove(cb, len(cb), cs, np.ascontiguousarray(wires[i]), np.ascontiguousarray(pis[i]),
+                         pis.shape[1], out, 400000, ctypes.byref(ln), cap, dig)
+        assert rc == 0
+    dt = time.perf_counter() - t
+    cores = int(os.environ.get("OMP_NUM_THREADS", os.cpu_count() or 1))
+    return {"value": sample / dt, "unit": "proofs/s", "cores": cores, "kind": "port",
+            "sample": f"{sample} Wormhole proofs (deg 13, standard_recursion_config), C+OpenMP restatement "
+                      f"oracle/prover.c, {dt:.1f} s"}
+
+
+def main():
+    args = parse()
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    import torch
+    dist = None
+    if world > 1:
+        import torch.distributed as dist
+        torch.cuda.set_device(local)
+        dist.init_process_group("nccl")
+    import qp_wormhole
+
+    circuit = qp_wormhole.Circuit.wormhole(zero_knowledge=False)
+    B = args.batch
+    wires, pis = make_witnesses(circuit, rank * B, B)
+    ctx = qp_wormhole.Context(local)
+    prover = qp_wormhole.Prover(ctx, circuit, max_batch=B)
+    d_wires = torch.from_numpy(wires.view(np.int64)).to(f"cuda:{local}")
+    torch.cuda.synchronize()
+
+    def step():
+        proofs = prover.prove_wires_dev(d_wires.data_ptr(), pis, B)
+        if dist is not None:
+            blob = np.frombuffer(b"".join(proofs), np.uint8)
+            t = torch.from_numpy(blob.copy()).to(f"cuda:{local}")
+            gathered = [torch.empty_like(t) for _ in range(world)] if rank == 0 else None
+            dist.gather(t, gathered, dst=0)
+        return proofs
+
+    for _ in range(args.warmup):
+        proofs = step()
+    # proofs of the warmup verify (rank 0 checks one with the oracle verifier)
+    verified = None
+    if rank == 0 and args.warmup:
+        from oracle_lib import lib as olib
+        vd = prover.verifier_data()
+        verified = olib().ora_verify(vd, len(vd), proofs[0], len(proofs[0])) == 0
+    prover.set_timing(True)
+    prover.kernel_stats(reset=True)
+    prover.stage_times(reset=True)
+    if dist is not None:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        step()
+    torch.cuda.synchronize()
+    if dist is not None:
+        dist.barrier()
+    dt = time.perf_counter() - t0
+    if dist is not None:
+        tt = torch.tensor([dt], dtype=torch.float64, device=f"cuda:{local}")
+        dist.all_reduce(tt, op=dist.ReduceOp.MAX)
+        dt = float(tt.item())
+    ks = prover.kernel_stats()
+    stages = prover.stage_times()
+    if rank == 0:
+        total = world * B * args.steps
+        lde = ks["lde_wires"]
+        achieved = lde["units"] / (lde["ms"] * 1e-3) / 1e9 if lde["ms"] else None
+        leaf = ks["leaf_hash_wires"]
+        rec = {
+            "metric": "Wormhole proofs/sec (whole node)",
+            "value": total / dt,
+            "unit": "proofs/s",
+            "n_gpus": world,
+            "steps": args.steps,
+            "warmup": args.warmup,
+            "ms_per_step": dt / args.steps * 1e3,
+            "higher_is_better": True,
+            "scaling": "weak",
+            "vs_baseline": None,
+            "dtype": "u64 (Goldilocks field)",
+            "data": "synthetic seeded Wormhole witnesses (SURVEY 8d), native circuit, standard_recursion_config",
+            "config": {"workload": f"batch{B}_wormhole_proofs_per_gpu", "circuit": "wormhole deg13 (135 wires)",
+                       "batch_per_gpu": B, "parallelism": f"proofs sharded x{world}, RCCL gather of leaf proofs"},
+            "roofline": {"kernel": "k_lde (wires LDE, 135 cols x 2^13 -> 2^16)", "bound": "hbm",
+                         "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                         "frac": achieved / HBM_PEAK_GBS if achieved else None, "traffic": None,
+                         "avg_launch_ms": lde["ms"] / max(lde["launches"], 1)},
+            "valu_kernels": {"leaf_hash_wires_perms_per_s": leaf["units"] / (leaf["ms"] * 1e-3) if leaf["ms"] else None,
+                             "avg_launch_ms": leaf["ms"] / max(leaf["launches"], 1),
+                             "quotient_avg_launch_ms": ks["quotient"]["ms"] / max(ks["quotient"]["launches"], 1)},
+            "stage_ms_per_step": {k: v / args.steps for k, v in stages.items()},
+            "proof_bytes": len(proofs[0]),
+            "warmup_proof_verified": verified,
+        }
+        if world == 1 and args.cpu_sample > 0:
+            rec["cpu_baseline"] = cpu_baseline(circuit, wires, pis, args.cpu_sample)
+        print(json.dumps(rec), flush=True)
+    prover.free()
+    if dist is not None:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

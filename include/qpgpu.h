@@ -165,6 +165,16 @@ int qp_prover_prove(qp_prover *p, const qp_witness *const *w, uint32_t nproofs, 
 /* prove from raw wire matrices [nproofs][num_wires][n] + public inputs [nproofs][npis] */
 int qp_prover_prove_wires(qp_prover *p, const uint64_t *wires, const uint64_t *pis, uint32_t nproofs, uint8_t *out,
                           size_t stride, size_t *lens);
+/* same, with the wire matrices already resident on the device:
+ * d_wires = device pointer [nproofs][num_wires][n]; pis on the host          */
+int qp_prover_prove_wires_dev(qp_prover *p, const uint64_t *d_wires, const uint64_t *pis, uint32_t nproofs,
+                              uint8_t *out, size_t stride, size_t *lens);
+/* HIP-event timing of the hot kernels on the prover's stream (off by default):
+ * slot 0 = wires LDE (NTT; units = algorithmic bytes 8*(n+N) per column),
+ * 1 = wires leaf hashing (units = permutations), 2 = wires Merkle levels
+ * (units = permutations), 3 = quotient evaluation (units = LDE points)     */
+int qp_prover_set_timing(qp_prover *p, int enable);
+int qp_prover_kernel_stats(qp_prover *p, double *ms, double *units, uint64_t *launches, uint32_t n, int reset);
 /* accumulated host wall time per stage (ms): commit wires, zs, quotient, openings,
  * FRI, PoW, queries, serialize; reset != 0 clears */
 int qp_prover_stage_times(qp_prover *p, double *ms, uint32_t n, int reset);

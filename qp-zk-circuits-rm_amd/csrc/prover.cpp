@@ -98,6 +98,16 @@ struct qp_prover {
   std::vector<uint32_t> h_qidx, h_pos;
   size_t proof_len = 0;
   double stage_ms[16] = {0};
+  // optional per-kernel HIP-event timing on the prover's stream
+  bool timing = false;
+  struct KT {
+    hipEvent_t a = nullptr, b = nullptr;
+    double ms = 0, units = 0;
+    uint64_t launches = 0;
+    bool pending = false;
+    double pend_units = 0;
+  } kt[8];
+  const uint64_t *ext_wires = nullptr;  // device-resident wires for prove_wires_dev
 };
 
 namespace {
@@ -264,6 +274,37 @@ int setup(qp_prover *P) {
   return QP_OK;
 }
 
+// kernel timers: 0 = LDE of the wires (NTT), 1 = leaf hashing of the wires,
+// 2 = Merkle tree levels of the wires, 3 = quotient evaluation
+void kt_begin(qp_prover *P, int k) {
+  if (!P->timing) return;
+  auto &t = P->kt[k];
+  if (!t.a) {
+    (void)hipEventCreate(&t.a);
+    (void)hipEventCreate(&t.b);
+  }
+  (void)hipEventRecord(t.a, P->ctx->stream);
+}
+void kt_end(qp_prover *P, int k, double units) {
+  if (!P->timing) return;
+  auto &t = P->kt[k];
+  (void)hipEventRecord(t.b, P->ctx->stream);
+  t.pending = true;
+  t.pend_units = units;
+}
+void kt_collect(qp_prover *P) {  // after a stream sync
+  for (auto &t : P->kt)
+    if (t.pending) {
+      float ms = 0;
+      if (hipEventElapsedTime(&ms, t.a, t.b) == hipSuccess) {
+        t.ms += ms;
+        t.units += t.pend_units;
+        t.launches++;
+      }
+      t.pending = false;
+    }
+}
+
 int fetch_caps(qp_prover *P, const uint64_t *dig_base, uint64_t dbs, uint32_t log_leaves, uint32_t nb) {
   qp_ctx *c = P->ctx;
   const uint64_t off = qpk::tree_level_offset(log_leaves, log_leaves - P->cap_h) * 4;
@@ -271,6 +312,7 @@ int fetch_caps(qp_prover *P, const uint64_t *dig_base, uint64_t dbs, uint32_t lo
   TRY(hipMemcpy2DAsync(P->h_caps.data(), cw * 8, dig_base + off, dbs * 8, cw * 8, nb, hipMemcpyDeviceToHost,
                        c->stream));
   TRY(hipStreamSynchronize(c->stream));
+  kt_collect(P);
   return QP_OK;
 }
 
@@ -309,10 +351,28 @@ int prove_batch(qp_prover *P, const uint64_t *const *wires_host, const uint64_t 
   TRY(hipSetDevice(c->device));
   int rc;
 
-  // ---- 1. wires commitment
-  for (uint32_t b = 0; b < nb; b++)
-    TRY(hipMemcpyAsync(P->wires.vals.p + b * P->wires.cbs(), wires_host[b], P->wires.cbs() * 8, hipMemcpyHostToDevice, s));
-  P->wires.build_from_values(c, nb);
+  // ---- 1. wires commitment (values already on the device for prove_wires_dev)
+  uint64_t *vals_save = P->wires.vals.p;
+  if (P->ext_wires) {
+    P->wires.vals.p = const_cast<uint64_t *>(P->ext_wires);
+  } else {
+    for (uint32_t b = 0; b < nb; b++)
+      TRY(hipMemcpyAsync(P->wires.vals.p + b * P->wires.cbs(), wires_host[b], P->wires.cbs() * 8,
+                         hipMemcpyHostToDevice, s));
+  }
+  {
+    Tree &t = P->wires;
+    qpk::intt(c->tw, t.vals.p, t.n(), t.coeffs.p, t.n(), t.npolys, t.log_n, nb, t.cbs(), t.cbs(), s);
+    kt_begin(P, 0);
+    qpk::lde(c->tw, t.coeffs.p, t.n(), t.lde.p, t.N(), t.npolys, t.log_n, t.rate_bits, gl::GEN, nb, t.cbs(), t.lbs(), s);
+    kt_end(P, 0, (double)nb * t.npolys * 8.0 * (double)(t.n() + t.N()));
+    kt_begin(P, 1);
+    qpk::leaf_hash(t.lde.p, t.N(), t.npolys, nullptr, 0, t.dig.p, (uint32_t)t.N(), nb, t.lbs(), 0, t.dbs(), s);
+    kt_end(P, 1, (double)nb * t.N() * ((t.npolys + 7) / 8));
+    kt_begin(P, 2);
+    qpk::merkle_tree(t.dig.p, t.log_n + t.rate_bits, t.cap_h, nb, t.dbs(), s);
+    kt_end(P, 2, (double)nb * (t.N() - (1u << t.cap_h)));
+  }
   TRY(hipGetLastError());
   if ((rc = fetch_caps(P, P->wires.dig.p, P->wires.dbs(), logN, nb))) return rc;
   P->pool->parallel_for(nb, [&](size_t b) {
@@ -337,6 +397,7 @@ int prove_batch(qp_prover *P, const uint64_t *const *wires_host, const uint64_t 
   qpk::k_z_scan<<<dim3(nc, nb), 1024, 0, s>>>(P->prods.p, P->zs.vals.p, P->log_n, nc, P->nchunks, pbs, P->zs.cbs());
   P->zs.build_from_values(c, nb);
   TRY(hipGetLastError());
+  P->wires.vals.p = vals_save;
   if ((rc = fetch_caps(P, P->zs.dig.p, P->zs.dbs(), logN, nb))) return rc;
   P->pool->parallel_for(nb, [&](size_t b) {
     ProofState &S = st[b];
@@ -373,7 +434,9 @@ int prove_batch(qp_prover *P, const uint64_t *const *wires_host, const uint64_t 
     a.qdf = P->qdf;
     a.num_constants = P->NC;
     a.g = P->gdesc;
+    kt_begin(P, 3);
     qpk::k_quotient<<<dim3(cdiv(N, 256), nb), 256, 0, s>>>(a);
+    kt_end(P, 3, (double)nb * N);
     const uint64_t n_inv = gl::inv(n);
     qpk::k_qintt_blocks<<<dim3(B, nc, nb), 512, 8u << P->log_n, s>>>(P->qvals.p, P->cbuf.p, P->log_n, P->rate_bits,
                                                                      (uint64_t)nc * N, (uint64_t)nc * N, c->tw.fwd,
@@ -760,6 +823,53 @@ int qp_prover_prove(qp_prover *P, const qp_witness *const *w, uint32_t nproofs, 
     } catch (const std::bad_alloc &) {
       rc = QP_ERR_OOM;
     }
+    if (rc) return rc;
+    done += nb;
+  }
+  return QP_OK;
+}
+
+int qp_prover_set_timing(qp_prover *P, int enable) {
+  if (!P) return QP_ERR_ARG;
+  P->timing = enable != 0;
+  return QP_OK;
+}
+
+int qp_prover_kernel_stats(qp_prover *P, double *ms, double *units, uint64_t *launches, uint32_t n, int reset) {
+  if (!P) return QP_ERR_ARG;
+  for (uint32_t i = 0; i < n && i < 8; i++) {
+    if (ms) ms[i] = P->kt[i].ms;
+    if (units) units[i] = P->kt[i].units;
+    if (launches) launches[i] = P->kt[i].launches;
+    if (reset) {
+      P->kt[i].ms = 0;
+      P->kt[i].units = 0;
+      P->kt[i].launches = 0;
+    }
+  }
+  return QP_OK;
+}
+
+int qp_prover_prove_wires_dev(qp_prover *P, const uint64_t *d_wires, const uint64_t *pis, uint32_t nproofs,
+                              uint8_t *out, size_t stride, size_t *lens) {
+  if (!P || !d_wires || !pis || !out || !nproofs) return QP_ERR_ARG;
+  if (stride < P->proof_len) {
+    P->ctx->err = "output stride smaller than the proof size";
+    return QP_ERR_ARG;
+  }
+  const uint64_t wsz = (uint64_t)P->W << P->log_n;
+  for (uint32_t done = 0; done < nproofs;) {
+    const uint32_t nb = std::min(P->max_batch, nproofs - done);
+    std::vector<const uint64_t *> wp(nb, nullptr), pp(nb);
+    for (uint32_t b = 0; b < nb; b++) pp[b] = pis + (uint64_t)(done + b) * P->npis;
+    P->ext_wires = d_wires + (uint64_t)done * wsz;
+    int rc;
+    try {
+      rc = prove_batch(P, wp.data(), pp.data(), nb, out + (size_t)done * stride, stride, lens ? lens + done : nullptr);
+    } catch (const std::bad_alloc &) {
+      rc = QP_ERR_OOM;
+    }
+    P->ext_wires = nullptr;
     if (rc) return rc;
     done += nb;
   }

@@ -64,6 +64,27 @@ class Prover:
         raw = out.raw
         return [raw[i * self.proof_size:i * self.proof_size + lens[i]] for i in range(nb)]
 
+    def prove_wires_dev(self, d_wires_ptr, pis, nproofs):
+        """wires already resident on the device (device pointer [nproofs][W][n])."""
+        pis = np.ascontiguousarray(pis, dtype=np.uint64)
+        out = ctypes.create_string_buffer(self.proof_size * nproofs)
+        lens = (ctypes.c_size_t * nproofs)()
+        self.ctx.check(lib().qp_prover_prove_wires_dev(self.h, d_wires_ptr, pis, nproofs, out, self.proof_size, lens),
+                       "qp_prover_prove_wires_dev")
+        raw = out.raw
+        return [raw[i * self.proof_size:i * self.proof_size + lens[i]] for i in range(nproofs)]
+
+    def set_timing(self, enable=True):
+        lib().qp_prover_set_timing(self.h, int(enable))
+
+    def kernel_stats(self, reset=False):
+        ms = (ctypes.c_double * 8)()
+        units = (ctypes.c_double * 8)()
+        cnt = (ctypes.c_uint64 * 8)()
+        lib().qp_prover_kernel_stats(self.h, ms, units, cnt, 8, int(reset))
+        names = ["lde_wires", "leaf_hash_wires", "merkle_wires", "quotient"]
+        return {nm: {"ms": ms[i], "units": units[i], "launches": cnt[i]} for i, nm in enumerate(names)}
+
     def stage_times(self, reset=False):
         ms = (ctypes.c_double * 16)()
         lib().qp_prover_stage_times(self.h, ms, 16, int(reset))
