@@ -19,9 +19,9 @@ for s in "$@"; do
     oracle) step oracle 300 make -s -C oracle ;;
     test) step pytest_gpu 900 python -m pytest tests -m gpu -x -q ;;
     kbench) step kbench 300 python tools/kbench.py 8 5 ;;
-    prof) export TMPDIR=/tmp; step rocprof 600 rocprofv3 --kernel-trace --stats -d gpurun_out/prof -o run -- python3 tools/kbench.py 8 3 ;;
+    prof) export TMPDIR=/tmp; step rocprof 600 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/prof -o run -- python3 tools/kbench.py 8 3 ;;
     bench) step bench 900 python bench.py ;;
-    benchprof) export TMPDIR=/tmp; step rocprof_bench 900 rocprofv3 --kernel-trace --stats -d gpurun_out/prof_bench -o run -- python3 bench.py --steps 3 --warmup 1 ;;
+    benchprof) export TMPDIR=/tmp; step rocprof_bench 900 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/prof_bench -o run -- python3 bench.py --steps 2 --warmup 1 --cpu-sample 0 ;;
     *) echo "unknown step $s" ;;
   esac
 done
