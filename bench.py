@@ -99,13 +99,12 @@ def main():
     d_wires = torch.from_numpy(wires.view(np.int64)).to(f"cuda:{local}")
     torch.cuda.synchronize()
 
+    from qp_wormhole.distributed import gather_proofs
+
     def step():
         proofs = prover.prove_wires_dev(d_wires.data_ptr(), pis, B)
-        if dist is not None:
-            blob = np.frombuffer(b"".join(proofs), np.uint8)
-            t = torch.from_numpy(blob.copy()).to(f"cuda:{local}")
-            gathered = [torch.empty_like(t) for _ in range(world)] if rank == 0 else None
-            dist.gather(t, gathered, dst=0)
+        if dist is not None:  # leaf proofs -> aggregator rank over RCCL
+            gather_proofs(proofs, prover.proof_size, dist, device=f"cuda:{local}")
         return proofs
 
     for _ in range(args.warmup):

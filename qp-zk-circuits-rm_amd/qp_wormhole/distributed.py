@@ -1,0 +1,52 @@
+"""Multi-GPU plumbing: one process per GPU, proofs sharded by rank, leaf proofs
+gathered to the aggregator rank.
+
+Proofs are independent, so there is no collective on the data path; the only
+exchange is the gather of serialized leaf proofs (fixed size per circuit) to
+the rank that feeds the recursive aggregator
+(wormhole/aggregator/src/aggregator.rs:74-92).  torch.distributed backend
+"nccl" is RCCL over xGMI on MI355X; "gloo" is used for CPU tests.
+"""
+import numpy as np
+
+
+def shard(total: int, rank: int, world: int) -> range:
+    """Contiguous shard of proof indices [0, total) for `rank` (sizes differ by <= 1)."""
+    base, extra = divmod(total, world)
+    start = rank * base + min(rank, extra)
+    return range(start, start + base + (1 if rank < extra else 0))
+
+
+def pack_proofs(proofs, slot: int) -> np.ndarray:
+    """[n][8 + slot] uint8: little-endian length prefix + proof bytes (zero padded)."""
+    out = np.zeros((len(proofs), 8 + slot), np.uint8)
+    for i, p in enumerate(proofs):
+        if len(p) > slot:
+            raise ValueError(f"proof of {len(p)} bytes exceeds slot {slot}")
+        out[i, :8] = np.frombuffer(len(p).to_bytes(8, "little"), np.uint8)
+        out[i, 8:8 + len(p)] = np.frombuffer(p, np.uint8)
+    return out
+
+
+def unpack_proofs(arr: np.ndarray):
+    res = []
+    for row in arr:
+        n = int.from_bytes(row[:8].tobytes(), "little")
+        res.append(row[8:8 + n].tobytes())
+    return res
+
+
+def gather_proofs(proofs, slot: int, dist, device="cpu", dst: int = 0):
+    """Gather every rank's proofs to `dst` (rank order).  All ranks must pass the
+    same number of proofs (bench shards evenly); returns the list on dst, None elsewhere."""
+    import torch
+    t = torch.from_numpy(pack_proofs(proofs, slot)).to(device)
+    rank, world = dist.get_rank(), dist.get_world_size()
+    bufs = [torch.empty_like(t) for _ in range(world)] if rank == dst else None
+    dist.gather(t, bufs, dst=dst)
+    if rank != dst:
+        return None
+    out = []
+    for b in bufs:
+        out.extend(unpack_proofs(b.cpu().numpy()))
+    return out

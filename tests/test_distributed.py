@@ -1,0 +1,64 @@
+"""Multi-process path on CPU (gloo, world size 2): shard assignment and the
+leaf-proof gather that bench.py and the aggregator hand-off use over RCCL."""
+import os
+import socket
+
+import pytest
+
+from qp_wormhole.distributed import pack_proofs, shard, unpack_proofs
+
+
+@pytest.mark.parametrize("total", [0, 1, 7, 256, 2048])
+@pytest.mark.parametrize("world", [1, 2, 3, 8])
+def test_shards_partition_the_batch(total, world):
+    seen = []
+    for r in range(world):
+        s = shard(total, r, world)
+        seen.extend(s)
+        assert len(s) in (total // world, total // world + 1)
+    assert seen == list(range(total))
+
+
+def test_pack_roundtrip():
+    proofs = [bytes([i]) * (100 + i) for i in range(5)]
+    assert unpack_proofs(pack_proofs(proofs, 200)) == proofs
+    with pytest.raises(ValueError):
+        pack_proofs([b"x" * 300], 200)
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def _worker(rank, world, port, q):
+    import torch.distributed as dist
+    from qp_wormhole.distributed import gather_proofs
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    mine = [bytes([rank * 16 + i]) * (1000 + rank) for i in shard(8, rank, world)]
+    got = gather_proofs(mine, 2048, dist)
+    if rank == 0:
+        q.put(got)
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+def test_gather_world2_gloo():
+    import torch.multiprocessing as mp
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_worker, args=(r, 2, port, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    got = q.get(timeout=120)
+    for p in procs:
+        p.join(timeout=120)
+        assert p.exitcode == 0
+    expect = [bytes([r * 16 + i]) * (1000 + r) for r in range(2) for i in shard(8, r, 2)]
+    assert got == expect
