@@ -6,6 +6,7 @@
 // wave load.
 #include "field.h"
 #include "poseidon.h"
+#include "poseidon_dev.h"
 #include "kernels.h"
 
 namespace qpk {
@@ -31,11 +32,11 @@ __global__ void __launch_bounds__(256) k_leaf_hash(const uint64_t *__restrict__ 
         if (c < ncols) s[k] = cols[(uint64_t)c * stride + i];
         else if (c < W) s[k] = salt[(uint64_t)i * nsalt + (c - ncols)];
       }
-      ps::permute(s);
+      psd::permute_nc(s);
     }
   }
   uint64_t *o = dig + (uint64_t)i * 4;
-  o[0] = s[0]; o[1] = s[1]; o[2] = s[2]; o[3] = s[3];
+  o[0] = psd::canon(s[0]); o[1] = psd::canon(s[1]); o[2] = psd::canon(s[2]); o[3] = psd::canon(s[3]);
 }
 
 __global__ void __launch_bounds__(256) k_merkle_level(const uint64_t *__restrict__ prev, uint64_t *__restrict__ next,
@@ -49,9 +50,9 @@ __global__ void __launch_bounds__(256) k_merkle_level(const uint64_t *__restrict
 #pragma unroll
   for (int k = 0; k < 8; k++) s[k] = l[k];
   s[8] = s[9] = s[10] = s[11] = 0;
-  ps::permute(s);
+  psd::permute_nc(s);
   uint64_t *o = next + (uint64_t)i * 4;
-  o[0] = s[0]; o[1] = s[1]; o[2] = s[2]; o[3] = s[3];
+  o[0] = psd::canon(s[0]); o[1] = psd::canon(s[1]); o[2] = psd::canon(s[2]); o[3] = psd::canon(s[3]);
 }
 
 void leaf_hash(const uint64_t *cols, uint64_t stride, uint32_t ncols, const uint64_t *salt, uint32_t nsalt,
@@ -114,7 +115,7 @@ __global__ void __launch_bounds__(256) k_permute(uint64_t *states, uint64_t n) {
   uint64_t s[12];
 #pragma unroll
   for (int k = 0; k < 12; k++) s[k] = states[i * 12 + k];
-  ps::permute(s);
+  psd::permute(s);
 #pragma unroll
   for (int k = 0; k < 12; k++) states[i * 12 + k] = s[k];
 }

@@ -1,0 +1,109 @@
+// poseidon_dev.h — throughput form of the Poseidon permutation for gfx950
+// kernels (leaf hashing, Merkle levels, PoW).  Same function as ps::permute
+// (poseidon.h), different arithmetic discipline:
+//   * state kept NON-canonical in [0, 2^64) between rounds (one final
+//     canonicalisation of the lanes the caller reads), as plonky2's own
+//     Goldilocks backend does; field values are unchanged;
+//   * rounds fully unrolled in three phases so round constants are scalar
+//     operands and no loop/branch executes per round;
+//   * MDS: 32-bit halves times the small circulant constants accumulate in
+//     u64 (< 2^41), so each output lane needs one short reduction with a
+//     high word < 2^10 instead of a full 128-bit reduction.
+#pragma once
+#include "field.h"
+#include "poseidon.h"
+
+namespace psd {
+
+constexpr uint64_t EPS = 0xFFFFFFFFull;
+
+// a + c, a in [0,2^64), c canonical: result in [0,2^64), same field value
+__device__ __forceinline__ uint64_t add_nc(uint64_t a, uint64_t c) {
+  uint64_t s = a + c;
+  return s + (s < c ? EPS : 0);
+}
+
+// reduce lo + 2^64 hi (any hi) to [0, 2^64)
+__device__ __forceinline__ uint64_t reduce_nc(uint64_t lo, uint64_t hi) {
+  const uint64_t hh = hi >> 32, hl = hi & EPS;
+  uint64_t t0 = lo - hh;
+  t0 -= (lo < hh) ? EPS : 0;
+  const uint64_t t1 = (hl << 32) - hl;
+  const uint64_t r = t0 + t1;
+  return r + (r < t1 ? EPS : 0);
+}
+
+__device__ __forceinline__ uint64_t mul_nc(uint64_t a, uint64_t b) {
+  uint64_t lo, hi;
+  gl::mul_wide(a, b, lo, hi);
+  return reduce_nc(lo, hi);
+}
+
+__device__ __forceinline__ uint64_t sbox_nc(uint64_t x) {
+  const uint64_t x2 = mul_nc(x, x);
+  const uint64_t x3 = mul_nc(x2, x);
+  const uint64_t x4 = mul_nc(x2, x2);
+  return mul_nc(x3, x4);
+}
+
+__device__ __forceinline__ uint64_t canon(uint64_t x) { return x >= gl::P ? x - gl::P : x; }
+
+// MDS(s)[r] = sum_i s[(i+r)%12]*CIRC[i] + 8*s[0]*(r==0), on the 32-bit halves
+__device__ __forceinline__ void mds_nc(uint64_t s[12]) {
+  uint32_t lo[12], hi[12];
+#pragma unroll
+  for (int i = 0; i < 12; i++) {
+    lo[i] = (uint32_t)s[i];
+    hi[i] = (uint32_t)(s[i] >> 32);
+  }
+#pragma unroll
+  for (int r = 0; r < 12; r++) {
+    uint64_t al = 0, ah = 0;
+#pragma unroll
+    for (int i = 0; i < 12; i++) {
+      al += (uint64_t)lo[(i + r) % 12] * ps::mds_circ(i);
+      ah += (uint64_t)hi[(i + r) % 12] * ps::mds_circ(i);
+    }
+    if (r == 0) {
+      al += (uint64_t)lo[0] * 8u;
+      ah += (uint64_t)hi[0] * 8u;
+    }
+    // value = al + ah*2^32 < 2^74: low word + carry, high word H < 2^10
+    const uint64_t l = al + (ah << 32);
+    const uint64_t H = (ah >> 32) + (l < al ? 1 : 0);
+    const uint64_t t1 = (H << 32) - H;  // H * eps
+    const uint64_t v = l + t1;
+    s[r] = v + (v < t1 ? EPS : 0);
+  }
+}
+
+__device__ __forceinline__ void full_round(uint64_t s[12], int rc) {
+#pragma unroll
+  for (int i = 0; i < 12; i++) s[i] = sbox_nc(add_nc(s[i], ps::RC_DEV[rc * 12 + i]));
+  mds_nc(s);
+}
+
+__device__ __forceinline__ void partial_round(uint64_t s[12], int rc) {
+#pragma unroll
+  for (int i = 1; i < 12; i++) s[i] = add_nc(s[i], ps::RC_DEV[rc * 12 + i]);
+  s[0] = sbox_nc(add_nc(s[0], ps::RC_DEV[rc * 12]));
+  mds_nc(s);
+}
+
+// permutation; inputs in [0,2^64), outputs in [0,2^64) (call canon on lanes read out)
+__device__ __forceinline__ void permute_nc(uint64_t s[12]) {
+#pragma unroll
+  for (int r = 0; r < 4; r++) full_round(s, r);
+#pragma unroll
+  for (int r = 4; r < 26; r++) partial_round(s, r);
+#pragma unroll
+  for (int r = 26; r < 30; r++) full_round(s, r);
+}
+
+__device__ __forceinline__ void permute(uint64_t s[12]) {
+  permute_nc(s);
+#pragma unroll
+  for (int i = 0; i < 12; i++) s[i] = canon(s[i]);
+}
+
+}  // namespace psd

@@ -14,6 +14,7 @@
 //   k_gather_*             query-round openings (a11)
 #include "field.h"
 #include "poseidon.h"
+#include "poseidon_dev.h"
 #include "prover_kernels.h"
 
 namespace qpk {
@@ -474,10 +475,10 @@ __global__ void __launch_bounds__(256) k_fri_leaf(const uint64_t *__restrict__ v
         s[k + 1] = c1[e];
       }
     }
-    ps::permute(s);
+    psd::permute_nc(s);
   }
   uint64_t *o = dig + b * d_bstride + (uint64_t)i * 4;
-  o[0] = s[0]; o[1] = s[1]; o[2] = s[2]; o[3] = s[3];
+  o[0] = psd::canon(s[0]); o[1] = psd::canon(s[1]); o[2] = psd::canon(s[2]); o[3] = psd::canon(s[3]);
 }
 
 // fold: out[k] = sum_{i<2^ab} beta^i c[2^ab k + i]  (coefficients, ext as 2 columns)
@@ -517,8 +518,8 @@ __global__ void __launch_bounds__(256) k_pow(const uint64_t *__restrict__ states
 #pragma unroll
   for (int i = 0; i < 8; i++)
     if ((uint32_t)i == ps_) s[i] = cand;
-  ps::permute(s);
-  if ((s[7] >> (64 - bits)) == 0) atomicMin((unsigned long long *)&found[b], (unsigned long long)cand);
+  psd::permute_nc(s);
+  if ((psd::canon(s[7]) >> (64 - bits)) == 0) atomicMin((unsigned long long *)&found[b], (unsigned long long)cand);
 }
 
 // ---------------------------------------------------------------- gathers
