@@ -12,6 +12,7 @@
 #include "field.h"
 #include "kernels.h"
 #include "ntt_device.h"
+#include "ntt16.h"
 
 namespace qpk {
 
@@ -50,7 +51,7 @@ __global__ void __launch_bounds__(512) k_intt(const uint64_t *__restrict__ in, u
   uint64_t *dst = out + blockIdx.y * out_bstride + (uint64_t)blockIdx.x * out_stride;
   for (uint32_t i = threadIdx.x; i < n; i += blockDim.x) lds[i] = src[i];
   __syncthreads();
-  if (log_n) dif_lds(lds, log_n, tw_inv);
+  nt::ntt_lds<true>(lds, log_n, tw_inv);
   for (uint32_t m = threadIdx.x; m < n; m += blockDim.x) dst[m] = gl::mul(lds[gl::rev_bits(m, log_n)], n_inv);
 }
 
@@ -75,8 +76,8 @@ __global__ void __launch_bounds__(512) k_lde(const uint64_t *__restrict__ coeffs
     f = gl::mul(f, step);
   }
   __syncthreads();
-  if (log_n) dif_lds(lds, log_n, tw);
-  for (uint32_t p = threadIdx.x; p < n; p += blockDim.x) dst[p] = lds[p];
+  nt::ntt_lds<false>(lds, log_n, tw);
+  for (uint32_t p = threadIdx.x; p < n; p += blockDim.x) dst[p] = nt::canon(lds[p]);
 }
 
 static unsigned ntt_threads(uint32_t log_n) {

@@ -1,0 +1,205 @@
+// ntt16.h — register-blocked radix-16 DIF NTT core for gfx950.
+//
+// Every transform the prover runs is a size-n (n <= 2^14) NTT held in one
+// workgroup's LDS.  This core replaces the radix-2 stage loop with passes of
+// radix 16: each thread pulls 16 elements of one sub-problem (stride S/16) into
+// registers, runs a 16-point DFT whose internal twiddles are powers of
+// w_16 = 2^12 in Goldilocks (multiplication by a power of two = shifts + one
+// short reduction, no 64x64 product), then applies one general twiddle
+// w_S^{t*p} per element (table lookup + one product) and writes back in place.
+// 13 radix-2 levels become 3 radix-16 passes + 1 radix-2 pass: ~4x fewer LDS
+// round trips and barriers, and 15/16 general products per element per 4
+// levels instead of 2.  Arithmetic stays non-canonical in [0, 2^64)
+// (plonky2's own representation); callers canonicalise on store.
+// Output order is the standard in-place DIF order: a[q] = X[bitrev(q)].
+#pragma once
+#include "field.h"
+#include "kernels.h"
+
+namespace nt {
+
+constexpr uint64_t EPS = 0xFFFFFFFFull;
+
+__device__ __forceinline__ uint64_t add(uint64_t a, uint64_t b) {
+  uint64_t s = a + b;
+  if (s < b) {
+    s += EPS;
+    if (s < EPS) s += EPS;
+  }
+  return s;
+}
+
+__device__ __forceinline__ uint64_t sub(uint64_t a, uint64_t b) {
+  uint64_t d = a - b;
+  if (a < b) {
+    uint64_t d1 = d - EPS;
+    d = d1 > d ? d1 - EPS : d1;  // second wrap when b - a > p (b non-canonical)
+  }
+  return d;
+}
+
+__device__ __forceinline__ uint64_t reduce(uint64_t lo, uint64_t hi) {
+  const uint64_t hh = hi >> 32, hl = hi & EPS;
+  uint64_t t0 = lo - hh;
+  t0 -= (lo < hh) ? EPS : 0;
+  const uint64_t t1 = (hl << 32) - hl;
+  const uint64_t r = t0 + t1;
+  return r + (r < t1 ? EPS : 0);
+}
+
+__device__ __forceinline__ uint64_t mul(uint64_t a, uint64_t b) {
+  uint64_t lo, hi;
+  gl::mul_wide(a, b, lo, hi);
+  return reduce(lo, hi);
+}
+
+__device__ __forceinline__ uint64_t canon(uint64_t x) { return x >= gl::P ? x - gl::P : x; }
+
+__device__ __forceinline__ uint64_t neg(uint64_t x) {
+  x = canon(x);
+  return x ? gl::P - x : 0;
+}
+
+// x * 2^E for a compile-time E in [0, 192) (2^96 = -1, 2^192 = 1)
+template <int E>
+__device__ __forceinline__ uint64_t mul_pow2(uint64_t x) {
+  if constexpr (E >= 96) {
+    return neg(mul_pow2<E - 96>(x));
+  } else if constexpr (E == 0) {
+    return x;
+  } else if constexpr (E < 64) {
+    return reduce(x << E, x >> (64 - E));
+  } else {
+    // x = x1 2^32 + x0: x 2^E = x0 2^E - x1 2^(E-64)   (2^96 = -1)
+    constexpr int F = E - 64;
+    const uint64_t x0 = x & EPS, x1 = x >> 32;
+    return sub(reduce(0, x0 << F), x1 << F);
+  }
+}
+
+// twiddle w_16^j (forward) or w_16^-j (inverse): w_16 = 2^12
+template <bool INV, int J>
+__device__ __forceinline__ uint64_t mul_w16(uint64_t x) {
+  if constexpr (J == 0) return x;
+  else if constexpr (!INV) return mul_pow2<(12 * J) % 192>(x);
+  else return mul_pow2<(192 - 12 * J) % 192>(x);
+}
+
+// radix-2 DIF stage of half-width H on a register array of size 16
+template <bool INV, int H>
+__device__ __forceinline__ void stage16(uint64_t a[16]) {
+#pragma unroll
+  for (int k = 0; k < 16; k += 2 * H) {
+#pragma unroll
+    for (int j = 0; j < H; j++) {
+      const uint64_t u = a[k + j], v = a[k + j + H];
+      a[k + j] = add(u, v);
+      const uint64_t d = sub(u, v);
+      // w_{2H}^j = w_16^{j * 8/H}
+      switch (j * (8 / H)) {
+        case 0: a[k + j + H] = d; break;
+        case 1: a[k + j + H] = mul_w16<INV, 1>(d); break;
+        case 2: a[k + j + H] = mul_w16<INV, 2>(d); break;
+        case 3: a[k + j + H] = mul_w16<INV, 3>(d); break;
+        case 4: a[k + j + H] = mul_w16<INV, 4>(d); break;
+        case 5: a[k + j + H] = mul_w16<INV, 5>(d); break;
+        case 6: a[k + j + H] = mul_w16<INV, 6>(d); break;
+        default: a[k + j + H] = mul_w16<INV, 7>(d); break;
+      }
+    }
+  }
+}
+
+template <bool INV>
+__device__ __forceinline__ void dft16(uint64_t a[16]) {
+  stage16<INV, 8>(a);
+  stage16<INV, 4>(a);
+  stage16<INV, 2>(a);
+  stage16<INV, 1>(a);
+}
+
+// w_S^e via the half table of w_{2^TW_LOG} (tw[j] = w^j, j < 2^(TW_LOG-1))
+__device__ __forceinline__ uint64_t tw_pow(const uint64_t *__restrict__ tw, uint32_t e, uint32_t log_S) {
+  const uint32_t E = e << (qpk::TW_LOG - log_S);
+  constexpr uint32_t HALF = 1u << (qpk::TW_LOG - 1);
+  return E < HALF ? tw[E] : gl::P - tw[E - HALF];  // tw entries are canonical and nonzero
+}
+
+__device__ __forceinline__ uint32_t brev4(uint32_t m) { return __builtin_bitreverse32(m) >> 28; }
+
+// radix-2^LOGS DIF on each group of S = 2^LOGS contiguous LDS elements
+// (the last levels of ntt_lds); twiddles are powers of w_S = w_16^(16/S)
+template <bool INV, int H, int S>
+__device__ __forceinline__ void stage_small(uint64_t r[S]) {
+#pragma unroll
+  for (int k = 0; k < S; k += 2 * H) {
+#pragma unroll
+    for (int j = 0; j < H; j++) {
+      const uint64_t u = r[k + j], v = r[k + j + H];
+      r[k + j] = add(u, v);
+      const uint64_t d = sub(u, v);
+      switch (j * (8 / H)) {
+        case 0: r[k + j + H] = d; break;
+        case 1: r[k + j + H] = mul_w16<INV, 1>(d); break;
+        case 2: r[k + j + H] = mul_w16<INV, 2>(d); break;
+        case 3: r[k + j + H] = mul_w16<INV, 3>(d); break;
+        case 4: r[k + j + H] = mul_w16<INV, 4>(d); break;
+        case 5: r[k + j + H] = mul_w16<INV, 5>(d); break;
+        case 6: r[k + j + H] = mul_w16<INV, 6>(d); break;
+        default: r[k + j + H] = mul_w16<INV, 7>(d); break;
+      }
+    }
+  }
+}
+
+template <bool INV, int LOGS>
+__device__ void tail(uint64_t *a, uint32_t n) {
+  constexpr int S = 1 << LOGS;
+  for (uint32_t g = threadIdx.x; g < (n >> LOGS); g += blockDim.x) {
+    uint64_t *base = a + (g << LOGS);
+    uint64_t r[S];
+#pragma unroll
+    for (int m = 0; m < S; m++) r[m] = base[m];
+    if constexpr (S >= 8) stage_small<INV, S / 2, S>(r);
+    if constexpr (S >= 4) stage_small<INV, 2, S>(r);
+    stage_small<INV, 1, S>(r);
+#pragma unroll
+    for (int m = 0; m < S; m++) base[m] = r[m];
+  }
+  __syncthreads();
+}
+
+// In-place DIF over LDS a[0..2^log_n), all threads of the block participate.
+// tw = forward or inverse twiddle table matching INV.  Ends with a barrier.
+template <bool INV>
+__device__ void ntt_lds(uint64_t *a, uint32_t log_n, const uint64_t *__restrict__ tw) {
+  const uint32_t n = 1u << log_n;
+  const uint32_t T = blockDim.x;
+  uint32_t log_S = log_n;
+  // radix-16 passes
+  while (log_S >= 4) {
+    const uint32_t S = 1u << log_S, q = S >> 4, log_q = log_S - 4;
+    for (uint32_t g = threadIdx.x; g < (n >> 4); g += T) {
+      const uint32_t sp = g >> log_q, t = g & (q - 1);
+      uint64_t *base = a + (sp << log_S) + t;
+      uint64_t r[16];
+#pragma unroll
+      for (int m = 0; m < 16; m++) r[m] = base[m * q];
+      dft16<INV>(r);
+      if (t) {
+#pragma unroll
+        for (int m = 1; m < 16; m++) r[m] = mul(r[m], tw_pow(tw, t * brev4(m), log_S));
+      }
+#pragma unroll
+      for (int m = 0; m < 16; m++) base[m * q] = r[m];
+    }
+    __syncthreads();
+    log_S -= 4;
+  }
+  // remaining radix-2^log_S levels (log_S < 4): groups of S contiguous elements
+  if (log_S == 1) tail<INV, 1>(a, n);
+  else if (log_S == 2) tail<INV, 2>(a, n);
+  else if (log_S == 3) tail<INV, 3>(a, n);
+}
+
+}  // namespace nt

@@ -16,6 +16,7 @@
 #include "poseidon.h"
 #include "poseidon_dev.h"
 #include "prover_kernels.h"
+#include "ntt16.h"
 
 namespace qpk {
 
@@ -288,7 +289,7 @@ __global__ void __launch_bounds__(512) k_qintt_blocks(const uint64_t *__restrict
   const uint64_t *src = vals + b * v_bstride + c * N + ((uint64_t)sp << log_n);
   for (uint32_t p = threadIdx.x; p < n; p += blockDim.x) lds[gl::rev_bits(p, log_n)] = src[p];
   __syncthreads();
-  dif_lds(lds, log_n, tw_inv);
+  nt::ntt_lds<true>(lds, log_n, tw_inv);
   // base^-1 = g^-1 w_N^-s
   const uint64_t wNs = wpow_N(tw, s, logN);
   const uint64_t binv = gl::mul(ginv, gl::inv(wNs));
