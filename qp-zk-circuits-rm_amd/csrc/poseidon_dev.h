@@ -17,26 +17,48 @@ namespace psd {
 
 constexpr uint64_t EPS = 0xFFFFFFFFull;
 
-// a + c, a in [0,2^64), c canonical: result in [0,2^64), same field value
-__device__ __forceinline__ uint64_t add_nc(uint64_t a, uint64_t c) {
-  uint64_t s = a + c;
-  return s + (s < c ? EPS : 0);
+// a + b for a, b in [0, 2^64) with b < p (canonical): result in [0, 2^64).
+// 32-bit carry chain (full-rate VALU) instead of 64-bit add + 64-bit compare.
+__device__ __forceinline__ uint64_t add_nc(uint64_t a, uint64_t b) {
+  uint32_t c0, c1, c2, c3;
+  uint32_t lo = __builtin_addc((uint32_t)a, (uint32_t)b, 0u, &c0);
+  uint32_t hi = __builtin_addc((uint32_t)(a >> 32), (uint32_t)(b >> 32), c0, &c1);
+  // wrapped past 2^64: + eps (cannot wrap again: b < p)
+  lo = __builtin_addc(lo, 0u - c1, 0u, &c2);
+  hi = __builtin_addc(hi, 0u, c2, &c3);
+  return ((uint64_t)hi << 32) | lo;
 }
 
-// reduce lo + 2^64 hi (any hi) to [0, 2^64)
+// reduce lo + 2^64 hi (any hi) to [0, 2^64) with 32-bit carry chains
 __device__ __forceinline__ uint64_t reduce_nc(uint64_t lo, uint64_t hi) {
-  const uint64_t hh = hi >> 32, hl = hi & EPS;
-  uint64_t t0 = lo - hh;
-  t0 -= (lo < hh) ? EPS : 0;
-  const uint64_t t1 = (hl << 32) - hl;
-  const uint64_t r = t0 + t1;
-  return r + (r < t1 ? EPS : 0);
+  const uint32_t hl = (uint32_t)hi, hh = (uint32_t)(hi >> 32);
+  uint32_t l0 = (uint32_t)lo, l1 = (uint32_t)(lo >> 32), c, bo, bo2;
+  // t = lo - hh ; on borrow t -= eps  (= t + 1 - 2^32)
+  l0 = __builtin_subc(l0, hh, 0u, &bo);
+  l1 = __builtin_subc(l1, 0u, bo, &bo2);
+  l0 = __builtin_addc(l0, bo2, 0u, &c);
+  l1 = l1 - bo2 + c;
+  // + hl * eps = (hl << 32) - hl
+  const uint32_t t0 = __builtin_subc(0u, hl, 0u, &bo);
+  const uint32_t t1 = hl - bo;
+  l0 = __builtin_addc(l0, t0, 0u, &c);
+  l1 = __builtin_addc(l1, t1, c, &c);
+  // carry out: + eps
+  l0 = __builtin_addc(l0, 0u - c, 0u, &bo);
+  l1 = l1 + bo;
+  return ((uint64_t)l1 << 32) | l0;
 }
 
 __device__ __forceinline__ uint64_t mul_nc(uint64_t a, uint64_t b) {
-  uint64_t lo, hi;
-  gl::mul_wide(a, b, lo, hi);
-  return reduce_nc(lo, hi);
+  const uint32_t a0 = (uint32_t)a, a1 = (uint32_t)(a >> 32), b0 = (uint32_t)b, b1 = (uint32_t)(b >> 32);
+  const uint64_t p00 = (uint64_t)a0 * b0;
+  const uint64_t m = (uint64_t)a1 * b0 + (p00 >> 32);
+  const uint64_t m2 = (uint64_t)a0 * b1 + (uint32_t)m;
+  const uint64_t h = (uint64_t)a1 * b1 + (m >> 32);
+  uint32_t c;
+  const uint32_t hl = __builtin_addc((uint32_t)h, (uint32_t)(m2 >> 32), 0u, &c);
+  const uint32_t hh = (uint32_t)(h >> 32) + c;
+  return reduce_nc(((uint64_t)(uint32_t)m2 << 32) | (uint32_t)p00, ((uint64_t)hh << 32) | hl);
 }
 
 __device__ __forceinline__ uint64_t sbox_nc(uint64_t x) {
