@@ -90,11 +90,12 @@ struct qp_prover {
   Tree cs;
   DevBuf sigmas, kis;
   Tree wires, zs, quot;
-  DevBuf chal, prods, qvals, cbuf, openings, comp, fin, pow_state, pow_found, pow_pos, qidx, qout;
+  DevBuf chal, apow, prods, qvals, cbuf, openings, comp, fin, pow_state, pow_found, pow_pos, qidx, qout;
   std::vector<DevBuf> fvals, fdig, fcoef;
   size_t qout_words = 0;
   std::unique_ptr<qh::ThreadPool> pool;
-  std::vector<uint64_t> h_chal, h_caps, h_open, h_final, h_qout, h_powst, h_found;
+  std::vector<uint64_t> h_chal, h_apow, h_caps, h_open, h_final, h_qout, h_powst, h_found;
+  uint32_t nterms = 0;
   std::vector<uint32_t> h_qidx, h_pos;
   size_t proof_len = 0;
   double stage_ms[16] = {0};
@@ -225,6 +226,13 @@ int setup(qp_prover *P) {
   TRY(P->zs.alloc(P->nc * P->nchunks, P->log_n, P->rate_bits, P->cap_h, B, true));
   TRY(P->quot.alloc(P->nc * P->qdf, P->log_n, P->rate_bits, P->cap_h, B, false));
   TRY(P->chal.alloc((size_t)B * qpk::CHAL_STRIDE));
+  P->nterms = P->nc + P->nc * P->nchunks + cd.num_gate_constraints;
+  if (P->nterms > qpk::APOW_STRIDE) {
+    c->err = "too many vanishing-polynomial terms for the alpha power table";
+    return QP_ERR_ARG;
+  }
+  TRY(P->apow.alloc((size_t)B * 2 * qpk::APOW_STRIDE));
+  P->h_apow.assign((size_t)B * 2 * qpk::APOW_STRIDE, 0);
   TRY(P->prods.alloc((size_t)B * P->nc * P->nchunks * n));
   TRY(P->qvals.alloc((size_t)B * P->nc * N));
   TRY(P->cbuf.alloc((size_t)B * P->nc * N));
@@ -405,8 +413,16 @@ int prove_batch(qp_prover *P, const uint64_t *const *wires_host, const uint64_t 
     S.t.observe(S.caps[1].data(), capw);
     uint64_t *ch = P->h_chal.data() + b * qpk::CHAL_STRIDE;
     for (uint32_t i = 0; i < nc; i++) ch[qpk::CH_ALPHA + i] = S.t.get();
+    for (uint32_t c2 = 0; c2 < 2; c2++) {
+      uint64_t *ap = P->h_apow.data() + (b * 2 + c2) * qpk::APOW_STRIDE, p = 1;
+      for (uint32_t i = 0; i < P->nterms; i++) {
+        ap[i] = p;
+        p = gl::mul(p, ch[qpk::CH_ALPHA + c2]);
+      }
+    }
   });
   if ((rc = push_chal(P, nb))) return rc;
+  TRY(hipMemcpyAsync(P->apow.p, P->h_apow.data(), (size_t)nb * 2 * qpk::APOW_STRIDE * 8, hipMemcpyHostToDevice, s));
   lap(1);
 
   // ---- 3. quotient polynomials (a8)
@@ -419,6 +435,7 @@ int prove_batch(qp_prover *P, const uint64_t *const *wires_host, const uint64_t 
     a.z_bstride = P->zs.lbs();
     a.chal = P->chal.p;
     a.tw = c->tw.fwd;
+    a.apow = P->apow.p;
     const uint32_t B = 1u << P->rate_bits;
     const uint64_t wN = gl::root_of_unity(logN);
     for (uint32_t k = 0; k < B; k++) {

@@ -13,6 +13,7 @@ enum : uint32_t {
   CH_ZETA_NEXT_INV = 16, CH_FRI_ALPHA = 18, CH_ALPHA_POW_NC = 20, CH_FRI_BETA = 22, CHAL_STRIDE = 40
 };
 constexpr uint32_t OPEN_STRIDE = 520;  // 257 ext openings per proof (+pad)
+constexpr uint32_t APOW_STRIDE = 256;  // alpha_c^i, i < #vanishing terms (per challenge)
 
 enum GateKindDev : uint32_t { GK_NOOP = 0, GK_CONSTANT, GK_PUBLIC_INPUT, GK_BASE_SUM, GK_ARITHMETIC, GK_POSEIDON };
 
@@ -24,7 +25,7 @@ struct GateDesc {
 struct QuotientArgs {
   const uint64_t *cs_lde, *w_lde, *z_lde;
   uint64_t w_bstride, z_bstride;
-  const uint64_t *chal, *tw;
+  const uint64_t *chal, *tw, *apow;
   uint64_t zh[16], zh_inv[16];
   uint64_t *q_out;
   uint64_t q_bstride;

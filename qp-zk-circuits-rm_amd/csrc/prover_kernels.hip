@@ -113,72 +113,81 @@ __global__ void __launch_bounds__(1024) k_z_scan(const uint64_t *__restrict__ pr
 }
 
 // ---------------------------------------------------------------- a8
-
-struct Acc2 {
-  uint64_t acc0, acc1, p0, p1, a0, a1;
-  __device__ __forceinline__ void emit(uint64_t t) {
-    acc0 = gl::add(acc0, gl::mul(t, p0));
-    acc1 = gl::add(acc1, gl::mul(t, p1));
-    p0 = gl::mul(p0, a0);
-    p1 = gl::mul(p1, a1);
-  }
-  __device__ __forceinline__ void emitf(uint64_t f, uint64_t t) { emit(gl::mul(f, t)); }
-};
+//
+// One lane per LDE point.  Terms are alpha-reduced as sum_i t_i alpha_c^i
+// with per-proof power tables (apow, uniform across the workgroup -> scalar
+// loads); a gate's constraints are summed first and multiplied by the gate's
+// selector filter once.  Arithmetic is non-canonical (field_nc.h).
 
 #define WV(j) wl[(uint64_t)(j) * N]
 
-__device__ __forceinline__ void poseidon_gate(const uint64_t *__restrict__ wl, uint64_t N, uint64_t f, Acc2 &A) {
+struct TermAcc {
+  const uint64_t *__restrict__ p0;  // alpha_0^i
+  const uint64_t *__restrict__ p1;  // alpha_1^i
+  uint64_t s0, s1;
+  uint32_t i;
+  __device__ __forceinline__ void emit(uint64_t t) {
+    s0 = gfn::add(s0, gfn::mul(t, p0[i]));
+    s1 = gfn::add(s1, gfn::mul(t, p1[i]));
+    i++;
+  }
+};
+
+__device__ __forceinline__ void poseidon_gate(const uint64_t *__restrict__ wl, uint64_t N, TermAcc &A) {
   const uint64_t swap = WV(24);
-  A.emitf(f, gl::mul(swap, gl::sub(swap, 1)));
+  A.emit(gfn::mul(swap, gfn::sub(swap, 1)));
   uint64_t s[12];
 #pragma unroll
   for (int i = 0; i < 4; i++) {
     const uint64_t delta = WV(25 + i), a = WV(i), c = WV(i + 4);
-    A.emitf(f, gl::sub(gl::mul(swap, gl::sub(c, a)), delta));
-    s[i] = gl::add(a, delta);
-    s[i + 4] = gl::sub(c, delta);
+    A.emit(gfn::sub(gfn::mul(swap, gfn::sub(c, a)), delta));
+    s[i] = gfn::add_c(a, delta);
+    s[i + 4] = gfn::sub(c, delta);
   }
 #pragma unroll
   for (int i = 8; i < 12; i++) s[i] = WV(i);
-  int rc = 0;
-  for (int r = 0; r < 4; r++, rc++) {
 #pragma unroll
-    for (int i = 0; i < 12; i++) s[i] = gl::add(s[i], ps::rc(rc * 12 + i));
+  for (int r = 0; r < 4; r++) {
+#pragma unroll
+    for (int i = 0; i < 12; i++) s[i] = gfn::add_c(s[i], ps::RC_DEV[r * 12 + i]);
     if (r) {
 #pragma unroll
       for (int i = 0; i < 12; i++) {
         const uint64_t sb = WV(29 + (r - 1) * 12 + i);
-        A.emitf(f, gl::sub(s[i], sb));
+        A.emit(gfn::sub(s[i], sb));
         s[i] = sb;
       }
     }
 #pragma unroll
-    for (int i = 0; i < 12; i++) s[i] = ps::sbox(s[i]);
-    ps::mds(s);
+    for (int i = 0; i < 12; i++) s[i] = gfn::sbox(s[i]);
+    psd::mds_nc(s);
   }
-  for (int r = 0; r < 22; r++, rc++) {
+  for (int r = 0; r < 22; r++) {
+    const int rc = 4 + r;
 #pragma unroll
-    for (int i = 0; i < 12; i++) s[i] = gl::add(s[i], ps::rc(rc * 12 + i));
+    for (int i = 0; i < 12; i++) s[i] = gfn::add_c(s[i], ps::RC_DEV[rc * 12 + i]);
     const uint64_t sb = WV(65 + r);
-    A.emitf(f, gl::sub(s[0], sb));
-    s[0] = ps::sbox(sb);
-    ps::mds(s);
+    A.emit(gfn::sub(s[0], sb));
+    s[0] = gfn::sbox(sb);
+    psd::mds_nc(s);
   }
-  for (int r = 0; r < 4; r++, rc++) {
 #pragma unroll
-    for (int i = 0; i < 12; i++) s[i] = gl::add(s[i], ps::rc(rc * 12 + i));
+  for (int r = 0; r < 4; r++) {
+    const int rc = 26 + r;
+#pragma unroll
+    for (int i = 0; i < 12; i++) s[i] = gfn::add_c(s[i], ps::RC_DEV[rc * 12 + i]);
 #pragma unroll
     for (int i = 0; i < 12; i++) {
       const uint64_t sb = WV(87 + r * 12 + i);
-      A.emitf(f, gl::sub(s[i], sb));
+      A.emit(gfn::sub(s[i], sb));
       s[i] = sb;
     }
 #pragma unroll
-    for (int i = 0; i < 12; i++) s[i] = ps::sbox(s[i]);
-    ps::mds(s);
+    for (int i = 0; i < 12; i++) s[i] = gfn::sbox(s[i]);
+    psd::mds_nc(s);
   }
 #pragma unroll
-  for (int i = 0; i < 12; i++) A.emitf(f, gl::sub(s[i], WV(12 + i)));
+  for (int i = 0; i < 12; i++) A.emit(gfn::sub(s[i], WV(12 + i)));
 }
 
 __global__ void __launch_bounds__(256) k_quotient(QuotientArgs a) {
@@ -196,81 +205,88 @@ __global__ void __launch_bounds__(256) k_quotient(QuotientArgs a) {
   const uint64_t x = gl::mul(gl::GEN, wpow_N(a.tw, j, logN));
   const uint64_t zh = a.zh[j & ((1u << a.rate_bits) - 1)];
   const uint64_t zh_inv = a.zh_inv[j & ((1u << a.rate_bits) - 1)];
-  Acc2 A;
-  A.acc0 = A.acc1 = 0;
-  A.p0 = A.p1 = 1;
-  A.a0 = ch[CH_ALPHA + 0];
-  A.a1 = ch[CH_ALPHA + 1];
+  TermAcc A;
+  A.p0 = a.apow + (uint64_t)b * 2 * APOW_STRIDE;
+  A.p1 = A.p0 + APOW_STRIDE;
+  A.s0 = A.s1 = 0;
+  A.i = 0;
   // L_0(x) (Z_c - 1)
   const uint64_t l0 = gl::mul(zh, gl::inv(gl::mul(gl::sub(x, 1), n % gl::P)));
-  for (uint32_t c = 0; c < 2; c++) A.emit(gl::mul(l0, gl::sub(zl[(uint64_t)c * N + t], 1)));
+  for (uint32_t c = 0; c < 2; c++) A.emit(gfn::mul(l0, gfn::sub(zl[(uint64_t)c * N + t], 1)));
   // partial-product checks
   const uint32_t R = a.R, qdf = a.qdf, nchunks = (R + qdf - 1) / qdf, npp = nchunks - 1;
   for (uint32_t c = 0; c < 2; c++) {
     const uint64_t beta = ch[CH_BETA + c], gamma = ch[CH_GAMMA + c];
-    uint64_t kx = x;  // k_j * x with k_j = g^j
+    uint64_t bkx = gfn::mul(beta, x);  // beta * k_j * x with k_j = g^j
     for (uint32_t k = 0; k < nchunks; k++) {
       uint64_t num = 1, den = 1;
       for (uint32_t jj = k * qdf; jj < (k + 1) * qdf && jj < R; jj++) {
         const uint64_t wv = WV(jj);
-        num = gl::mul(num, gl::add(gl::add(wv, gl::mul(beta, kx)), gamma));
-        den = gl::mul(den, gl::add(gl::add(wv, gl::mul(beta, cs[(uint64_t)(a.num_constants + jj) * N])), gamma));
-        kx = gl::mul(kx, gl::GEN);
+        const uint64_t wg = gfn::add_c(wv, gamma);
+        num = gfn::mul(num, gfn::add(wg, bkx));
+        den = gfn::mul(den, gfn::add(wg, gfn::mul(beta, cs[(uint64_t)(a.num_constants + jj) * N])));
+        bkx = gfn::mul(bkx, gl::GEN);
       }
       const uint64_t prev = k == 0 ? zl[(uint64_t)c * N + t] : zl[((uint64_t)2 + c * npp + k - 1) * N + t];
       const uint64_t next = k == nchunks - 1 ? zl[(uint64_t)c * N + tn] : zl[((uint64_t)2 + c * npp + k) * N + t];
-      A.emit(gl::sub(gl::mul(prev, num), gl::mul(next, den)));
+      A.emit(gfn::sub(gfn::mul(prev, num), gfn::mul(next, den)));
     }
   }
-  // gate constraints: every gate restarts at alpha^(#pre-terms)
-  const uint64_t base0 = A.p0, base1 = A.p1;
+  // gate constraints: every gate's terms start at alpha^(#pre-terms); the
+  // selector filter multiplies each gate's sum once
+  const uint32_t pre = A.i;
+  uint64_t acc0 = A.s0, acc1 = A.s1;
   uint64_t consts[8];
   for (uint32_t k = 0; k < a.num_constants && k < 8; k++) consts[k] = cs[(uint64_t)k * N];
   const uint32_t nsel = a.g.nsel;
   for (uint32_t gi = 0; gi < a.g.ngates; gi++) {
+    if (a.g.kind[gi] == GK_NOOP) continue;
     const uint32_t si = a.g.sel_index[gi];
     const uint64_t s = consts[si];
     uint64_t f = 1;
     for (uint32_t jj = a.g.grp_lo[si]; jj < a.g.grp_hi[si]; jj++)
-      if (jj != gi) f = gl::mul(f, gl::sub(jj, s));
-    if (nsel > 1) f = gl::mul(f, gl::sub(0xFFFFFFFFull, s));
-    A.p0 = base0;
-    A.p1 = base1;
+      if (jj != gi) f = gfn::mul(f, gfn::sub(jj, s));
+    if (nsel > 1) f = gfn::mul(f, gfn::sub(0xFFFFFFFFull, s));
+    A.s0 = A.s1 = 0;
+    A.i = pre;
     const uint64_t *gc = consts + nsel;
     switch (a.g.kind[gi]) {
       case GK_CONSTANT:
-        for (uint32_t i = 0; i < a.g.param[gi]; i++) A.emitf(f, gl::sub(gc[i], WV(i)));
+        for (uint32_t i = 0; i < a.g.param[gi]; i++) A.emit(gfn::sub(gc[i], WV(i)));
         break;
       case GK_PUBLIC_INPUT:
-        for (uint32_t i = 0; i < 4; i++) A.emitf(f, gl::sub(WV(i), ch[CH_PIH + i]));
+        for (uint32_t i = 0; i < 4; i++) A.emit(gfn::sub(WV(i), ch[CH_PIH + i]));
         break;
       case GK_BASE_SUM: {
         const uint32_t L = a.g.param[gi];
         uint64_t acc = 0;
-        for (uint32_t i = L; i-- > 0;) acc = gl::add(gl::add(acc, acc), WV(1 + i));
-        A.emitf(f, gl::sub(acc, WV(0)));
+        for (uint32_t i = L; i-- > 0;) acc = gfn::add(gfn::add(acc, acc), WV(1 + i));
+        A.emit(gfn::sub(acc, WV(0)));
         for (uint32_t i = 0; i < L; i++) {
           const uint64_t l = WV(1 + i);
-          A.emitf(f, gl::mul(l, gl::sub(l, 1)));
+          A.emit(gfn::mul(l, gfn::sub(l, 1)));
         }
         break;
       }
       case GK_ARITHMETIC:
         for (uint32_t i = 0; i < a.g.param[gi]; i++) {
-          const uint64_t comp = gl::add(gl::mul(gl::mul(WV(4 * i), WV(4 * i + 1)), gc[0]), gl::mul(WV(4 * i + 2), gc[1]));
-          A.emitf(f, gl::sub(WV(4 * i + 3), comp));
+          const uint64_t comp = gfn::add(gfn::mul(gfn::mul(WV(4 * i), WV(4 * i + 1)), gc[0]),
+                                         gfn::mul(WV(4 * i + 2), gc[1]));
+          A.emit(gfn::sub(WV(4 * i + 3), comp));
         }
         break;
       case GK_POSEIDON:
-        poseidon_gate(wl, N, f, A);
+        poseidon_gate(wl, N, A);
         break;
       default:
         break;
     }
+    acc0 = gfn::add(acc0, gfn::mul(f, A.s0));
+    acc1 = gfn::add(acc1, gfn::mul(f, A.s1));
   }
   uint64_t *q = a.q_out + b * a.q_bstride;
-  q[t] = gl::mul(A.acc0, zh_inv);
-  q[N + t] = gl::mul(A.acc1, zh_inv);
+  q[t] = gfn::canon(gfn::mul(acc0, zh_inv));
+  q[N + t] = gfn::canon(gfn::mul(acc1, zh_inv));
 }
 #undef WV
 
