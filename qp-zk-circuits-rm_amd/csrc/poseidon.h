@@ -115,6 +115,9 @@ __host__ __device__ constexpr uint32_t mds_circ(int i) {
 
 static const uint64_t RC_HOST[ROUNDS * WIDTH] = {QP_POSEIDON_RC_LIST};
 __constant__ static const uint64_t RC_DEV[ROUNDS * WIDTH] = {QP_POSEIDON_RC_LIST};
+// compile-time view (constants folded into instruction operands)
+constexpr uint64_t RC_CX[ROUNDS * WIDTH] = {QP_POSEIDON_RC_LIST};
+__host__ __device__ constexpr uint64_t rc_cx(int i) { return RC_CX[i]; }
 
 QP_HD uint64_t rc(int i) {
 #ifdef __HIP_DEVICE_COMPILE__

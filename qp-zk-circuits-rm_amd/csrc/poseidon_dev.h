@@ -13,6 +13,7 @@
 #include "field.h"
 #include "poseidon.h"
 #include "field_nc.h"
+#include "poseidon_fast.h"
 
 namespace psd {
 
@@ -77,8 +78,9 @@ __device__ __forceinline__ void partial_round(uint64_t s[12], int rc) {
   mds_nc(s);
 }
 
-// permutation; inputs in [0,2^64), outputs in [0,2^64) (call canon on lanes read out)
-__device__ __forceinline__ void permute_nc(uint64_t s[12]) {
+// first-generation form (carry-chain arithmetic, separate round-constant
+// additions); kept for tools/poseidon_ubench.hip comparisons only
+__device__ __forceinline__ void permute_nc_v1(uint64_t s[12]) {
 #pragma unroll
   for (int r = 0; r < 4; r++) full_round(s, r);
 #pragma unroll
@@ -86,6 +88,11 @@ __device__ __forceinline__ void permute_nc(uint64_t s[12]) {
 #pragma unroll
   for (int r = 26; r < 30; r++) full_round(s, r);
 }
+
+// permutation used by the kernels: poseidon_fast.h (2.24 vs 1.67 Gperm/s for
+// permute_nc_v1 on MI355X, tools/poseidon_ubench.hip).  Inputs in [0,2^64),
+// outputs in [0,2^64) (call canon on lanes read out)
+__device__ __forceinline__ void permute_nc(uint64_t s[12]) { pf::permute_nc<0>(s); }
 
 __device__ __forceinline__ void permute(uint64_t s[12]) {
   permute_nc(s);

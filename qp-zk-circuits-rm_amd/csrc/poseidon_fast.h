@@ -1,0 +1,233 @@
+// poseidon_fast.h — Poseidon (width 12, x^7, 8 full + 22 partial rounds)
+// written to the measured gfx950 VALU cost model (tools/isa_rates.hip,
+// profiles/r01_isa_rates.log): almost every VALU op issues at one per 4
+// cycles per SIMD (add/sub/logic/mov at 2), so the permutation is bound by
+// its VALU instruction count and v_mad_u64_u32 — a 32x32+64 product-sum in one
+// issue — is the densest instruction there is.
+//
+// Same function as ps::permute (poseidon.h); arithmetic discipline:
+//   * state NON-canonical in [0, 2^64) (plonky2's GoldilocksField form);
+//   * MDS row r = sum_i CIRC[i] * s[(i+r)%12] (+ DIAG) computed on 32-bit
+//     halves as 24 explicit v_mad_u64_u32 with the small constants inline
+//     (the compiler would otherwise strength-reduce them into longer
+//     shift/add carry chains);
+//   * the NEXT round's constant is folded into the first mad of each row
+//     (addend = the constant's halves), so no round-constant additions are
+//     executed except the first round's;
+//   * each row reduces in 4 instructions: value = al + 2^32 ah with
+//     al, ah < 2^41 -> t = al + eps*hi32(ah) (one mad), t.hi += lo32(ah) with
+//     carry c, t += c*eps.
+//   * sbox x^7 = x^3 * x^4 with a 5-mad product and an 8-instruction
+//     Goldilocks reduction whose carries come straight from the mad/sub
+//     carry-outs.
+#pragma once
+#include <stdint.h>
+#include <hip/hip_runtime.h>
+#include "poseidon.h"
+
+namespace pf {
+
+constexpr uint64_t EPS = 0xFFFFFFFFull;
+constexpr uint64_t P = 0xFFFFFFFF00000001ull;
+
+__device__ __forceinline__ uint32_t lo32(uint64_t x) { return (uint32_t)x; }
+__device__ __forceinline__ uint32_t hi32(uint64_t x) { return (uint32_t)(x >> 32); }
+
+// C as a value the compiler cannot see through (an SGPR; no instruction is
+// emitted for the empty asm), so x * C stays one v_mad_u64_u32
+template <int C>
+__device__ __forceinline__ uint32_t opaque() {
+  uint32_t c;
+  asm("" : "=s"(c) : "0"((uint32_t)C));
+  return c;
+}
+
+// acc = x * C + add   (C an inline constant in [0, 64])
+template <int C>
+__device__ __forceinline__ uint64_t mad_c(uint32_t x, uint64_t add) {
+  uint64_t r, cdummy;
+  asm("v_mad_u64_u32 %0, %1, %2, %3, %4" : "=v"(r), "=s"(cdummy) : "v"(x), "i"(C), "v"(add));
+  return r;
+}
+// acc = x * C + add, add a scalar (SGPR) 64-bit value
+template <int C>
+__device__ __forceinline__ uint64_t mad_cs(uint32_t x, uint64_t add) {
+  uint64_t r, cdummy;
+  asm("v_mad_u64_u32 %0, %1, %2, %3, %4" : "=v"(r), "=s"(cdummy) : "v"(x), "i"(C), "s"(add));
+  return r;
+}
+
+// value = al + 2^32 ah (al, ah < 2^42)  ->  [0, 2^64), same residue
+__device__ __forceinline__ uint64_t reduce_row(uint64_t al, uint64_t ah) {
+  uint64_t t, c1, c2;
+  uint32_t e;
+  // t = al + eps * hi32(ah)   (< 2^43, no overflow)
+  asm("v_mad_u64_u32 %0, %1, %2, -1, %3" : "=v"(t), "=s"(c1) : "v"(hi32(ah)), "v"(al));
+  // t.hi += lo32(ah), carry c2 (worth 2^64 = eps)
+  uint32_t t0 = lo32(t), t1 = hi32(t);
+  asm("v_add_co_u32_e64 %0, %1, %2, %3" : "=v"(t1), "=s"(c2) : "v"(t1), "v"(lo32(ah)));
+  asm("v_cndmask_b32_e64 %0, 0, -1, %1" : "=v"(e) : "s"(c2));
+  // t + e: when c2, t < 2^42 so no overflow
+  const uint64_t tt = ((uint64_t)t1 << 32) | t0;
+  uint64_t r;
+  asm("v_mad_u64_u32 %0, %1, %2, 1, %3" : "=v"(r), "=s"(c1) : "v"(e), "v"(tt));
+  return r;
+}
+
+// a * b mod p, a, b in [0, 2^64), result in [0, 2^64)
+__device__ __forceinline__ uint64_t mul(uint64_t a, uint64_t b) {
+  const uint32_t a0 = lo32(a), a1 = hi32(a), b0 = lo32(b), b1 = hi32(b);
+  const uint64_t L = (uint64_t)a0 * b0;
+  const uint64_t T = (uint64_t)a0 * b1 + hi32(L);
+  const uint64_t U = (uint64_t)a1 * b0 + lo32(T);
+  const uint64_t V = (uint64_t)a1 * b1 + hi32(T);
+  const uint64_t W = V + hi32(U);  // < 2^64: a1 b1 + 2 (2^32 - 1) < 2^64
+  // 128-bit product = X + 2^64 W, X = (L0, U0);  ≡ X + eps*w2 - w3
+  const uint64_t X = ((uint64_t)lo32(U) << 32) | lo32(L);
+  uint64_t t, c1, c2, c3;
+  uint32_t e;
+  asm("v_mad_u64_u32 %0, %1, %2, -1, %3" : "=v"(t), "=s"(c1) : "v"(lo32(W)), "v"(X));
+  asm("v_cndmask_b32_e64 %0, 0, -1, %1" : "=v"(e) : "s"(c1));
+  // carry: true value t + 2^64 ≡ t + eps; t < 2^64 - 2^33 then, no overflow
+  asm("v_mad_u64_u32 %0, %1, %2, 1, %3" : "=v"(t), "=s"(c2) : "v"(e), "v"(t));
+  // t - w3, borrow b (worth -2^64 ≡ -eps)
+  uint32_t r0 = lo32(t), r1 = hi32(t);
+  asm("v_sub_co_u32_e64 %0, %1, %2, %3" : "=v"(r0), "=s"(c3) : "v"(r0), "v"(hi32(W)));
+  asm("v_subb_co_u32_e64 %0, %1, %2, 0, %3" : "=v"(r1), "=s"(c3) : "v"(r1), "s"(c3));
+  asm("v_cndmask_b32_e64 %0, 0, -1, %1" : "=v"(e) : "s"(c3));
+  // borrow: t - w3 + 2^64 >= 2^64 - 2^32, minus eps stays >= 0
+  asm("v_sub_co_u32_e64 %0, %1, %2, %3" : "=v"(r0), "=s"(c3) : "v"(r0), "v"(e));
+  asm("v_subb_co_u32_e64 %0, %1, %2, 0, %3" : "=v"(r1), "=s"(c3) : "v"(r1), "s"(c3));
+  return ((uint64_t)r1 << 32) | r0;
+}
+
+// C forms of the same (compiler-chosen carries)
+__device__ __forceinline__ uint64_t reduce_row_c(uint64_t al, uint64_t ah) {
+  const uint64_t t = al + (ah >> 32) * EPS;
+  const uint32_t t1 = hi32(t) + lo32(ah);
+  const uint64_t r = ((uint64_t)t1 << 32) | lo32(t);
+  return t1 < lo32(ah) ? r + EPS : r;
+}
+__device__ __forceinline__ uint64_t mul_c(uint64_t a, uint64_t b) {
+  const uint32_t a0 = lo32(a), a1 = hi32(a), b0 = lo32(b), b1 = hi32(b);
+  const uint64_t L = (uint64_t)a0 * b0;
+  const uint64_t T = (uint64_t)a0 * b1 + hi32(L);
+  const uint64_t U = (uint64_t)a1 * b0 + lo32(T);
+  const uint64_t V = (uint64_t)a1 * b1 + hi32(T);
+  const uint64_t W = V + hi32(U);
+  const uint64_t X = ((uint64_t)lo32(U) << 32) | lo32(L);
+  uint64_t t = X + (uint64_t)lo32(W) * EPS;
+  t = t < X ? t + EPS : t;
+  const uint64_t w3 = hi32(W);
+  const uint64_t r = t - w3;
+  return t < w3 ? r - EPS : r;
+}
+__device__ __forceinline__ uint64_t sbox_c(uint64_t x) {
+  const uint64_t x2 = mul_c(x, x);
+  const uint64_t x3 = mul_c(x2, x);
+  const uint64_t x4 = mul_c(x2, x2);
+  return mul_c(x3, x4);
+}
+
+__device__ __forceinline__ uint64_t sbox(uint64_t x) {
+  const uint64_t x2 = mul(x, x);
+  const uint64_t x3 = mul(x2, x);
+  const uint64_t x4 = mul(x2, x2);
+  return mul(x3, x4);
+}
+
+// a + c, a in [0, 2^64), c < p
+__device__ __forceinline__ uint64_t add_c(uint64_t a, uint64_t c) {
+  const uint64_t s = a + c;
+  return s + (s < c ? EPS : 0);
+}
+
+__device__ __forceinline__ uint64_t canon(uint64_t x) { return x >= P ? x - P : x; }
+
+// MDS row R with the next round's constant k folded in (k < p, as SGPR halves)
+template <int M, int R, int I>
+__device__ __forceinline__ void row_terms(uint64_t &al, uint64_t &ah, const uint32_t lo[12], const uint32_t hi[12]) {
+  if constexpr (I < 12) {
+    constexpr int C = (int)ps::mds_circ(I) + ((R == 0 && I == 0) ? 8 : 0);
+    if constexpr (M == 0) {
+      al = mad_c<C>(lo[(I + R) % 12], al);
+      ah = mad_c<C>(hi[(I + R) % 12], ah);
+    } else {
+      const uint32_t c = opaque<C>();
+      al += (uint64_t)lo[(I + R) % 12] * c;
+      ah += (uint64_t)hi[(I + R) % 12] * c;
+    }
+    row_terms<M, R, I + 1>(al, ah, lo, hi);
+  }
+}
+
+template <int M, int R, int RC>
+__device__ __forceinline__ void mds_rows(uint64_t s[12], const uint32_t lo[12], const uint32_t hi[12]) {
+  if constexpr (R < 12) {
+    constexpr int C0 = (int)ps::mds_circ(0) + (R == 0 ? 8 : 0);
+    uint64_t al, ah;
+    constexpr uint64_t k = RC >= 0 ? ps::rc_cx(RC * 12 + R) : 0;
+    if constexpr (M == 0) {
+      // constant of the next round folded into the accumulators' start
+      if constexpr (RC >= 0) {
+        al = mad_cs<C0>(lo[R], k & EPS);
+        ah = mad_cs<C0>(hi[R], k >> 32);
+      } else {
+        al = mad_c<C0>(lo[R], 0);
+        ah = mad_c<C0>(hi[R], 0);
+      }
+    } else {
+      const uint32_t c = opaque<C0>();
+      al = (uint64_t)lo[R] * c + (k & EPS);
+      ah = (uint64_t)hi[R] * c + (k >> 32);
+    }
+    row_terms<M, R, 1>(al, ah, lo, hi);
+    s[R] = M == 2 ? reduce_row_c(al, ah) : reduce_row(al, ah);
+    mds_rows<M, R + 1, RC>(s, lo, hi);
+  }
+}
+
+// s <- MDS(s) + RC[next] (next < 0: no constant)
+template <int M, int NEXT>
+__device__ __forceinline__ void mds(uint64_t s[12]) {
+  uint32_t lo[12], hi[12];
+#pragma unroll
+  for (int i = 0; i < 12; i++) {
+    lo[i] = lo32(s[i]);
+    hi[i] = hi32(s[i]);
+  }
+  mds_rows<M, 0, NEXT>(s, lo, hi);
+}
+
+template <int M, int R>
+__device__ __forceinline__ void rounds(uint64_t s[12]) {
+  if constexpr (R < 30) {
+    constexpr bool full = R < 4 || R >= 26;
+    if constexpr (full) {
+#pragma unroll
+      for (int i = 0; i < 12; i++) s[i] = M == 2 ? sbox_c(s[i]) : sbox(s[i]);
+    } else {
+      s[0] = M == 2 ? sbox_c(s[0]) : sbox(s[0]);
+    }
+    mds<M, R + 1 < 30 ? R + 1 : -1>(s);
+    rounds<M, R + 1>(s);
+  }
+}
+
+// permutation; inputs in [0, 2^64), outputs in [0, 2^64) (canon() lanes read out)
+// M: 0 = asm mads, 1 = compiler mads on opaque constants, 2 = 1 + C reductions
+template <int M = 1>
+__device__ __forceinline__ void permute_nc(uint64_t s[12]) {
+#pragma unroll
+  for (int i = 0; i < 12; i++) s[i] = add_c(s[i], ps::rc_cx(i));
+  rounds<M, 0>(s);
+}
+
+template <int M = 1>
+__device__ __forceinline__ void permute(uint64_t s[12]) {
+  permute_nc<M>(s);
+#pragma unroll
+  for (int i = 0; i < 12; i++) s[i] = canon(s[i]);
+}
+
+}  // namespace pf
