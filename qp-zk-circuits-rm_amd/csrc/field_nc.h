@@ -9,6 +9,7 @@
 #pragma once
 #include <stdint.h>
 #include <hip/hip_runtime.h>
+#include "poseidon_fast.h"
 
 namespace gfn {
 
@@ -69,23 +70,9 @@ __device__ __forceinline__ uint64_t reduce(uint64_t lo, uint64_t hi) {
   return pack(l0, l1);
 }
 
-__device__ __forceinline__ uint64_t mul(uint64_t a, uint64_t b) {
-  const uint32_t a0 = (uint32_t)a, a1 = (uint32_t)(a >> 32), b0 = (uint32_t)b, b1 = (uint32_t)(b >> 32);
-  const uint64_t p00 = (uint64_t)a0 * b0;
-  const uint64_t m = (uint64_t)a1 * b0 + (p00 >> 32);
-  const uint64_t m2 = (uint64_t)a0 * b1 + (uint32_t)m;
-  const uint64_t h = (uint64_t)a1 * b1 + (m >> 32);
-  uint32_t c;
-  const uint32_t hl = __builtin_addc((uint32_t)h, (uint32_t)(m2 >> 32), 0u, &c);
-  const uint32_t hh = (uint32_t)(h >> 32) + c;
-  return reduce(pack((uint32_t)p00, (uint32_t)m2), pack(hl, hh));
-}
+// product and sbox: the asm forms of poseidon_fast.h (5 mads + 8-op reduction)
+__device__ __forceinline__ uint64_t mul(uint64_t a, uint64_t b) { return pf::mul(a, b); }
 
-__device__ __forceinline__ uint64_t sbox(uint64_t x) {
-  const uint64_t x2 = mul(x, x);
-  const uint64_t x3 = mul(x2, x);
-  const uint64_t x4 = mul(x2, x2);
-  return mul(x3, x4);
-}
+__device__ __forceinline__ uint64_t sbox(uint64_t x) { return pf::sbox(x); }
 
 }  // namespace gfn

@@ -15,6 +15,7 @@
 #pragma once
 #include "field.h"
 #include "kernels.h"
+#include "poseidon_fast.h"
 
 namespace nt {
 
@@ -47,11 +48,8 @@ __device__ __forceinline__ uint64_t reduce(uint64_t lo, uint64_t hi) {
   return r + (r < t1 ? EPS : 0);
 }
 
-__device__ __forceinline__ uint64_t mul(uint64_t a, uint64_t b) {
-  uint64_t lo, hi;
-  gl::mul_wide(a, b, lo, hi);
-  return reduce(lo, hi);
-}
+// general product: the asm form (5 mads + 8-op reduction, poseidon_fast.h)
+__device__ __forceinline__ uint64_t mul(uint64_t a, uint64_t b) { return pf::mul(a, b); }
 
 __device__ __forceinline__ uint64_t canon(uint64_t x) { return x >= gl::P ? x - gl::P : x; }
 

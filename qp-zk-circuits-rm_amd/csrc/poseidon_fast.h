@@ -161,6 +161,30 @@ __device__ __forceinline__ void row_terms(uint64_t &al, uint64_t &ah, const uint
   }
 }
 
+// runtime-constant variant: s <- MDS(s) + k (k[12] wave-uniform, < p)
+template <int R>
+__device__ __forceinline__ void mds_rows_k(uint64_t s[12], const uint32_t lo[12], const uint32_t hi[12],
+                                           const uint64_t k[12]) {
+  if constexpr (R < 12) {
+    constexpr int C0 = (int)ps::mds_circ(0) + (R == 0 ? 8 : 0);
+    uint64_t al = mad_cs<C0>(lo[R], k[R] & EPS);
+    uint64_t ah = mad_cs<C0>(hi[R], k[R] >> 32);
+    row_terms<0, R, 1>(al, ah, lo, hi);
+    s[R] = reduce_row(al, ah);
+    mds_rows_k<R + 1>(s, lo, hi, k);
+  }
+}
+
+__device__ __forceinline__ void mds_k(uint64_t s[12], const uint64_t k[12]) {
+  uint32_t lo[12], hi[12];
+#pragma unroll
+  for (int i = 0; i < 12; i++) {
+    lo[i] = lo32(s[i]);
+    hi[i] = hi32(s[i]);
+  }
+  mds_rows_k<0>(s, lo, hi, k);
+}
+
 template <int M, int R, int RC>
 __device__ __forceinline__ void mds_rows(uint64_t s[12], const uint32_t lo[12], const uint32_t hi[12]) {
   if constexpr (R < 12) {

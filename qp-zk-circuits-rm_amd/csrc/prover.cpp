@@ -452,7 +452,7 @@ int prove_batch(qp_prover *P, const uint64_t *const *wires_host, const uint64_t 
     a.num_constants = P->NC;
     a.g = P->gdesc;
     kt_begin(P, 3);
-    qpk::k_quotient<<<dim3(cdiv(N, 256), nb), 256, 0, s>>>(a);
+    qpk::k_quotient<2><<<dim3(cdiv(N, 256), nb), 256, 0, s>>>(a);
     kt_end(P, 3, (double)nb * N);
     const uint64_t n_inv = gl::inv(n);
     qpk::k_qintt_blocks<<<dim3(B, nc, nb), 512, 8u << P->log_n, s>>>(P->qvals.p, P->cbuf.p, P->log_n, P->rate_bits,

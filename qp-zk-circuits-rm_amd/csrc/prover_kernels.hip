@@ -133,10 +133,18 @@ struct TermAcc {
   }
 };
 
+// Poseidon gate constraints (plonky2 PoseidonGate): the MDS of
+// round r adds round r+1's constants (poseidon_fast.h folding), so each round
+// starts with its constants already in the state.
+__device__ __forceinline__ void rc_row(uint64_t k[12], int r) {
+#pragma unroll
+  for (int i = 0; i < 12; i++) k[i] = ps::RC_DEV[r * 12 + i];
+}
+
 __device__ __forceinline__ void poseidon_gate(const uint64_t *__restrict__ wl, uint64_t N, TermAcc &A) {
   const uint64_t swap = WV(24);
   A.emit(gfn::mul(swap, gfn::sub(swap, 1)));
-  uint64_t s[12];
+  uint64_t s[12], k[12];
 #pragma unroll
   for (int i = 0; i < 4; i++) {
     const uint64_t delta = WV(25 + i), a = WV(i), c = WV(i + 4);
@@ -147,9 +155,9 @@ __device__ __forceinline__ void poseidon_gate(const uint64_t *__restrict__ wl, u
 #pragma unroll
   for (int i = 8; i < 12; i++) s[i] = WV(i);
 #pragma unroll
-  for (int r = 0; r < 4; r++) {
+  for (int i = 0; i < 12; i++) s[i] = gfn::add_c(s[i], ps::RC_DEV[i]);
 #pragma unroll
-    for (int i = 0; i < 12; i++) s[i] = gfn::add_c(s[i], ps::RC_DEV[r * 12 + i]);
+  for (int r = 0; r < 4; r++) {
     if (r) {
 #pragma unroll
       for (int i = 0; i < 12; i++) {
@@ -160,22 +168,18 @@ __device__ __forceinline__ void poseidon_gate(const uint64_t *__restrict__ wl, u
     }
 #pragma unroll
     for (int i = 0; i < 12; i++) s[i] = gfn::sbox(s[i]);
-    psd::mds_nc(s);
+    rc_row(k, r + 1);
+    pf::mds_k(s, k);
   }
   for (int r = 0; r < 22; r++) {
-    const int rc = 4 + r;
-#pragma unroll
-    for (int i = 0; i < 12; i++) s[i] = gfn::add_c(s[i], ps::RC_DEV[rc * 12 + i]);
     const uint64_t sb = WV(65 + r);
     A.emit(gfn::sub(s[0], sb));
     s[0] = gfn::sbox(sb);
-    psd::mds_nc(s);
+    rc_row(k, 5 + r);
+    pf::mds_k(s, k);
   }
 #pragma unroll
   for (int r = 0; r < 4; r++) {
-    const int rc = 26 + r;
-#pragma unroll
-    for (int i = 0; i < 12; i++) s[i] = gfn::add_c(s[i], ps::RC_DEV[rc * 12 + i]);
 #pragma unroll
     for (int i = 0; i < 12; i++) {
       const uint64_t sb = WV(87 + r * 12 + i);
@@ -184,13 +188,29 @@ __device__ __forceinline__ void poseidon_gate(const uint64_t *__restrict__ wl, u
     }
 #pragma unroll
     for (int i = 0; i < 12; i++) s[i] = gfn::sbox(s[i]);
-    psd::mds_nc(s);
+    if (r < 3) {
+      rc_row(k, 27 + r);
+      pf::mds_k(s, k);
+    } else {
+      pf::mds<0, -1>(s);
+    }
   }
 #pragma unroll
   for (int i = 0; i < 12; i++) A.emit(gfn::sub(s[i], WV(12 + i)));
 }
 
-__global__ void __launch_bounds__(256) k_quotient(QuotientArgs a) {
+// Two phases with separate register allocation (the Poseidon gate alone is
+// a permutation's worth of live state; fused, the kernel needed 184 VGPRs =
+// 2 waves/SIMD):
+//   PH 0: L_0 terms, partial-product checks, every gate except Poseidon;
+//         raw (non-canonical) alpha sums -> q_out
+//   PH 1: Poseidon gates; adds the PH 0 sums, multiplies by 1/Z_H, canonical.
+//   PH 2: both in one pass (measured faster: 27.6 vs 30.4 ms at batch 256 —
+//         the second pass re-reads the wires; the fused kernel runs at 4
+//         waves/SIMD with a small spill).  PH 0/1 are kept for register-budget
+//         experiments.
+template <int PH>
+__global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) k_quotient(QuotientArgs a) {
   const uint32_t logN = a.log_n + a.rate_bits;
   const uint64_t N = 1ull << logN, n = 1ull << a.log_n;
   const uint32_t t = blockIdx.x * blockDim.x + threadIdx.x;
@@ -201,46 +221,49 @@ __global__ void __launch_bounds__(256) k_quotient(QuotientArgs a) {
   const uint64_t *wl = a.w_lde + b * a.w_bstride + t;      // [W][N]
   const uint64_t *zl = a.z_lde + b * a.z_bstride;          // [nzs][N]
   const uint32_t j = gl::rev_bits(t, logN);                // natural point index
-  const uint32_t tn = gl::rev_bits((j + (1u << a.rate_bits)) & (uint32_t)(N - 1), logN);
-  const uint64_t x = gl::mul(gl::GEN, wpow_N(a.tw, j, logN));
-  const uint64_t zh = a.zh[j & ((1u << a.rate_bits) - 1)];
-  const uint64_t zh_inv = a.zh_inv[j & ((1u << a.rate_bits) - 1)];
+  uint64_t *q = a.q_out + b * a.q_bstride;
   TermAcc A;
   A.p0 = a.apow + (uint64_t)b * 2 * APOW_STRIDE;
   A.p1 = A.p0 + APOW_STRIDE;
   A.s0 = A.s1 = 0;
   A.i = 0;
-  // L_0(x) (Z_c - 1)
-  const uint64_t l0 = gl::mul(zh, gl::inv(gl::mul(gl::sub(x, 1), n % gl::P)));
-  for (uint32_t c = 0; c < 2; c++) A.emit(gfn::mul(l0, gfn::sub(zl[(uint64_t)c * N + t], 1)));
-  // partial-product checks
   const uint32_t R = a.R, qdf = a.qdf, nchunks = (R + qdf - 1) / qdf, npp = nchunks - 1;
-  for (uint32_t c = 0; c < 2; c++) {
-    const uint64_t beta = ch[CH_BETA + c], gamma = ch[CH_GAMMA + c];
-    uint64_t bkx = gfn::mul(beta, x);  // beta * k_j * x with k_j = g^j
-    for (uint32_t k = 0; k < nchunks; k++) {
-      uint64_t num = 1, den = 1;
-      for (uint32_t jj = k * qdf; jj < (k + 1) * qdf && jj < R; jj++) {
-        const uint64_t wv = WV(jj);
-        const uint64_t wg = gfn::add_c(wv, gamma);
-        num = gfn::mul(num, gfn::add(wg, bkx));
-        den = gfn::mul(den, gfn::add(wg, gfn::mul(beta, cs[(uint64_t)(a.num_constants + jj) * N])));
-        bkx = gfn::mul(bkx, gl::GEN);
+  if (PH != 1) {
+    const uint32_t tn = gl::rev_bits((j + (1u << a.rate_bits)) & (uint32_t)(N - 1), logN);
+    const uint64_t x = gl::mul(gl::GEN, wpow_N(a.tw, j, logN));
+    const uint64_t zh = a.zh[j & ((1u << a.rate_bits) - 1)];
+    // L_0(x) (Z_c - 1)
+    const uint64_t l0 = gl::mul(zh, gl::inv(gl::mul(gl::sub(x, 1), n % gl::P)));
+    for (uint32_t c = 0; c < 2; c++) A.emit(gfn::mul(l0, gfn::sub(zl[(uint64_t)c * N + t], 1)));
+    // partial-product checks
+    for (uint32_t c = 0; c < 2; c++) {
+      const uint64_t beta = ch[CH_BETA + c], gamma = ch[CH_GAMMA + c];
+      uint64_t bkx = gfn::mul(beta, x);  // beta * k_j * x with k_j = g^j
+      for (uint32_t k = 0; k < nchunks; k++) {
+        uint64_t num = 1, den = 1;
+        for (uint32_t jj = k * qdf; jj < (k + 1) * qdf && jj < R; jj++) {
+          const uint64_t wv = WV(jj);
+          const uint64_t wg = gfn::add_c(wv, gamma);
+          num = gfn::mul(num, gfn::add(wg, bkx));
+          den = gfn::mul(den, gfn::add(wg, gfn::mul(beta, cs[(uint64_t)(a.num_constants + jj) * N])));
+          bkx = gfn::mul(bkx, gl::GEN);
+        }
+        const uint64_t prev = k == 0 ? zl[(uint64_t)c * N + t] : zl[((uint64_t)2 + c * npp + k - 1) * N + t];
+        const uint64_t next = k == nchunks - 1 ? zl[(uint64_t)c * N + tn] : zl[((uint64_t)2 + c * npp + k) * N + t];
+        A.emit(gfn::sub(gfn::mul(prev, num), gfn::mul(next, den)));
       }
-      const uint64_t prev = k == 0 ? zl[(uint64_t)c * N + t] : zl[((uint64_t)2 + c * npp + k - 1) * N + t];
-      const uint64_t next = k == nchunks - 1 ? zl[(uint64_t)c * N + tn] : zl[((uint64_t)2 + c * npp + k) * N + t];
-      A.emit(gfn::sub(gfn::mul(prev, num), gfn::mul(next, den)));
     }
   }
   // gate constraints: every gate's terms start at alpha^(#pre-terms); the
   // selector filter multiplies each gate's sum once
-  const uint32_t pre = A.i;
-  uint64_t acc0 = A.s0, acc1 = A.s1;
+  const uint32_t pre = 2 * (1 + nchunks);
+  uint64_t acc0 = A.s0, acc1 = A.s1;  // PH 1 adds the PH 0 sums at the end
   uint64_t consts[8];
   for (uint32_t k = 0; k < a.num_constants && k < 8; k++) consts[k] = cs[(uint64_t)k * N];
   const uint32_t nsel = a.g.nsel;
   for (uint32_t gi = 0; gi < a.g.ngates; gi++) {
-    if (a.g.kind[gi] == GK_NOOP) continue;
+    const uint32_t kind = a.g.kind[gi];
+    if (kind == GK_NOOP || (PH == 0 && kind == GK_POSEIDON) || (PH == 1 && kind != GK_POSEIDON)) continue;
     const uint32_t si = a.g.sel_index[gi];
     const uint64_t s = consts[si];
     uint64_t f = 1;
@@ -250,44 +273,57 @@ __global__ void __launch_bounds__(256) k_quotient(QuotientArgs a) {
     A.s0 = A.s1 = 0;
     A.i = pre;
     const uint64_t *gc = consts + nsel;
-    switch (a.g.kind[gi]) {
-      case GK_CONSTANT:
-        for (uint32_t i = 0; i < a.g.param[gi]; i++) A.emit(gfn::sub(gc[i], WV(i)));
-        break;
-      case GK_PUBLIC_INPUT:
-        for (uint32_t i = 0; i < 4; i++) A.emit(gfn::sub(WV(i), ch[CH_PIH + i]));
-        break;
-      case GK_BASE_SUM: {
-        const uint32_t L = a.g.param[gi];
-        uint64_t acc = 0;
-        for (uint32_t i = L; i-- > 0;) acc = gfn::add(gfn::add(acc, acc), WV(1 + i));
-        A.emit(gfn::sub(acc, WV(0)));
-        for (uint32_t i = 0; i < L; i++) {
-          const uint64_t l = WV(1 + i);
-          A.emit(gfn::mul(l, gfn::sub(l, 1)));
+    if (kind == GK_POSEIDON) {
+      poseidon_gate(wl, N, A);
+    } else {
+      switch (kind) {
+        case GK_CONSTANT:
+          for (uint32_t i = 0; i < a.g.param[gi]; i++) A.emit(gfn::sub(gc[i], WV(i)));
+          break;
+        case GK_PUBLIC_INPUT:
+          for (uint32_t i = 0; i < 4; i++) A.emit(gfn::sub(WV(i), ch[CH_PIH + i]));
+          break;
+        case GK_BASE_SUM: {
+          const uint32_t L = a.g.param[gi];
+          uint64_t acc = 0;
+          for (uint32_t i = L; i-- > 0;) acc = gfn::add(gfn::add(acc, acc), WV(1 + i));
+          A.emit(gfn::sub(acc, WV(0)));
+          for (uint32_t i = 0; i < L; i++) {
+            const uint64_t l = WV(1 + i);
+            A.emit(gfn::mul(l, gfn::sub(l, 1)));
+          }
+          break;
         }
-        break;
+        case GK_ARITHMETIC:
+          for (uint32_t i = 0; i < a.g.param[gi]; i++) {
+            const uint64_t comp = gfn::add(gfn::mul(gfn::mul(WV(4 * i), WV(4 * i + 1)), gc[0]),
+                                           gfn::mul(WV(4 * i + 2), gc[1]));
+            A.emit(gfn::sub(WV(4 * i + 3), comp));
+          }
+          break;
+        default:
+          break;
       }
-      case GK_ARITHMETIC:
-        for (uint32_t i = 0; i < a.g.param[gi]; i++) {
-          const uint64_t comp = gfn::add(gfn::mul(gfn::mul(WV(4 * i), WV(4 * i + 1)), gc[0]),
-                                         gfn::mul(WV(4 * i + 2), gc[1]));
-          A.emit(gfn::sub(WV(4 * i + 3), comp));
-        }
-        break;
-      case GK_POSEIDON:
-        poseidon_gate(wl, N, A);
-        break;
-      default:
-        break;
     }
     acc0 = gfn::add(acc0, gfn::mul(f, A.s0));
     acc1 = gfn::add(acc1, gfn::mul(f, A.s1));
   }
-  uint64_t *q = a.q_out + b * a.q_bstride;
-  q[t] = gfn::canon(gfn::mul(acc0, zh_inv));
-  q[N + t] = gfn::canon(gfn::mul(acc1, zh_inv));
+  if (PH == 0) {
+    q[t] = acc0;
+    q[N + t] = acc1;
+  } else {
+    if (PH == 1) {
+      acc0 = gfn::add(acc0, q[t]);
+      acc1 = gfn::add(acc1, q[N + t]);
+    }
+    const uint64_t zh_inv = a.zh_inv[j & ((1u << a.rate_bits) - 1)];
+    q[t] = gfn::canon(gfn::mul(acc0, zh_inv));
+    q[N + t] = gfn::canon(gfn::mul(acc1, zh_inv));
+  }
 }
+template __global__ void k_quotient<0>(QuotientArgs);
+template __global__ void k_quotient<1>(QuotientArgs);
+template __global__ void k_quotient<2>(QuotientArgs);
 #undef WV
 
 // coset iNTT, stage 1: block s' holds coset s = rev_r(s') values in bit-reversed

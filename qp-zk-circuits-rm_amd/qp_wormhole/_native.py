@@ -10,7 +10,7 @@ import re
 import numpy as np
 
 HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(HERE, "libqpgpu.so")
+LIB_PATH = os.environ.get("QPGPU_LIB") or os.path.join(HERE, "libqpgpu.so")  # QPGPU_LIB: A/B tuning builds
 HEADER = os.path.join(os.path.dirname(os.path.dirname(HERE)), "include", "qpgpu.h")
 
 U64P = np.ctypeslib.ndpointer(np.uint64, flags="C_CONTIGUOUS")
