@@ -3,6 +3,7 @@
 # first step that crashes/aborts/times out (exit >= 2 other than pytest's 1).
 cd "${GRAFT_REPO_ROOT:-/root/repo}"
 mkdir -p gpurun_out
+export TMPDIR=/tmp
 step() {  # step <name> <timeout> <cmd...>
   local name=$1 to=$2; shift 2
   echo "=== $name: $*" | tee -a gpurun_out/session.log
@@ -13,15 +14,26 @@ step() {  # step <name> <timeout> <cmd...>
   if [ $rc -ne 0 ] && [ $rc -ne 1 ]; then echo "stopping after $name (rc=$rc)"; exit $rc; fi
   return 0
 }
+# PMC passes over a short bench run, one counter group per pass (FETCH_SIZE
+# takes 3 of the 4 TCC slots and WRITE_SIZE 2, so they need separate runs)
+pmc() {  # pmc <name> <counters...>
+  local name=$1; shift
+  step "pmc_$name" 300 rocprofv3 --pmc "$@" --output-format csv -d "gpurun_out/pmc_$name" -o run -- \
+    python3 bench.py --steps 1 --warmup 1 --cpu-sample 0 --batch 64
+}
 for s in "$@"; do
   case $s in
     build) step build 600 make -s -C qp-zk-circuits-rm_amd/csrc -j16 ;;
     oracle) step oracle 300 make -s -C oracle ;;
-    test) step pytest_gpu 900 python -m pytest tests -m gpu -x -q ;;
+    test) step pytest_gpu 900 python -u -m pytest tests -m gpu -x -v --timeout 300 --timeout-method thread ;;
+    smoke) step smoke 300 python -c "import __graft_entry__ as g; g.smoke()" ;;
     kbench) step kbench 300 python tools/kbench.py 8 5 ;;
-    prof) export TMPDIR=/tmp; step rocprof 600 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/prof -o run -- python3 tools/kbench.py 8 3 ;;
+    prof) step rocprof 600 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/prof -o run -- python3 tools/kbench.py 8 3 ;;
     bench) step bench 900 python bench.py ;;
-    benchprof) export TMPDIR=/tmp; step rocprof_bench 900 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/prof_bench -o run -- python3 bench.py --steps 2 --warmup 1 --cpu-sample 0 ;;
+    benchprof) step rocprof_bench 900 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/prof_bench -o run -- python3 bench.py --steps 2 --warmup 1 --cpu-sample 0 ;;
+    pmc_fetch) pmc fetch FETCH_SIZE ;;
+    pmc_write) pmc write WRITE_SIZE ;;
+    pmc_valu) pmc valu SQ_WAVES SQ_INSTS_VALU SQ_WAVE_CYCLES SQ_BUSY_CYCLES ;;
     *) echo "unknown step $s" ;;
   esac
 done
