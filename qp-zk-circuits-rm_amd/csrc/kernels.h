@@ -13,10 +13,16 @@ namespace qpk {
 
 constexpr unsigned TW_LOG = 16;  // twiddle tables cover sizes up to 2^16
 
+constexpr unsigned LDE_MAX_RATE = 4;  // coset-fused LDE kernel: up to 16 cosets
+
 struct Twiddles {
   uint64_t *fwd = nullptr;  // fwd[j] = w_{2^TW_LOG}^j,   j < 2^(TW_LOG-1)
   uint64_t *inv = nullptr;  // inv[j] = w_{2^TW_LOG}^-j
+  // coset pre-twists of the fused LDE: for rate r (1..LDE_MAX_RATE), at
+  // offset 16*(2^r - 2): ptw[16 s + m] = w_{16*2^r}^(s*m), s < 2^r, m < 16
+  uint64_t *ptw = nullptr;
 };
+__host__ __device__ inline uint32_t ptw_offset(uint32_t rate_bits) { return 16u * ((1u << rate_bits) - 2u); }
 
 hipError_t twiddles_init(Twiddles &t, hipStream_t s);
 void twiddles_free(Twiddles &t);

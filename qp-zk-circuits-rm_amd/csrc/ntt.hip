@@ -9,12 +9,32 @@
 //     DIF leaves block s in bit-reversed order, which is exactly Merkle-leaf
 //     order at rows rev_r(s)*n + p.
 //   * ifft is a DIF with inverse twiddles and a bit-reversed LDS read on store.
+#include <stdlib.h>
+#include <vector>
 #include "field.h"
 #include "kernels.h"
 #include "ntt_device.h"
 #include "ntt16.h"
 
+// occupancy target of the LDS NTT kernels (64 KiB LDS per size-2^13 workgroup
+// allows 2 workgroups = 4 waves per SIMD; uncapped, the compiler spends ~165
+// VGPRs and only one workgroup fits per CU).  QP_NTT_WAVES=0: no cap.
+#ifndef QP_NTT_WAVES
+#define QP_NTT_WAVES 4
+#endif
+#if QP_NTT_WAVES
+#define QP_NTT_OCC __attribute__((amdgpu_waves_per_eu(QP_NTT_WAVES)))
+#else
+#define QP_NTT_OCC
+#endif
+
 namespace qpk {
+
+// A/B switch for measurements: QPGPU_LDE_PERCOSET=1 selects the per-coset LDE
+static bool getenv_flag(const char *name) {
+  const char *v = getenv(name);
+  return v && v[0] && v[0] != '0';
+}
 
 __global__ void k_twiddles(uint64_t *fwd, uint64_t *inv, uint64_t w, uint64_t wi, uint32_t half) {
   uint32_t j = blockIdx.x * blockDim.x + threadIdx.x;
@@ -32,16 +52,30 @@ hipError_t twiddles_init(Twiddles &t, hipStream_t s) {
   if (e) return e;
   uint64_t w = gl::root_of_unity(TW_LOG);
   k_twiddles<<<(half + 255) / 256, 256, 0, s>>>(t.fwd, t.inv, w, gl::inv(w), half);
-  return hipGetLastError();
+  e = hipGetLastError();
+  if (e) return e;
+  // coset pre-twists of k_lde_cosets
+  std::vector<uint64_t> ptw(ptw_offset(LDE_MAX_RATE + 1));
+  for (uint32_t r = 1; r <= LDE_MAX_RATE; r++) {
+    const uint64_t wr = gl::root_of_unity(4 + r);
+    for (uint32_t sc = 0; sc < (1u << r); sc++)
+      for (uint32_t m = 0; m < 16; m++) ptw[ptw_offset(r) + 16 * sc + m] = gl::pow(wr, (uint64_t)sc * m);
+  }
+  e = hipMalloc(&t.ptw, ptw.size() * 8);
+  if (e) return e;
+  e = hipMemcpyAsync(t.ptw, ptw.data(), ptw.size() * 8, hipMemcpyHostToDevice, s);
+  if (e) return e;
+  return hipStreamSynchronize(s);
 }
 
 void twiddles_free(Twiddles &t) {
   if (t.fwd) (void)hipFree(t.fwd);
   if (t.inv) (void)hipFree(t.inv);
-  t.fwd = t.inv = nullptr;
+  if (t.ptw) (void)hipFree(t.ptw);
+  t.fwd = t.inv = t.ptw = nullptr;
 }
 
-__global__ void __launch_bounds__(512) k_intt(const uint64_t *__restrict__ in, uint64_t in_stride,
+__global__ void __launch_bounds__(512) QP_NTT_OCC k_intt(const uint64_t *__restrict__ in, uint64_t in_stride,
                                               uint64_t *__restrict__ out, uint64_t out_stride, uint32_t log_n,
                                               uint64_t n_inv, const uint64_t *__restrict__ tw_inv,
                                               uint64_t in_bstride, uint64_t out_bstride) {
@@ -55,7 +89,7 @@ __global__ void __launch_bounds__(512) k_intt(const uint64_t *__restrict__ in, u
   for (uint32_t m = threadIdx.x; m < n; m += blockDim.x) dst[m] = gl::mul(lds[gl::rev_bits(m, log_n)], n_inv);
 }
 
-__global__ void __launch_bounds__(512) k_lde(const uint64_t *__restrict__ coeffs, uint64_t c_stride,
+__global__ void __launch_bounds__(512) QP_NTT_OCC k_lde(const uint64_t *__restrict__ coeffs, uint64_t c_stride,
                                              uint64_t *__restrict__ out, uint64_t o_stride, uint32_t log_n,
                                              uint32_t rate_bits, uint64_t shift, const uint64_t *__restrict__ tw,
                                              uint64_t c_bstride, uint64_t o_bstride) {
@@ -80,6 +114,62 @@ __global__ void __launch_bounds__(512) k_lde(const uint64_t *__restrict__ coeffs
   for (uint32_t p = threadIdx.x; p < n; p += blockDim.x) dst[p] = nt::canon(lds[p]);
 }
 
+// Coset-fused LDE: one workgroup per column produces all B = 2^r cosets, so
+// the n coefficients are read from HBM once (the per-coset kernel above reads
+// them B times) and scaled by shift^k once.  n = 16 T (T = 2^LOG_T threads):
+// thread t holds a_m = c_{t+Tm} shift^{t+Tm}, m < 16, in registers — exactly
+// the inputs of its first radix-16 DIF butterfly.  For coset s the inputs are
+// a_m w_N^{s(t+Tm)} = w_N^{st} * (a_m w_{16B}^{sm}); the common factor w_N^{st}
+// commutes with the 16-point DFT and merges with the pass's own twiddle
+// w_n^{t brev4(j)} into one lookup w_N^{t(s + B brev4(j))}, so each coset costs
+// one pre-twist product per element instead of a scale and a power update.
+// The remaining levels run in LDS (ntt_lds_from); output rows in leaf order.
+template <int LOG_T>
+__global__ void __launch_bounds__(1 << LOG_T) QP_NTT_OCC k_lde_cosets(const uint64_t *__restrict__ coeffs, uint64_t c_stride,
+                                                          uint64_t c_bstride, uint64_t *__restrict__ out,
+                                                          uint64_t o_stride, uint64_t o_bstride, uint32_t rate_bits,
+                                                          uint64_t shift, uint64_t shift_T,
+                                                          const uint64_t *__restrict__ tw,
+                                                          const uint64_t *__restrict__ ptw) {
+  constexpr uint32_t T = 1u << LOG_T, LOG_N = LOG_T + 4;
+  extern __shared__ __attribute__((aligned(16))) uint64_t lds[];
+  const uint32_t t = threadIdx.x;
+  const uint64_t *src = coeffs + blockIdx.y * c_bstride + (uint64_t)blockIdx.x * c_stride;
+  uint64_t *dst0 = out + blockIdx.y * o_bstride + (uint64_t)blockIdx.x * o_stride;
+  uint64_t a[16];
+#pragma unroll
+  for (int m = 0; m < 16; m++) a[m] = src[t + T * m];
+  {
+    uint64_t f = gl::pow(shift, t);
+#pragma unroll
+    for (int m = 0; m < 16; m++) {
+      a[m] = nt::mul(a[m], f);
+      f = nt::mul(f, shift_T);
+    }
+  }
+  const uint32_t logN = LOG_N + rate_bits, B = 1u << rate_bits;
+  const uint64_t *pt = ptw + ptw_offset(rate_bits);
+  for (uint32_t s = 0; s < B; s++) {
+    uint64_t r[16];
+    r[0] = a[0];
+#pragma unroll
+    for (int m = 1; m < 16; m++) r[m] = nt::mul(a[m], pt[16 * s + m]);
+    nt::dft16<false>(r);
+#pragma unroll
+    for (int m = 0; m < 16; m++) {
+      const uint32_t e = t * (s + (nt::brev4(m) << rate_bits));
+      if (e) r[m] = nt::mul(r[m], nt::tw_pow(tw, e, logN));
+      lds[t + T * m] = r[m];
+    }
+    __syncthreads();
+    nt::ntt_lds_from<false>(lds, LOG_N, LOG_T, tw);
+    uint64_t *dst = dst0 + ((uint64_t)gl::rev_bits(s, rate_bits) << LOG_N);
+#pragma unroll
+    for (int m = 0; m < 16; m++) dst[t + T * m] = nt::canon(lds[t + T * m]);
+    __syncthreads();
+  }
+}
+
 static unsigned ntt_threads(uint32_t log_n) {
   uint32_t half = log_n ? (1u << (log_n - 1)) : 1;
   return half < 64 ? 64 : (half > 512 ? 512 : half);
@@ -98,6 +188,24 @@ void lde(const Twiddles &t, const uint64_t *coeffs, uint64_t c_stride, uint64_t 
          uint32_t ncols, uint32_t log_n, uint32_t rate_bits, uint64_t shift, uint32_t nbat, uint64_t c_bstride,
          uint64_t o_bstride, hipStream_t s) {
   if (!ncols || !nbat) return;
+  if (rate_bits >= 1 && rate_bits <= LDE_MAX_RATE && log_n >= 10 && log_n <= 13 && log_n + rate_bits <= TW_LOG &&
+      !getenv_flag("QPGPU_LDE_PERCOSET")) {
+    const uint32_t T = 1u << (log_n - 4);
+    const uint64_t shift_T = gl::pow(shift, T);
+    dim3 g(ncols, nbat);
+    const size_t lds_bytes = (size_t)8 << log_n;
+#define QP_LDE_COSETS(LT)                                                                                      \
+  k_lde_cosets<LT><<<g, 1u << LT, lds_bytes, s>>>(coeffs, c_stride, c_bstride, out, o_stride, o_bstride, rate_bits, \
+                                                  shift, shift_T, t.fwd, t.ptw)
+    switch (log_n) {
+      case 10: QP_LDE_COSETS(6); break;
+      case 11: QP_LDE_COSETS(7); break;
+      case 12: QP_LDE_COSETS(8); break;
+      default: QP_LDE_COSETS(9); break;
+    }
+#undef QP_LDE_COSETS
+    return;
+  }
   dim3 grid(1u << rate_bits, ncols, nbat);
   k_lde<<<grid, ntt_threads(log_n), (8u << log_n), s>>>(coeffs, c_stride, out, o_stride, log_n, rate_bits, shift,
                                                         t.fwd, c_bstride, o_bstride);

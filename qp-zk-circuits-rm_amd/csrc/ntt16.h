@@ -167,13 +167,14 @@ __device__ void tail(uint64_t *a, uint32_t n) {
   __syncthreads();
 }
 
-// In-place DIF over LDS a[0..2^log_n), all threads of the block participate.
+// In-place DIF over LDS a[0..2^log_n), all threads of the block participate,
+// starting at sub-problem size 2^log_S (log_S = log_n: the whole transform;
+// smaller: the levels above were already done, e.g. from registers).
 // tw = forward or inverse twiddle table matching INV.  Ends with a barrier.
 template <bool INV>
-__device__ void ntt_lds(uint64_t *a, uint32_t log_n, const uint64_t *__restrict__ tw) {
+__device__ void ntt_lds_from(uint64_t *a, uint32_t log_n, uint32_t log_S, const uint64_t *__restrict__ tw) {
   const uint32_t n = 1u << log_n;
   const uint32_t T = blockDim.x;
-  uint32_t log_S = log_n;
   // radix-16 passes
   while (log_S >= 4) {
     const uint32_t S = 1u << log_S, q = S >> 4, log_q = log_S - 4;
@@ -198,6 +199,11 @@ __device__ void ntt_lds(uint64_t *a, uint32_t log_n, const uint64_t *__restrict_
   if (log_S == 1) tail<INV, 1>(a, n);
   else if (log_S == 2) tail<INV, 2>(a, n);
   else if (log_S == 3) tail<INV, 3>(a, n);
+}
+
+template <bool INV>
+__device__ void ntt_lds(uint64_t *a, uint32_t log_n, const uint64_t *__restrict__ tw) {
+  ntt_lds_from<INV>(a, log_n, log_n, tw);
 }
 
 }  // namespace nt

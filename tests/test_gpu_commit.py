@@ -47,7 +47,7 @@ def test_ifft(ctx, log_n):
         assert (got[c] == e).all()
 
 
-@pytest.mark.parametrize("log_n,rate_bits", [(2, 1), (5, 3), (10, 3), (13, 3), (12, 4)])
+@pytest.mark.parametrize("log_n,rate_bits", [(2, 1), (5, 3), (10, 3), (13, 3), (12, 4), (11, 1), (11, 2), (13, 1), (10, 4), (14, 2)])
 def test_lde_leaf_order(ctx, log_n, rate_bits):
     import qp_wormhole
     rng = np.random.default_rng(100 + log_n)
