@@ -36,26 +36,33 @@ def parse():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=3)
     ap.add_argument("--warmup", type=int, default=1)
-    ap.add_argument("--batch", type=int, default=256, help="proofs per GPU per step")
-    ap.add_argument("--cpu-sample", type=int, default=2, help="proofs in the CPU baseline sample (0 = skip)")
+    ap.add_argument("--batch", type=int, default=0,
+                    help="proofs per GPU per step (default: 256 Wormhole, 1024 voting)")
+    ap.add_argument("--circuit", choices=["wormhole", "voting"], default="wormhole",
+                    help="wormhole = BASELINE configs[2] (the headline); voting = configs[4]")
+    ap.add_argument("--cpu-sample", type=int, default=2, help="min proofs in the CPU baseline sample (0 = skip)")
+    ap.add_argument("--cpu-seconds", type=float, default=10.0, help="min seconds of CPU baseline proving")
     return ap.parse_args()
 
 
 def make_witnesses(circuit, first, count):
-    from qp_wormhole.synthetic import synthetic_inputs
+    from qp_wormhole.synthetic import synthetic_inputs, synthetic_vote_inputs
+    gen = synthetic_vote_inputs if circuit.kind == "voting" else synthetic_inputs
     n, W = circuit.n, circuit.num_wires
     wires = np.empty((count, W, n), np.uint64)
     pis = np.empty((count, circuit.num_public_inputs), np.uint64)
     for i in range(count):
-        w = circuit.commit(synthetic_inputs(first + i))
+        w = circuit.commit(gen(first + i))
         wires[i] = w.wires()
         pis[i] = w.public_inputs()
         w.free()
     return wires, pis
 
 
-def cpu_baseline(circuit, wires, pis, sample):
-    """oracle/prover.c (C + OpenMP restatement of plonky2 prove) on `sample` proofs."""
+def cpu_baseline(circuit, wires, pis, sample, min_seconds):
+    """oracle/prover.c (C + OpenMP restatement of plonky2 prove): at least
+    `sample` proofs of the bench's own witnesses, continuing (cycling through
+    them) until `min_seconds` of CPU proving have been timed."""
     from oracle_lib import U64P, lib as olib
     L = olib()
     L.ora_prove.argtypes = [ctypes.c_char_p, ctypes.c_size_t, U64P, U64P, U64P, ctypes.c_size_t, ctypes.c_char_p,
@@ -67,14 +74,19 @@ def cpu_baseline(circuit, wires, pis, sample):
     cap = np.zeros(64, np.uint64)
     dig = np.zeros(4, np.uint64)
     t = time.perf_counter()
-    for i in range(sample):
+    done = 0
+    while done < sample or time.perf_counter() - t < min_seconds:
+        i = done % wires.shape[0]
         rc = L.ora_prove(cb, len(cb), cs, np.ascontiguousarray(wires[i]), np.ascontiguousarray(pis[i]),
                          pis.shape[1], out, 400000, ctypes.byref(ln), cap, dig)
         assert rc == 0
+        done += 1
     dt = time.perf_counter() - t
+    sample = done
     cores = int(os.environ.get("OMP_NUM_THREADS", os.cpu_count() or 1))
     return {"value": sample / dt, "unit": "proofs/s", "cores": cores, "kind": "port",
-            "sample": f"{sample} Wormhole proofs (deg 13, standard_recursion_config), C+OpenMP restatement "
+            "sample": f"{sample} {circuit.kind} proofs (deg {circuit.degree_bits}, standard_recursion_config), "
+                      f"C+OpenMP restatement "
                       f"oracle/prover.c, {dt:.1f} s"}
 
 
@@ -91,8 +103,9 @@ def main():
         dist.init_process_group("nccl")
     import qp_wormhole
 
-    circuit = qp_wormhole.Circuit.wormhole(zero_knowledge=False)
-    B = args.batch
+    voting = args.circuit == "voting"
+    circuit = qp_wormhole.Circuit.voting() if voting else qp_wormhole.Circuit.wormhole(zero_knowledge=False)
+    B = args.batch or (1024 if voting else 256)
     wires, pis = make_witnesses(circuit, rank * B, B)
     ctx = qp_wormhole.Context(local)
     prover = qp_wormhole.Prover(ctx, circuit, max_batch=B)
@@ -140,7 +153,7 @@ def main():
         achieved = lde["units"] / (lde["ms"] * 1e-3) / 1e9 if lde["ms"] else None
         leaf = ks["leaf_hash_wires"]
         rec = {
-            "metric": "Wormhole proofs/sec (whole node)",
+            "metric": "Voting proofs/sec (whole node)" if voting else "Wormhole proofs/sec (whole node)",
             "value": total / dt,
             "unit": "proofs/s",
             "n_gpus": world,
@@ -151,10 +164,12 @@ def main():
             "scaling": "weak",
             "vs_baseline": None,
             "dtype": "u64 (Goldilocks field)",
-            "data": "synthetic seeded Wormhole witnesses (SURVEY 8d), native circuit, standard_recursion_config",
-            "config": {"workload": f"batch{B}_wormhole_proofs_per_gpu", "circuit": "wormhole deg13 (135 wires)",
+            "data": f"synthetic seeded {circuit.kind} witnesses (SURVEY 8d), native circuit, standard_recursion_config",
+            "config": {"workload": f"batch{B}_{circuit.kind}_proofs_per_gpu",
+                       "circuit": f"{circuit.kind} deg{circuit.degree_bits} (135 wires)",
                        "batch_per_gpu": B, "parallelism": f"proofs sharded x{world}, RCCL gather of leaf proofs"},
-            "roofline": {"kernel": "k_lde (wires LDE, 135 cols x 2^13 -> 2^16)", "bound": "hbm",
+            "roofline": {"kernel": f"k_lde (wires LDE, 135 cols x 2^{circuit.degree_bits} -> "
+                                   f"2^{circuit.degree_bits + 3})", "bound": "hbm",
                          "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": achieved / HBM_PEAK_GBS if achieved else None, "traffic": None,
                          "avg_launch_ms": lde["ms"] / max(lde["launches"], 1)},
@@ -166,7 +181,7 @@ def main():
             "warmup_proof_verified": verified,
         }
         if world == 1 and args.cpu_sample > 0:
-            rec["cpu_baseline"] = cpu_baseline(circuit, wires, pis, args.cpu_sample)
+            rec["cpu_baseline"] = cpu_baseline(circuit, wires, pis, args.cpu_sample, args.cpu_seconds)
         print(json.dumps(rec), flush=True)
     prover.free()
     if dist is not None:

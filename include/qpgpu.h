@@ -138,6 +138,28 @@ int qp_circuit_constants_sigmas(const qp_circuit *c, uint64_t *out);
  * conflict returns QP_ERR_WITNESS with the reference's message in err.     */
 int qp_wormhole_commit(const qp_circuit *c, const qp_wormhole_inputs *in, qp_witness **out, char *err,
                        size_t errcap);
+/* VotePublicInputs + VotePrivateInputs (voting/src/lib.rs:26-52), felt form */
+typedef struct {
+    uint64_t proposal_id[4];
+    uint64_t merkle_root[4];
+    uint64_t nullifier[4];
+    uint8_t vote;                      /* 0 = no, 1 = yes */
+    uint64_t private_key[4];
+    uint32_t num_siblings;             /* merkle_siblings.len() */
+    const uint64_t *siblings;          /* [num_siblings][4] */
+    uint32_t num_path_indices;         /* path_indices.len() */
+    const uint8_t *path_indices;       /* [num_path_indices], 0 = left, 1 = right */
+    uint64_t actual_merkle_depth;
+} qp_voting_inputs;
+
+/* VoteTargets::new + VoteCircuitData::circuit + builder.build()
+ * (voting/src/lib.rs:71-197, :346-357) — host part.                         */
+int qp_voting_circuit_new(int zero_knowledge, qp_circuit **out);
+/* VoteCircuitData::fill_targets (voting/src/lib.rs:199-261) + witness
+ * generation.  Input validation errors return QP_ERR_ARG and witness
+ * conflicts (an invalid Merkle proof or nullifier: plonky2's prove() fails)
+ * QP_ERR_WITNESS, both with the reference's message in err.               */
+int qp_voting_commit(const qp_circuit *c, const qp_voting_inputs *in, qp_witness **out, char *err, size_t errcap);
 /* full wire matrix, column-major [num_wires][n] */
 int qp_witness_wires(const qp_witness *w, uint64_t *out);
 int qp_witness_public_inputs(const qp_witness *w, uint64_t *out, uint32_t cap, uint32_t *n);

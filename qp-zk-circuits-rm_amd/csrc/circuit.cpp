@@ -153,6 +153,39 @@ Target CircuitBuilder::mul_const_add(F c, Target x, Target y) {
   Target ct = constant(c);
   return mul_add(ct, x, y);
 }
+Target CircuitBuilder::add_virtual_bool_target_safe() {
+  Target t = add_virtual_target();
+  connect(mul_sub(t, t, t), zero());
+  return t;
+}
+
+// common/src/gadgets.rs:53-65: a + b - 2ab
+Target xor_gadget(CircuitBuilder &b, Target a, Target c) {
+  Target ab = b.mul(a, c);
+  Target two_ab = b.mul_const(2, ab);
+  Target a_plus_b = b.add(a, c);
+  return b.sub(a_plus_b, two_ab);
+}
+
+// common/src/gadgets.rs:14-41: left < right for a constant left
+Target is_const_less_than(CircuitBuilder &b, uint32_t left, Target right, uint32_t n_log) {
+  auto right_bits = b.split_le(right, n_log);
+  Target lt = b._false();
+  Target eq = b._true();
+  for (uint32_t i = n_log; i-- > 0;) {
+    Target a = b.constant_bool((left >> i) & 1);
+    Target bb = right_bits[i];
+    Target not_a = b._not(a);
+    Target not_a_and_b = b._and(not_a, bb);
+    Target this_lt = b._and(not_a_and_b, eq);
+    lt = b._or(lt, this_lt);
+    Target a_xor_b = xor_gadget(b, a, bb);
+    Target not_xor = b._not(a_xor_b);
+    eq = b._and(eq, not_xor);
+  }
+  return lt;
+}
+
 Target CircuitBuilder::_not(Target b) {
   Target o = one();
   return sub(o, b);

@@ -125,6 +125,8 @@ class CircuitBuilder {
   Target add_virtual_public_input();
   std::vector<Target> add_virtual_hash_public_input();
   void register_public_input(Target t) { public_inputs_.push_back(t); }
+  // virtual target + assert_bool (b*b - b == 0)
+  Target add_virtual_bool_target_safe();
 
   Target constant(F c);
   Target zero() { return constant(0); }
@@ -186,6 +188,10 @@ class CircuitBuilder {
   std::map<std::tuple<F, F, uint32_t, uint32_t, uint32_t>, Target> arith_cache_;
   uint32_t arith_ops_, base_sum_limbs_;
 };
+
+// common/src/gadgets.rs:14-65 (shared by the Wormhole and voting circuits)
+Target xor_gadget(CircuitBuilder &b, Target a, Target c);
+Target is_const_less_than(CircuitBuilder &b, uint32_t left, Target right, uint32_t n_log);
 
 // Per-proof witness: values per partition slot.
 class Witness {

@@ -31,6 +31,26 @@ int qp_wormhole_circuit_new(int zk, qp_circuit **out) {
   }
 }
 
+int qp_voting_circuit_new(int zk, qp_circuit **out) {
+  if (!out) return QP_ERR_ARG;
+  *out = nullptr;
+  try {
+    auto c = std::make_unique<qp_circuit>();
+    c->kind = qp_circuit::VOTING;
+    qc::CircuitBuilder b(zk ? qc::CircuitConfig::standard_recursion_zk_config()
+                            : qc::CircuitConfig::standard_recursion_config());
+    c->voting = qv::build_voting(b);
+    c->gates_used = (uint32_t)b.num_gates();
+    c->cd = b.build();
+    *out = c.release();
+    return QP_OK;
+  } catch (const std::bad_alloc &) {
+    return QP_ERR_OOM;
+  } catch (const std::exception &) {
+    return QP_ERR_STATE;
+  }
+}
+
 void qp_circuit_free(qp_circuit *c) { delete c; }
 
 int qp_circuit_info(const qp_circuit *c, uint32_t *info) {
@@ -96,6 +116,39 @@ int qp_wormhole_commit(const qp_circuit *c, const qp_wormhole_inputs *in, qp_wit
     if (!e.empty()) {
       put_err(err, errcap, e);
       return e.find("set twice") != std::string::npos ? QP_ERR_WITNESS : QP_ERR_ARG;
+    }
+    *out = w.release();
+    return QP_OK;
+  } catch (const std::bad_alloc &) {
+    return QP_ERR_OOM;
+  }
+}
+
+int qp_voting_commit(const qp_circuit *c, const qp_voting_inputs *in, qp_witness **out, char *err, size_t errcap) {
+  if (!c || !in || !out || c->kind != qp_circuit::VOTING) return QP_ERR_ARG;
+  *out = nullptr;
+  if ((in->num_siblings && !in->siblings) || (in->num_path_indices && !in->path_indices)) return QP_ERR_ARG;
+  try {
+    qv::VoteInputs vi;
+    memcpy(vi.proposal_id, in->proposal_id, 32);
+    memcpy(vi.merkle_root, in->merkle_root, 32);
+    memcpy(vi.nullifier, in->nullifier, 32);
+    vi.vote = in->vote != 0;
+    memcpy(vi.private_key, in->private_key, 32);
+    for (uint32_t i = 0; i < in->num_siblings; i++)
+      vi.merkle_siblings.push_back({in->siblings[4 * i], in->siblings[4 * i + 1], in->siblings[4 * i + 2],
+                                    in->siblings[4 * i + 3]});
+    for (uint32_t i = 0; i < in->num_path_indices; i++) vi.path_indices.push_back(in->path_indices[i] != 0);
+    vi.actual_merkle_depth = in->actual_merkle_depth;
+    auto w = std::make_unique<qp_witness>(c);
+    std::string e = qv::fill_targets(c->voting, vi, w->w);
+    if (!e.empty()) {
+      put_err(err, errcap, e);
+      return QP_ERR_ARG;
+    }
+    if (!w->w.generate(e)) {
+      put_err(err, errcap, e);
+      return QP_ERR_WITNESS;
     }
     *out = w.release();
     return QP_OK;

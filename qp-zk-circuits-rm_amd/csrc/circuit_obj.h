@@ -2,12 +2,14 @@
 #pragma once
 #include <stdint.h>
 #include "circuit.h"
+#include "voting.h"
 #include "wormhole.h"
 
 struct qp_circuit {
   enum Kind { WORMHOLE = 1, VOTING = 2 } kind = WORMHOLE;
   qc::CircuitData cd;
   qw::WormholeTargets wormhole;
+  qv::VoteTargets voting;
   uint32_t gates_used = 0;
 };
 

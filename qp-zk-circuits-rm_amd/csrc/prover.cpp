@@ -171,8 +171,8 @@ int setup(qp_prover *P) {
   P->final_len = 1u << (P->log_n - tot);
   P->common = cd.common_bytes();
   if (P->nc != 2 || cd.config.zero_knowledge || (1u << P->rate_bits) != P->qdf || P->log_n > 14 ||
-      P->log_n < 10 || P->nchunks > 16 || P->NC > 8 || P->arity.size() > 8 || P->nq > 64) {
-    c->err = "unsupported circuit shape for the GPU prover (need 2 challenges, non-zk, qdf = blowup, 2^10 <= n <= 2^14)";
+      P->log_n < 6 || P->nchunks > 16 || P->NC > 8 || P->arity.size() > 8 || P->nq > 64) {
+    c->err = "unsupported circuit shape for the GPU prover (need 2 challenges, non-zk, qdf = blowup, 2^6 <= n <= 2^14)";
     return QP_ERR_ARG;
   }
   qpk::GateDesc &g = P->gdesc;

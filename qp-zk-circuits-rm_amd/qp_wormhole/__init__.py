@@ -9,8 +9,8 @@ from ._native import (Context, PolynomialBatch, QpError, header_symbols, ifft, l
                       poseidon_permute)
 
 from .circuits import (Circuit, CircuitInputs, PrivateCircuitInputs, ProcessedStorageProof,  # noqa: F401,E402
-                       PublicCircuitInputs, Witness)
+                       PublicCircuitInputs, VoteCircuitData, VotePrivateInputs, VotePublicInputs, Witness)
 from .prover import Prover, ProofWithPublicInputs, WormholeProver  # noqa: F401,E402
 
 __all__ = ["Circuit", "CircuitInputs", "PrivateCircuitInputs", "ProcessedStorageProof", "PublicCircuitInputs",
-           "Witness", "Prover", "ProofWithPublicInputs", "WormholeProver", "Context", "PolynomialBatch", "QpError", "ifft", "lde", "poseidon_permute", "lib", "header_symbols"]
+           "Witness", "VoteCircuitData", "VotePrivateInputs", "VotePublicInputs", "Prover", "ProofWithPublicInputs", "WormholeProver", "Context", "PolynomialBatch", "QpError", "ifft", "lde", "poseidon_permute", "lib", "header_symbols"]

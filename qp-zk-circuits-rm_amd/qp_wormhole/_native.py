@@ -72,6 +72,8 @@ def lib():
                                                   ctypes.POINTER(ctypes.c_size_t)]),
         "qp_circuit_constants_sigmas": (ctypes.c_int, [VP, U64P]),
         "qp_wormhole_commit": (ctypes.c_int, [VP, VP, PP, ctypes.c_char_p, ctypes.c_size_t]),
+        "qp_voting_circuit_new": (ctypes.c_int, [ctypes.c_int, PP]),
+        "qp_voting_commit": (ctypes.c_int, [VP, VP, PP, ctypes.c_char_p, ctypes.c_size_t]),
         "qp_witness_wires": (ctypes.c_int, [VP, U64P]),
         "qp_witness_public_inputs": (ctypes.c_int, [VP, U64P, ctypes.c_uint32, ctypes.POINTER(ctypes.c_uint32)]),
         "qp_witness_free": (None, [VP]),

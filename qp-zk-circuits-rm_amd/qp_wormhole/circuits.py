@@ -1,5 +1,9 @@
 """Host-side mirror of the reference's circuit / prover input types.
 
+VoteCircuitData mirrors voting/src/lib.rs:26-52, :113-121 (VotePublicInputs +
+VotePrivateInputs); Circuit.voting() builds the native voting circuit
+(VoteTargets::new + VoteCircuitData::circuit, voting/src/lib.rs:71-197).
+
 CircuitInputs mirrors wormhole/circuit/src/inputs.rs:21-52 (public +
 private inputs); WormholeCircuit builds the native circuit
 (wormhole/circuit/src/circuit.rs:63-109) through the C ABI; Witness is the
@@ -80,6 +84,60 @@ class CircuitInputs:
         return s
 
 
+U64_4 = ctypes.c_uint64 * 4
+
+
+class _VoteInputs(ctypes.Structure):
+    _fields_ = [("proposal_id", U64_4), ("merkle_root", U64_4), ("nullifier", U64_4), ("vote", ctypes.c_uint8),
+                ("private_key", U64_4), ("num_siblings", ctypes.c_uint32),
+                ("siblings", ctypes.POINTER(ctypes.c_uint64)), ("num_path_indices", ctypes.c_uint32),
+                ("path_indices", ctypes.POINTER(ctypes.c_uint8)), ("actual_merkle_depth", ctypes.c_uint64)]
+
+
+@dataclass
+class VotePublicInputs:
+    """voting/src/lib.rs:26-36 (digests are 4 field elements)."""
+    proposal_id: List[int]
+    merkle_root: List[int]
+    vote: bool
+    nullifier: List[int]
+
+
+@dataclass
+class VotePrivateInputs:
+    """voting/src/lib.rs:42-52."""
+    private_key: List[int]
+    merkle_siblings: List[List[int]]
+    path_indices: List[bool]
+    actual_merkle_depth: int
+
+
+@dataclass
+class VoteCircuitData:
+    """voting/src/lib.rs:113-121: the witness data fill_targets consumes."""
+    public_inputs: VotePublicInputs
+    private_inputs: VotePrivateInputs
+
+    def to_c(self):
+        s = _VoteInputs()
+        pub, prv = self.public_inputs, self.private_inputs
+        s.proposal_id[:] = list(pub.proposal_id)
+        s.merkle_root[:] = list(pub.merkle_root)
+        s.nullifier[:] = list(pub.nullifier)
+        s.vote = 1 if pub.vote else 0
+        s.private_key[:] = list(prv.private_key)
+        sibs = [int(x) for d in prv.merkle_siblings for x in d]
+        s.num_siblings = len(prv.merkle_siblings)
+        keep_s = (ctypes.c_uint64 * max(len(sibs), 1))(*sibs)
+        s.siblings = ctypes.cast(keep_s, ctypes.POINTER(ctypes.c_uint64))
+        s.num_path_indices = len(prv.path_indices)
+        keep_p = (ctypes.c_uint8 * max(len(prv.path_indices), 1))(*[1 if b else 0 for b in prv.path_indices])
+        s.path_indices = ctypes.cast(keep_p, ctypes.POINTER(ctypes.c_uint8))
+        s.actual_merkle_depth = prv.actual_merkle_depth
+        s._keep = (keep_s, keep_p)
+        return s
+
+
 class Witness:
     def __init__(self, circuit, handle):
         self.circuit, self.h = circuit, handle
@@ -130,6 +188,15 @@ class Circuit:
             raise QpError(rc, "qp_wormhole_circuit_new")
         return cls(h, "wormhole")
 
+    @classmethod
+    def voting(cls, zero_knowledge=False):
+        """VoteTargets::new + VoteCircuitData::circuit + builder.build() (voting/src/lib.rs:346-357)."""
+        h = ctypes.c_void_p()
+        rc = lib().qp_voting_circuit_new(int(zero_knowledge), ctypes.byref(h))
+        if rc:
+            raise QpError(rc, "qp_voting_circuit_new")
+        return cls(h, "voting")
+
     def common_data(self):
         ln = ctypes.c_size_t()
         lib().qp_circuit_common_data(self.h, None, 0, ctypes.byref(ln))
@@ -146,11 +213,14 @@ class Circuit:
             raise QpError(rc, "qp_circuit_constants_sigmas")
         return out
 
-    def commit(self, inputs: CircuitInputs) -> Witness:
+    def commit(self, inputs) -> Witness:
+        """WormholeProver::commit (CircuitInputs) or VoteCircuitData::fill_targets
+        (VoteCircuitData) followed by witness generation."""
         s = inputs.to_c()
         h = ctypes.c_void_p()
         err = ctypes.create_string_buffer(512)
-        rc = lib().qp_wormhole_commit(self.h, ctypes.byref(s), ctypes.byref(h), err, 512)
+        fn = lib().qp_voting_commit if self.kind == "voting" else lib().qp_wormhole_commit
+        rc = fn(self.h, ctypes.byref(s), ctypes.byref(h), err, 512)
         if rc:
             raise QpError(rc, err.value.decode())
         return Witness(self, h)

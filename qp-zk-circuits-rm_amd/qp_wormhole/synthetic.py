@@ -122,3 +122,51 @@ def synthetic_inputs(k: int, depth: int = -1) -> CircuitInputs:
         PublicCircuitInputs(funding_amount, null, root, exit_account),
         PrivateCircuitInputs(secret, ProcessedStorageProof(nodes, indices), transfer_count, funding_account,
                              unspendable))
+
+
+# ---------------------------------------------------------------- voting circuit
+
+def vote_nullifier(private_key, proposal_id):
+    """voting/src/lib.rs:277-283: H(H(private_key) || proposal_id)."""
+    return hash_no_pad(list(hash_no_pad(list(private_key))) + list(proposal_id))
+
+
+def vote_test_inputs():
+    """create_test_inputs (voting/src/lib.rs:285-337): 4-leaf tree of H([k;32] as
+    felts), voter = key 1 at depth 2, proposal id = [42;32], vote = yes."""
+    from .circuits import VoteCircuitData, VotePrivateInputs, VotePublicInputs
+    keys = [bytes_to_digest(bytes([k] * 32)) for k in (1, 2, 3, 4)]
+    leaves = [hash_no_pad(k) for k in keys]
+    level1 = [hash_no_pad(leaves[0] + leaves[1]), hash_no_pad(leaves[2] + leaves[3])]
+    root = hash_no_pad(level1[0] + level1[1])
+    proposal = bytes_to_digest(bytes([42] * 32))
+    return VoteCircuitData(
+        VotePublicInputs(proposal_id=proposal, merkle_root=root, vote=True,
+                         nullifier=vote_nullifier(keys[0], proposal)),
+        VotePrivateInputs(private_key=keys[0], merkle_siblings=[leaves[1], level1[1]], path_indices=[False, False],
+                          actual_merkle_depth=2))
+
+
+def synthetic_vote_inputs(k: int, depth: int = -1):
+    """Seeded voter k: random key, a random Merkle path of `depth` levels
+    (default: seeded in [0, 31]; 32 does not fit the circuit's 5-bit depth
+    split, see tests/test_voting.py) with random siblings and sides, the root it
+    implies, a random proposal id and vote, and the matching nullifier."""
+    from .circuits import VoteCircuitData, VotePrivateInputs, VotePublicInputs
+    r = _Rng(0x10000 + k)
+    key = [r.u64() % P for _ in range(4)]
+    if depth < 0:
+        depth = r.u64() % 32
+    cur = hash_no_pad(key)
+    sibs, path = [], []
+    for _ in range(depth):
+        s = [r.u64() % P for _ in range(4)]
+        right = bool(r.u64() & 1)
+        cur = hash_no_pad(s + cur if right else cur + s)
+        sibs.append(s)
+        path.append(right)
+    proposal = [r.u64() % P for _ in range(4)]
+    return VoteCircuitData(
+        VotePublicInputs(proposal_id=proposal, merkle_root=cur, vote=bool(r.u64() & 1),
+                         nullifier=vote_nullifier(key, proposal)),
+        VotePrivateInputs(private_key=key, merkle_siblings=sibs, path_indices=path, actual_merkle_depth=depth))
