@@ -20,6 +20,7 @@ import ctypes
 import json
 import os
 import sys
+import threading
 import time
 
 import numpy as np
@@ -38,6 +39,9 @@ def parse():
     ap.add_argument("--warmup", type=int, default=1)
     ap.add_argument("--batch", type=int, default=0,
                     help="proofs per GPU per step (default: 256 Wormhole, 1024 voting)")
+    ap.add_argument("--provers", type=int, default=2,
+                    help="concurrent provers per GPU (own HIP stream + host thread each, B/provers proofs each): "
+                         "one prover's host transcript phases overlap the other's kernels")
     ap.add_argument("--circuit", choices=["wormhole", "voting"], default="wormhole",
                     help="wormhole = BASELINE configs[2] (the headline); voting = configs[4]")
     ap.add_argument("--cpu-sample", type=int, default=2, help="min proofs in the CPU baseline sample (0 = skip)")
@@ -107,30 +111,53 @@ def main():
     circuit = qp_wormhole.Circuit.voting() if voting else qp_wormhole.Circuit.wormhole(zero_knowledge=False)
     B = args.batch or (1024 if voting else 256)
     wires, pis = make_witnesses(circuit, rank * B, B)
-    ctx = qp_wormhole.Context(local)
-    prover = qp_wormhole.Prover(ctx, circuit, max_batch=B)
+    NP = max(1, min(args.provers, B))
+    per = [B // NP + (1 if i < B % NP else 0) for i in range(NP)]
+    first = [sum(per[:i]) for i in range(NP)]
+    provers = [qp_wormhole.Prover(qp_wormhole.Context(local), circuit, max_batch=per[i]) for i in range(NP)]
+    prover = provers[0]
     d_wires = torch.from_numpy(wires.view(np.int64)).to(f"cuda:{local}")
+    wstride = wires[0].nbytes
     torch.cuda.synchronize()
 
     from qp_wormhole.distributed import gather_proofs
 
+    def prove_all():
+        out = [None] * NP
+
+        def run(i):
+            out[i] = provers[i].prove_wires_dev(d_wires.data_ptr() + first[i] * wstride,
+                                                pis[first[i]:first[i] + per[i]], per[i])
+        if NP == 1:
+            run(0)
+        else:
+            th = [threading.Thread(target=run, args=(i,)) for i in range(NP)]
+            for t in th:
+                t.start()
+            for t in th:
+                t.join()
+        if any(o is None for o in out):
+            raise RuntimeError("a prover thread failed")
+        return [p for o in out for p in o]
+
     def step():
-        proofs = prover.prove_wires_dev(d_wires.data_ptr(), pis, B)
+        proofs = prove_all()
         if dist is not None:  # leaf proofs -> aggregator rank over RCCL
             gather_proofs(proofs, prover.proof_size, dist, device=f"cuda:{local}")
         return proofs
 
     for _ in range(args.warmup):
         proofs = step()
-    # proofs of the warmup verify (rank 0 checks one with the oracle verifier)
+    # proofs of the warmup verify (rank 0 checks the first and last with the oracle verifier)
     verified = None
     if rank == 0 and args.warmup:
         from oracle_lib import lib as olib
         vd = prover.verifier_data()
-        verified = olib().ora_verify(vd, len(vd), proofs[0], len(proofs[0])) == 0
-    prover.set_timing(True)
-    prover.kernel_stats(reset=True)
-    prover.stage_times(reset=True)
+        verified = all(olib().ora_verify(vd, len(vd), p, len(p)) == 0 for p in (proofs[0], proofs[-1]))
+    for p in provers:
+        p.set_timing(True)
+        p.kernel_stats(reset=True)
+        p.stage_times(reset=True)
     if dist is not None:
         dist.barrier()
     torch.cuda.synchronize()
@@ -145,8 +172,19 @@ def main():
         tt = torch.tensor([dt], dtype=torch.float64, device=f"cuda:{local}")
         dist.all_reduce(tt, op=dist.ReduceOp.MAX)
         dt = float(tt.item())
-    ks = prover.kernel_stats()
+    # kernel statistics summed over the provers (HIP events on each prover's stream)
+    ks = provers[0].kernel_stats()
+    for p in provers[1:]:
+        for k, v in p.kernel_stats().items():
+            for f in ("ms", "units", "launches"):
+                ks[k][f] += v[f]
     stages = prover.stage_times()
+    # the same kernels alone on the GPU (one prover, one step, after the timed region)
+    iso = None
+    if rank == 0 and NP > 1:
+        prover.kernel_stats(reset=True)
+        prover.prove_wires_dev(d_wires.data_ptr(), pis[:per[0]], per[0])
+        iso = prover.kernel_stats()
     if rank == 0:
         total = world * B * args.steps
         lde = ks["lde_wires"]
@@ -167,12 +205,15 @@ def main():
             "data": f"synthetic seeded {circuit.kind} witnesses (SURVEY 8d), native circuit, standard_recursion_config",
             "config": {"workload": f"batch{B}_{circuit.kind}_proofs_per_gpu",
                        "circuit": f"{circuit.kind} deg{circuit.degree_bits} (135 wires)",
-                       "batch_per_gpu": B, "parallelism": f"proofs sharded x{world}, RCCL gather of leaf proofs"},
+                       "batch_per_gpu": B, "provers_per_gpu": NP,
+                       "parallelism": f"proofs sharded x{world}, RCCL gather of leaf proofs"},
             "roofline": {"kernel": f"k_lde (wires LDE, 135 cols x 2^{circuit.degree_bits} -> "
                                    f"2^{circuit.degree_bits + 3})", "bound": "hbm",
                          "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": achieved / HBM_PEAK_GBS if achieved else None, "traffic": None,
-                         "avg_launch_ms": lde["ms"] / max(lde["launches"], 1)},
+                         "avg_launch_ms": lde["ms"] / max(lde["launches"], 1),
+                         "note": "per-launch HIP-event time on the prover streams over the timed region, where "
+                                 "the other prover's kernels share the GPU; isolated_*: one prover alone"},
             "valu_kernels": {"leaf_hash_wires_perms_per_s": leaf["units"] / (leaf["ms"] * 1e-3) if leaf["ms"] else None,
                              "avg_launch_ms": leaf["ms"] / max(leaf["launches"], 1),
                              "quotient_avg_launch_ms": ks["quotient"]["ms"] / max(ks["quotient"]["launches"], 1)},
@@ -180,10 +221,17 @@ def main():
             "proof_bytes": len(proofs[0]),
             "warmup_proof_verified": verified,
         }
+        if iso is not None and iso["lde_wires"]["ms"]:
+            il = iso["lde_wires"]
+            ia = il["units"] / (il["ms"] * 1e-3) / 1e9
+            rec["roofline"].update({"isolated_achieved": ia, "isolated_frac": ia / HBM_PEAK_GBS,
+                                    "isolated_avg_launch_ms": il["ms"] / max(il["launches"], 1)})
+        rec["stage_ms_per_step"]["note"] = f"prover 0 ({per[0]} proofs), host + device"
         if world == 1 and args.cpu_sample > 0:
             rec["cpu_baseline"] = cpu_baseline(circuit, wires, pis, args.cpu_sample, args.cpu_seconds)
         print(json.dumps(rec), flush=True)
-    prover.free()
+    for p in provers:
+        p.free()
     if dist is not None:
         dist.destroy_process_group()
 

@@ -12,6 +12,9 @@
 namespace qpk {
 
 constexpr unsigned TW_LOG = 16;  // twiddle tables cover sizes up to 2^16
+// LDS slots of a size-n NTT workgroup: one pad slot per 32 elements (ntt16.h lp())
+__host__ __device__ constexpr uint32_t ntt_lds_words(uint32_t n) { return n + (n >> 5); }
+#define QP_HAVE_LDS_WORDS 1
 
 constexpr unsigned LDE_MAX_RATE = 4;  // coset-fused LDE kernel: up to 16 cosets
 

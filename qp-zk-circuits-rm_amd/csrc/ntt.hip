@@ -83,10 +83,10 @@ __global__ void __launch_bounds__(512) QP_NTT_OCC k_intt(const uint64_t *__restr
   const uint32_t n = 1u << log_n;
   const uint64_t *src = in + blockIdx.y * in_bstride + (uint64_t)blockIdx.x * in_stride;
   uint64_t *dst = out + blockIdx.y * out_bstride + (uint64_t)blockIdx.x * out_stride;
-  for (uint32_t i = threadIdx.x; i < n; i += blockDim.x) lds[i] = src[i];
+  for (uint32_t i = threadIdx.x; i < n; i += blockDim.x) lds[nt::lp(i)] = src[i];
   __syncthreads();
   nt::ntt_lds<true>(lds, log_n, tw_inv);
-  for (uint32_t m = threadIdx.x; m < n; m += blockDim.x) dst[m] = gl::mul(lds[gl::rev_bits(m, log_n)], n_inv);
+  for (uint32_t m = threadIdx.x; m < n; m += blockDim.x) dst[m] = gl::mul(lds[nt::lp(gl::rev_bits(m, log_n))], n_inv);
 }
 
 __global__ void __launch_bounds__(512) QP_NTT_OCC k_lde(const uint64_t *__restrict__ coeffs, uint64_t c_stride,
@@ -106,12 +106,12 @@ __global__ void __launch_bounds__(512) QP_NTT_OCC k_lde(const uint64_t *__restri
   uint64_t f = gl::pow(base, threadIdx.x);
   const uint64_t step = gl::pow(base, blockDim.x);
   for (uint32_t k = threadIdx.x; k < n; k += blockDim.x) {
-    lds[k] = gl::mul(src[k], f);
+    lds[nt::lp(k)] = gl::mul(src[k], f);
     f = gl::mul(f, step);
   }
   __syncthreads();
   nt::ntt_lds<false>(lds, log_n, tw);
-  for (uint32_t p = threadIdx.x; p < n; p += blockDim.x) dst[p] = nt::canon(lds[p]);
+  for (uint32_t p = threadIdx.x; p < n; p += blockDim.x) dst[p] = nt::canon(lds[nt::lp(p)]);
 }
 
 // Coset-fused LDE: one workgroup per column produces all B = 2^r cosets, so
@@ -159,13 +159,13 @@ __global__ void __launch_bounds__(1 << LOG_T) QP_NTT_OCC k_lde_cosets(const uint
     for (int m = 0; m < 16; m++) {
       const uint32_t e = t * (s + (nt::brev4(m) << rate_bits));
       if (e) r[m] = nt::mul(r[m], nt::tw_pow(tw, e, logN));
-      lds[t + T * m] = r[m];
+      lds[nt::lp(t) + nt::lp(T * m)] = r[m];
     }
     __syncthreads();
     nt::ntt_lds_from<false>(lds, LOG_N, LOG_T, tw);
     uint64_t *dst = dst0 + ((uint64_t)gl::rev_bits(s, rate_bits) << LOG_N);
 #pragma unroll
-    for (int m = 0; m < 16; m++) dst[t + T * m] = nt::canon(lds[t + T * m]);
+    for (int m = 0; m < 16; m++) dst[t + T * m] = nt::canon(lds[nt::lp(t) + nt::lp(T * m)]);
     __syncthreads();
   }
 }
@@ -180,7 +180,7 @@ void intt(const Twiddles &t, const uint64_t *in, uint64_t in_stride, uint64_t *o
   if (!ncols || !nbat) return;
   uint64_t n_inv = gl::inv((uint64_t)1 << log_n);
   dim3 grid(ncols, nbat);
-  k_intt<<<grid, ntt_threads(log_n), (8u << log_n), s>>>(in, in_stride, out, out_stride, log_n, n_inv, t.inv,
+  k_intt<<<grid, ntt_threads(log_n), 8u * qpk::ntt_lds_words(1u << log_n), s>>>(in, in_stride, out, out_stride, log_n, n_inv, t.inv,
                                                          in_bstride, out_bstride);
 }
 
@@ -193,7 +193,7 @@ void lde(const Twiddles &t, const uint64_t *coeffs, uint64_t c_stride, uint64_t 
     const uint32_t T = 1u << (log_n - 4);
     const uint64_t shift_T = gl::pow(shift, T);
     dim3 g(ncols, nbat);
-    const size_t lds_bytes = (size_t)8 << log_n;
+    const size_t lds_bytes = (size_t)8 * qpk::ntt_lds_words(1u << log_n);
 #define QP_LDE_COSETS(LT)                                                                                      \
   k_lde_cosets<LT><<<g, 1u << LT, lds_bytes, s>>>(coeffs, c_stride, c_bstride, out, o_stride, o_bstride, rate_bits, \
                                                   shift, shift_T, t.fwd, t.ptw)
@@ -207,7 +207,7 @@ void lde(const Twiddles &t, const uint64_t *coeffs, uint64_t c_stride, uint64_t 
     return;
   }
   dim3 grid(1u << rate_bits, ncols, nbat);
-  k_lde<<<grid, ntt_threads(log_n), (8u << log_n), s>>>(coeffs, c_stride, out, o_stride, log_n, rate_bits, shift,
+  k_lde<<<grid, ntt_threads(log_n), 8u * qpk::ntt_lds_words(1u << log_n), s>>>(coeffs, c_stride, out, o_stride, log_n, rate_bits, shift,
                                                         t.fwd, c_bstride, o_bstride);
 }
 

@@ -12,6 +12,14 @@
 // levels instead of 2.  Arithmetic stays non-canonical in [0, 2^64)
 // (plonky2's own representation); callers canonicalise on store.
 // Output order is the standard in-place DIF order: a[q] = X[bitrev(q)].
+//
+// LDS layout: element i lives at slot lp(i) = i + i/32 (one pad slot per 32
+// elements, lds_words(n) slots).  Without it the stride-2 accesses of the
+// S = 32 radix-16 pass put all 64 lanes of a wave on two 8-byte bank pairs
+// (a 32-way conflict); padded, lane sp of that pass lands on bank pair
+// (sp + ...) mod 32 and every pass is conflict-free.  For the addresses the
+// passes generate, lp(b0 + m*q) = lp(b0) + lp(m*q) (q | 32 or 32 | q), so the
+// per-element offsets stay wave-uniform.
 #pragma once
 #include "field.h"
 #include "kernels.h"
@@ -123,6 +131,11 @@ __device__ __forceinline__ uint64_t tw_pow(const uint64_t *__restrict__ tw, uint
   return E < HALF ? tw[E] : gl::P - tw[E - HALF];  // tw entries are canonical and nonzero
 }
 
+#ifndef QP_LDS_PAD
+#define QP_LDS_PAD 1
+#endif
+__host__ __device__ __forceinline__ constexpr uint32_t lp(uint32_t i) { return QP_LDS_PAD ? i + (i >> 5) : i; }
+
 __device__ __forceinline__ uint32_t brev4(uint32_t m) { return __builtin_bitreverse32(m) >> 28; }
 
 // radix-2^LOGS DIF on each group of S = 2^LOGS contiguous LDS elements
@@ -151,10 +164,10 @@ __device__ __forceinline__ void stage_small(uint64_t r[S]) {
 }
 
 template <bool INV, int LOGS>
-__device__ void tail(uint64_t *a, uint32_t n) {
+__device__ __forceinline__ void tail(uint64_t *a, uint32_t n) {
   constexpr int S = 1 << LOGS;
   for (uint32_t g = threadIdx.x; g < (n >> LOGS); g += blockDim.x) {
-    uint64_t *base = a + (g << LOGS);
+    uint64_t *base = a + lp(g << LOGS);
     uint64_t r[S];
 #pragma unroll
     for (int m = 0; m < S; m++) r[m] = base[m];
@@ -167,12 +180,12 @@ __device__ void tail(uint64_t *a, uint32_t n) {
   __syncthreads();
 }
 
-// In-place DIF over LDS a[0..2^log_n), all threads of the block participate,
+// In-place DIF over LDS a[lp(0..2^log_n)), all threads of the block participate,
 // starting at sub-problem size 2^log_S (log_S = log_n: the whole transform;
 // smaller: the levels above were already done, e.g. from registers).
 // tw = forward or inverse twiddle table matching INV.  Ends with a barrier.
 template <bool INV>
-__device__ void ntt_lds_from(uint64_t *a, uint32_t log_n, uint32_t log_S, const uint64_t *__restrict__ tw) {
+__device__ __forceinline__ void ntt_lds_from(uint64_t *a, uint32_t log_n, uint32_t log_S, const uint64_t *__restrict__ tw) {
   const uint32_t n = 1u << log_n;
   const uint32_t T = blockDim.x;
   // radix-16 passes
@@ -180,17 +193,17 @@ __device__ void ntt_lds_from(uint64_t *a, uint32_t log_n, uint32_t log_S, const 
     const uint32_t S = 1u << log_S, q = S >> 4, log_q = log_S - 4;
     for (uint32_t g = threadIdx.x; g < (n >> 4); g += T) {
       const uint32_t sp = g >> log_q, t = g & (q - 1);
-      uint64_t *base = a + (sp << log_S) + t;
+      uint64_t *base = a + lp((sp << log_S) + t);
       uint64_t r[16];
 #pragma unroll
-      for (int m = 0; m < 16; m++) r[m] = base[m * q];
+      for (int m = 0; m < 16; m++) r[m] = base[lp(m * q)];
       dft16<INV>(r);
       if (t) {
 #pragma unroll
         for (int m = 1; m < 16; m++) r[m] = mul(r[m], tw_pow(tw, t * brev4(m), log_S));
       }
 #pragma unroll
-      for (int m = 0; m < 16; m++) base[m * q] = r[m];
+      for (int m = 0; m < 16; m++) base[lp(m * q)] = r[m];
     }
     __syncthreads();
     log_S -= 4;
@@ -202,7 +215,7 @@ __device__ void ntt_lds_from(uint64_t *a, uint32_t log_n, uint32_t log_S, const 
 }
 
 template <bool INV>
-__device__ void ntt_lds(uint64_t *a, uint32_t log_n, const uint64_t *__restrict__ tw) {
+__device__ __forceinline__ void ntt_lds(uint64_t *a, uint32_t log_n, const uint64_t *__restrict__ tw) {
   ntt_lds_from<INV>(a, log_n, log_n, tw);
 }
 

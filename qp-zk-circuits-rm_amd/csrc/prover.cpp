@@ -90,7 +90,7 @@ struct qp_prover {
   Tree cs;
   DevBuf sigmas, kis;
   Tree wires, zs, quot;
-  DevBuf chal, apow, prods, qvals, cbuf, openings, comp, fin, pow_state, pow_found, pow_pos, qidx, qout;
+  DevBuf chal, apow, prods, qvals, cbuf, openings, comp, fin, pow_state, pow_found, pow_pos, pow_active, qidx, qout;
   std::vector<DevBuf> fvals, fdig, fcoef;
   size_t qout_words = 0;
   std::unique_ptr<qh::ThreadPool> pool;
@@ -253,6 +253,7 @@ int setup(qp_prover *P) {
   TRY(P->pow_state.alloc((size_t)B * 12));
   TRY(P->pow_found.alloc(B));
   TRY(P->pow_pos.alloc((B + 1) / 2));
+  TRY(P->pow_active.alloc((B + 1) / 2));
   TRY(P->qidx.alloc(((size_t)B * P->nq + 1) / 2));
   {
     size_t w = 0;
@@ -455,7 +456,7 @@ int prove_batch(qp_prover *P, const uint64_t *const *wires_host, const uint64_t 
     qpk::k_quotient<2><<<dim3(cdiv(N, 256), nb), 256, 0, s>>>(a);
     kt_end(P, 3, (double)nb * N);
     const uint64_t n_inv = gl::inv(n);
-    qpk::k_qintt_blocks<<<dim3(B, nc, nb), 512, 8u << P->log_n, s>>>(P->qvals.p, P->cbuf.p, P->log_n, P->rate_bits,
+    qpk::k_qintt_blocks<<<dim3(B, nc, nb), 512, 8u * qpk::ntt_lds_words(1u << P->log_n), s>>>(P->qvals.p, P->cbuf.p, P->log_n, P->rate_bits,
                                                                      (uint64_t)nc * N, (uint64_t)nc * N, c->tw.fwd,
                                                                      c->tw.inv, n_inv, gl::inv(gl::GEN));
     const uint64_t winv_r = gl::inv(gl::root_of_unity(P->rate_bits));
@@ -487,16 +488,17 @@ int prove_batch(qp_prover *P, const uint64_t *const *wires_host, const uint64_t 
   // ---- 4. openings (a10)
   {
     const uint32_t ncs = P->NC + P->R, nzs = nc * P->nchunks, nq = nc * P->qdf;
-    qpk::k_openings<<<dim3(ncs, nb), 256, 0, s>>>(P->cs.coeffs.p, 0, ncs, P->log_n, P->chal.p, qpk::CH_ZETA,
-                                                  P->openings.p, 0);
-    qpk::k_openings<<<dim3(P->W, nb), 256, 0, s>>>(P->wires.coeffs.p, P->wires.cbs(), P->W, P->log_n, P->chal.p,
-                                                   qpk::CH_ZETA, P->openings.p, ncs);
-    qpk::k_openings<<<dim3(nzs, nb), 256, 0, s>>>(P->zs.coeffs.p, P->zs.cbs(), nzs, P->log_n, P->chal.p, qpk::CH_ZETA,
-                                                  P->openings.p, ncs + P->W);
-    qpk::k_openings<<<dim3(nq, nb), 256, 0, s>>>(P->quot.coeffs.p, P->quot.cbs(), nq, P->log_n, P->chal.p,
-                                                 qpk::CH_ZETA, P->openings.p, ncs + P->W + nzs);
-    qpk::k_openings<<<dim3(nc, nb), 256, 0, s>>>(P->zs.coeffs.p, P->zs.cbs(), nc, P->log_n, P->chal.p,
-                                                 qpk::CH_ZETA_NEXT, P->openings.p, ncs + P->W + nzs + nq);
+    const unsigned ot = (unsigned)std::min<uint64_t>(256, std::max<uint64_t>(64, n / 4));
+    auto og = [&](uint32_t np) { return dim3((np + qpk::OPEN_PB - 1) / qpk::OPEN_PB, nb); };
+    qpk::k_openings<<<og(ncs), ot, 0, s>>>(P->cs.coeffs.p, 0, ncs, P->log_n, P->chal.p, qpk::CH_ZETA, P->openings.p, 0);
+    qpk::k_openings<<<og(P->W), ot, 0, s>>>(P->wires.coeffs.p, P->wires.cbs(), P->W, P->log_n, P->chal.p,
+                                            qpk::CH_ZETA, P->openings.p, ncs);
+    qpk::k_openings<<<og(nzs), ot, 0, s>>>(P->zs.coeffs.p, P->zs.cbs(), nzs, P->log_n, P->chal.p, qpk::CH_ZETA,
+                                           P->openings.p, ncs + P->W);
+    qpk::k_openings<<<og(nq), ot, 0, s>>>(P->quot.coeffs.p, P->quot.cbs(), nq, P->log_n, P->chal.p, qpk::CH_ZETA,
+                                          P->openings.p, ncs + P->W + nzs);
+    qpk::k_openings<<<og(nc), ot, 0, s>>>(P->zs.coeffs.p, P->zs.cbs(), nc, P->log_n, P->chal.p, qpk::CH_ZETA_NEXT,
+                                          P->openings.p, ncs + P->W + nzs + nq);
     TRY(hipGetLastError());
     TRY(hipMemcpyAsync(P->h_open.data(), P->openings.p, (size_t)nb * qpk::OPEN_STRIDE * 8, hipMemcpyDeviceToHost, s));
     TRY(hipStreamSynchronize(s));
@@ -595,16 +597,31 @@ int prove_batch(qp_prover *P, const uint64_t *const *wires_host, const uint64_t 
   TRY(hipMemcpyAsync(P->pow_pos.p, P->h_pos.data(), (size_t)nb * 4, hipMemcpyHostToDevice, s));
   TRY(hipMemsetAsync(P->pow_found.p, 0xFF, (size_t)nb * 8, s));
   {
-    const uint64_t window = 1ull << 16;
-    for (uint64_t base = 0;; base += window) {
-      qpk::k_pow<<<dim3((uint32_t)(window / 256), nb), 256, 0, s>>>(P->pow_state.p, (const uint32_t *)P->pow_pos.p,
-                                                                    P->pow_found.p, base, P->pow_bits);
+    // Minimal witness per proof: every proof still searching scans the same
+    // candidate window [base, base + W) per launch; only those proofs are
+    // launched (compacted list), so a proof stops costing work as soon as its
+    // window holds a hit.  W = 2^14 keeps the overshoot past the minimal
+    // witness ~W/2 (vs an expected 2^pow_bits search); when few proofs remain
+    // W grows so a launch still covers >= 2^21 candidates (idle CUs otherwise).
+    std::vector<uint32_t> active(nb);
+    for (uint32_t b = 0; b < nb; b++) active[b] = b;
+    uint64_t base = 0;
+    while (!active.empty()) {
+      const uint32_t na = (uint32_t)active.size();
+      uint64_t window = 1ull << 14;
+      while ((uint64_t)na * window < (1ull << 21)) window <<= 1;
+      TRY(hipMemcpyAsync(P->pow_active.p, active.data(), (size_t)na * 4, hipMemcpyHostToDevice, s));
+      qpk::k_pow<<<dim3((uint32_t)(window / 256), na), 256, 0, s>>>(
+          P->pow_state.p, (const uint32_t *)P->pow_pos.p, (const uint32_t *)P->pow_active.p, P->pow_found.p, base,
+          P->pow_bits);
       TRY(hipGetLastError());
       TRY(hipMemcpyAsync(P->h_found.data(), P->pow_found.p, (size_t)nb * 8, hipMemcpyDeviceToHost, s));
       TRY(hipStreamSynchronize(s));
-      bool all = true;
-      for (uint32_t b = 0; b < nb; b++) all &= P->h_found[b] != ~0ull;
-      if (all) break;
+      std::vector<uint32_t> still;
+      for (uint32_t b : active)
+        if (P->h_found[b] == ~0ull) still.push_back(b);
+      active.swap(still);
+      base += window;
       if (base > (1ull << 40)) {
         c->err = "proof of work not found";
         return QP_ERR_STATE;

@@ -54,6 +54,7 @@ __global__ void k_qintt_blocks(const uint64_t *vals, uint64_t *out, uint32_t log
                                uint64_t n_inv, uint64_t ginv);
 __global__ void k_qintt_radix(const uint64_t *cbuf, uint64_t *coeffs, uint32_t log_n, uint32_t rate_bits,
                               uint64_t c_bstride, uint64_t o_bstride, uint64_t winv_r, uint64_t r_inv, uint64_t gninv);
+constexpr int OPEN_PB = 8;  // polys per k_openings block
 __global__ void k_openings(const uint64_t *coeffs, uint64_t c_bstride, uint32_t npolys, uint32_t log_n,
                            const uint64_t *pts, uint32_t pt_off, uint64_t *out, uint32_t out_off);
 __global__ void k_fri_compose(FriComposeArgs a);
@@ -63,7 +64,8 @@ __global__ void k_fri_leaf(const uint64_t *vals, uint64_t *dig, uint32_t log_len
                            uint64_t d_bstride);
 __global__ void k_fold(const uint64_t *cin, uint64_t *cout, uint32_t log_len, uint32_t ab, uint32_t layer,
                        const uint64_t *chal, uint64_t i_bstride, uint64_t o_bstride);
-__global__ void k_pow(const uint64_t *states, const uint32_t *pos, uint64_t *found, uint64_t base, uint32_t bits);
+__global__ void k_pow(const uint64_t *states, const uint32_t *pos, const uint32_t *active, uint64_t *found, uint64_t base,
+                      uint32_t bits);
 __global__ void k_gather_rows_b(const uint64_t *cols, uint64_t stride, uint64_t bstride, uint32_t ncols,
                                 const uint32_t *idx, uint32_t nq, uint32_t shift, uint64_t *out, uint64_t o_bstride);
 __global__ void k_gather_paths_b(const uint64_t *dig, uint64_t d_bstride, uint32_t log_leaves, uint32_t cap_h,

@@ -210,7 +210,10 @@ __device__ __forceinline__ void poseidon_gate(const uint64_t *__restrict__ wl, u
 //         waves/SIMD with a small spill).  PH 0/1 are kept for register-budget
 //         experiments.
 template <int PH>
-__global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) k_quotient(QuotientArgs a) {
+#ifndef QP_QUOTIENT_WAVES
+#define QP_QUOTIENT_WAVES 4
+#endif
+__global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(QP_QUOTIENT_WAVES))) k_quotient(QuotientArgs a) {
   const uint32_t logN = a.log_n + a.rate_bits;
   const uint64_t N = 1ull << logN, n = 1ull << a.log_n;
   const uint32_t t = blockIdx.x * blockDim.x + threadIdx.x;
@@ -339,7 +342,7 @@ __global__ void __launch_bounds__(512) k_qintt_blocks(const uint64_t *__restrict
   const uint32_t s = gl::rev_bits(sp, rate_bits);
   const uint64_t N = (uint64_t)n << rate_bits;
   const uint64_t *src = vals + b * v_bstride + c * N + ((uint64_t)sp << log_n);
-  for (uint32_t p = threadIdx.x; p < n; p += blockDim.x) lds[gl::rev_bits(p, log_n)] = src[p];
+  for (uint32_t p = threadIdx.x; p < n; p += blockDim.x) lds[nt::lp(gl::rev_bits(p, log_n))] = src[p];
   __syncthreads();
   nt::ntt_lds<true>(lds, log_n, tw_inv);
   // base^-1 = g^-1 w_N^-s
@@ -349,7 +352,7 @@ __global__ void __launch_bounds__(512) k_qintt_blocks(const uint64_t *__restrict
   const uint64_t step = gl::pow(binv, blockDim.x);
   uint64_t *dst = out + b * o_bstride + ((uint64_t)c << rate_bits) * n + (uint64_t)s * n;
   for (uint32_t k = threadIdx.x; k < n; k += blockDim.x) {
-    dst[k] = gl::mul(lds[gl::rev_bits(k, log_n)], f);
+    dst[k] = gl::mul(lds[nt::lp(gl::rev_bits(k, log_n))], f);
     f = gl::mul(f, step);
   }
 }
@@ -383,32 +386,43 @@ __global__ void __launch_bounds__(256) k_qintt_radix(const uint64_t *__restrict_
 
 // ---------------------------------------------------------------- a10
 
-// value of each coefficient column at an extension point: out[b][poly]
+// value of each coefficient column at an extension point: out[b][poly].
+// A block evaluates OPEN_PB polys of one proof: thread t walks k = t + jT with
+// one running power z^k shared by the OPEN_PB columns (2 base products per
+// coefficient instead of 6), then a tree reduction per poly.  blockDim = T
+// (host: 256, or n/4 >= 64 for small circuits so z^t's pow stays amortised).
 __global__ void __launch_bounds__(256) k_openings(const uint64_t *__restrict__ coeffs, uint64_t c_bstride,
                                                   uint32_t npolys, uint32_t log_n, const uint64_t *__restrict__ pts,
                                                   uint32_t pt_off, uint64_t *__restrict__ out, uint32_t out_off) {
-  __shared__ ext red[256];
-  const uint32_t n = 1u << log_n;
-  const uint32_t p = blockIdx.x, b = blockIdx.y;
-  const uint64_t *cf = coeffs + b * c_bstride + (uint64_t)p * n;
+  __shared__ ext red[OPEN_PB][256];
+  const uint32_t n = 1u << log_n, T = blockDim.x, t = threadIdx.x;
+  const uint32_t p0 = blockIdx.x * OPEN_PB, b = blockIdx.y;
+  const uint32_t np = min((uint32_t)OPEN_PB, npolys - p0);
+  const uint64_t *cf = coeffs + b * c_bstride + (uint64_t)p0 * n;
   const ext z = ext{pts[b * CHAL_STRIDE + pt_off], pts[b * CHAL_STRIDE + pt_off + 1]};
-  ext zp = gl::ext_pow(z, threadIdx.x);
-  const ext zs = gl::ext_pow(z, blockDim.x);
-  ext acc{0, 0};
-  for (uint32_t k = threadIdx.x; k < n; k += blockDim.x) {
-    acc = gl::ext_add(acc, gl::ext_scale(zp, cf[k]));
+  ext zp = gl::ext_pow(z, t);
+  const ext zs = gl::ext_pow(z, T);
+  ext acc[OPEN_PB];
+#pragma unroll
+  for (int j = 0; j < OPEN_PB; j++) acc[j] = ext{0, 0};
+  for (uint32_t k = t; k < n; k += T) {
+#pragma unroll
+    for (int j = 0; j < OPEN_PB; j++)
+      if ((uint32_t)j < np) acc[j] = gl::ext_add(acc[j], gl::ext_scale(zp, cf[(uint64_t)j * n + k]));
     zp = gl::ext_mul(zp, zs);
   }
-  red[threadIdx.x] = acc;
+#pragma unroll
+  for (int j = 0; j < OPEN_PB; j++) red[j][t] = acc[j];
   __syncthreads();
-  for (uint32_t o = blockDim.x / 2; o; o >>= 1) {
-    if (threadIdx.x < o) red[threadIdx.x] = gl::ext_add(red[threadIdx.x], red[threadIdx.x + o]);
+  for (uint32_t o = T / 2; o; o >>= 1) {
+    if (t < o)
+      for (uint32_t j = 0; j < np; j++) red[j][t] = gl::ext_add(red[j][t], red[j][t + o]);
     __syncthreads();
   }
-  if (!threadIdx.x) {
-    uint64_t *dst = out + b * OPEN_STRIDE + 2 * (out_off + p);
-    dst[0] = red[0].c0;
-    dst[1] = red[0].c1;
+  if (t < np) {
+    uint64_t *dst = out + b * OPEN_STRIDE + 2 * (out_off + p0 + t);
+    dst[0] = red[t][0].c0;
+    dst[1] = red[t][0].c1;
   }
 }
 
@@ -560,9 +574,9 @@ __global__ void __launch_bounds__(256) k_fold(const uint64_t *__restrict__ cin, 
 // ---------------------------------------------------------------- a12
 
 __global__ void __launch_bounds__(256) k_pow(const uint64_t *__restrict__ states, const uint32_t *__restrict__ pos,
-                                             uint64_t *__restrict__ found, uint64_t base, uint32_t bits) {
-  const uint32_t b = blockIdx.y;
-  if (found[b] != ~0ull && found[b] < base) return;
+                                             const uint32_t *__restrict__ active, uint64_t *__restrict__ found,
+                                             uint64_t base, uint32_t bits) {
+  const uint32_t b = active[blockIdx.y];
   const uint64_t cand = base + (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
   uint64_t s[12];
 #pragma unroll
