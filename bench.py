@@ -30,6 +30,26 @@ sys.path.insert(0, os.path.join(ROOT, "qp-zk-circuits-rm_amd"))
 sys.path.insert(0, os.path.join(ROOT, "tests"))
 
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec peak (MI355X_MICROARCH.md)
+# HBM traffic of the roofline kernel from rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE
+# passes (tools/pmc_summary.py applies the gfx950 corrections); per proof, scaled
+# to the bench's per-launch proof count
+PMC_FILE = os.path.join(ROOT, "profiles", "r01_v5_pmc_hbm_b128.json")
+
+
+def pmc_traffic(kernel, ncols, log_n, proofs):
+    """HBM bytes per launch of `kernel` for `proofs` proofs of `ncols` columns, or None."""
+    try:
+        recs = json.load(open(PMC_FILE))
+    except (OSError, ValueError):
+        return None
+    for r in recs:
+        if r.get("kernel") != kernel or not r.get("hbm_bytes"):
+            continue
+        lanes_per_proof = ncols * (1 << log_n) // 16  # one 2^(log_n - 4)-lane workgroup per column
+        if r["grid_lanes"] % lanes_per_proof:
+            continue
+        return r["hbm_bytes"] / (r["grid_lanes"] // lanes_per_proof) * proofs
+    return None
 
 
 def parse():
@@ -210,7 +230,13 @@ def main():
             "roofline": {"kernel": f"k_lde (wires LDE, 135 cols x 2^{circuit.degree_bits} -> "
                                    f"2^{circuit.degree_bits + 3})", "bound": "hbm",
                          "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                         "frac": achieved / HBM_PEAK_GBS if achieved else None, "traffic": None,
+                         "frac": achieved / HBM_PEAK_GBS if achieved else None,
+                         "traffic": pmc_traffic("qpk::k_lde_cosets<9>", circuit.num_wires, circuit.degree_bits,
+                                                per[0]) if circuit.degree_bits == 13 else None,
+                         "traffic_unit": "bytes per launch",
+                         "algorithmic_bytes_per_launch": lde["units"] / max(lde["launches"], 1),
+                         "traffic_source": "profiles/r01_v5_pmc_hbm_b128.json (rocprofv3 --pmc FETCH_SIZE, WRITE_SIZE "
+                                           "passes of this bench at batch 128), per proof x proofs per launch",
                          "avg_launch_ms": lde["ms"] / max(lde["launches"], 1),
                          "note": "per-launch HIP-event time on the prover streams over the timed region, where "
                                  "the other prover's kernels share the GPU; isolated_*: one prover alone"},

@@ -92,7 +92,10 @@ __device__ __forceinline__ void permute_nc_v1(uint64_t s[12]) {
 // permutation used by the kernels: poseidon_fast.h (2.24 vs 1.67 Gperm/s for
 // permute_nc_v1 on MI355X, tools/poseidon_ubench.hip).  Inputs in [0,2^64),
 // outputs in [0,2^64) (call canon on lanes read out)
-__device__ __forceinline__ void permute_nc(uint64_t s[12]) { pf::permute_nc<0>(s); }
+#ifndef QP_POSEIDON_MODE
+#define QP_POSEIDON_MODE 0
+#endif
+__device__ __forceinline__ void permute_nc(uint64_t s[12]) { pf::permute_nc<QP_POSEIDON_MODE>(s); }
 
 __device__ __forceinline__ void permute(uint64_t s[12]) {
   permute_nc(s);

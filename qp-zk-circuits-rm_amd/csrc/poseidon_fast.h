@@ -211,6 +211,70 @@ __device__ __forceinline__ void mds_rows(uint64_t s[12], const uint32_t lo[12], 
   }
 }
 
+// One MDS row as a single asm block: 24 v_mad_u64_u32 on the rotated halves
+// (x[i] = half[(i+R)%12]) with the circulant constants inline, starting from
+// the folded round-constant halves kl/kh.  Inside one asm statement the
+// compiler's conservative inline-asm hazard padding (an s_nop after every
+// SGPR-writing asm VALU op) disappears; the mads only write the dead carry
+// SGPR pair and read none, so no wait state is needed between them.
+#define QP_MDS_ROW_ASM(C0)                                                                                  \
+  asm("v_mad_u64_u32 %0, %2, %3, " #C0 ", %27\n\t"                                                     \
+      "v_mad_u64_u32 %1, %2, %15, " #C0 ", %28\n\t"                                                    \
+      "v_mad_u64_u32 %0, %2, %4, 15, %0\n\t"                                                           \
+      "v_mad_u64_u32 %1, %2, %16, 15, %1\n\t"                                                          \
+      "v_mad_u64_u32 %0, %2, %5, 41, %0\n\t"                                                           \
+      "v_mad_u64_u32 %1, %2, %17, 41, %1\n\t"                                                          \
+      "v_mad_u64_u32 %0, %2, %6, 16, %0\n\t"                                                           \
+      "v_mad_u64_u32 %1, %2, %18, 16, %1\n\t"                                                          \
+      "v_mad_u64_u32 %0, %2, %7, 2, %0\n\t"                                                            \
+      "v_mad_u64_u32 %1, %2, %19, 2, %1\n\t"                                                           \
+      "v_mad_u64_u32 %0, %2, %8, 28, %0\n\t"                                                           \
+      "v_mad_u64_u32 %1, %2, %20, 28, %1\n\t"                                                          \
+      "v_mad_u64_u32 %0, %2, %9, 13, %0\n\t"                                                           \
+      "v_mad_u64_u32 %1, %2, %21, 13, %1\n\t"                                                          \
+      "v_mad_u64_u32 %0, %2, %10, 13, %0\n\t"                                                          \
+      "v_mad_u64_u32 %1, %2, %22, 13, %1\n\t"                                                          \
+      "v_mad_u64_u32 %0, %2, %11, 39, %0\n\t"                                                          \
+      "v_mad_u64_u32 %1, %2, %23, 39, %1\n\t"                                                          \
+      "v_mad_u64_u32 %0, %2, %12, 18, %0\n\t"                                                          \
+      "v_mad_u64_u32 %1, %2, %24, 18, %1\n\t"                                                          \
+      "v_mad_u64_u32 %0, %2, %13, 34, %0\n\t"                                                          \
+      "v_mad_u64_u32 %1, %2, %25, 34, %1\n\t"                                                          \
+      "v_mad_u64_u32 %0, %2, %14, 20, %0\n\t"                                                          \
+      "v_mad_u64_u32 %1, %2, %26, 20, %1"                                                                \
+      : "=&v"(al), "=&v"(ah), "=&s"(cd)                                                                  \
+      : "v"(lo[(0 + R) % 12]), "v"(lo[(1 + R) % 12]), "v"(lo[(2 + R) % 12]), "v"(lo[(3 + R) % 12]),     \
+        "v"(lo[(4 + R) % 12]), "v"(lo[(5 + R) % 12]), "v"(lo[(6 + R) % 12]), "v"(lo[(7 + R) % 12]),     \
+        "v"(lo[(8 + R) % 12]), "v"(lo[(9 + R) % 12]), "v"(lo[(10 + R) % 12]), "v"(lo[(11 + R) % 12]),   \
+        "v"(hi[(0 + R) % 12]), "v"(hi[(1 + R) % 12]), "v"(hi[(2 + R) % 12]), "v"(hi[(3 + R) % 12]),     \
+        "v"(hi[(4 + R) % 12]), "v"(hi[(5 + R) % 12]), "v"(hi[(6 + R) % 12]), "v"(hi[(7 + R) % 12]),     \
+        "v"(hi[(8 + R) % 12]), "v"(hi[(9 + R) % 12]), "v"(hi[(10 + R) % 12]), "v"(hi[(11 + R) % 12]),   \
+        "s"(kl), "s"(kh))
+
+template <int R>
+__device__ __forceinline__ void mds_row_block(uint64_t &al, uint64_t &ah, const uint32_t lo[12],
+                                              const uint32_t hi[12], uint64_t kl, uint64_t kh) {
+  static_assert(ps::mds_circ(0) == 17 && ps::mds_circ(1) == 15 && ps::mds_circ(11) == 20, "MDS constants");
+  uint64_t cd;
+  if constexpr (R == 0) {
+    QP_MDS_ROW_ASM(25);  // circulant 17 + diagonal 8
+  } else {
+    QP_MDS_ROW_ASM(17);
+  }
+  (void)cd;
+}
+
+template <int R, int RC>
+__device__ __forceinline__ void mds_rows_block(uint64_t s[12], const uint32_t lo[12], const uint32_t hi[12]) {
+  if constexpr (R < 12) {
+    constexpr uint64_t k = RC >= 0 ? ps::rc_cx(RC * 12 + R) : 0;
+    uint64_t al, ah;
+    mds_row_block<R>(al, ah, lo, hi, k & EPS, k >> 32);
+    s[R] = reduce_row(al, ah);
+    mds_rows_block<R + 1, RC>(s, lo, hi);
+  }
+}
+
 // s <- MDS(s) + RC[next] (next < 0: no constant)
 template <int M, int NEXT>
 __device__ __forceinline__ void mds(uint64_t s[12]) {
@@ -220,12 +284,65 @@ __device__ __forceinline__ void mds(uint64_t s[12]) {
     lo[i] = lo32(s[i]);
     hi[i] = hi32(s[i]);
   }
-  mds_rows<M, 0, NEXT>(s, lo, hi);
+  if constexpr (M >= 3) mds_rows_block<0, NEXT>(s, lo, hi);
+  else mds_rows<M, 0, NEXT>(s, lo, hi);
+}
+
+// block-asm MDS with the next round's constants read at run time (uniform
+// index: scalar loads into SGPRs) — the body of the rolled partial-round loop
+template <int R>
+__device__ __forceinline__ void mds_rows_block_dyn(uint64_t s[12], const uint32_t lo[12], const uint32_t hi[12],
+                                                   const uint64_t *__restrict__ k) {
+  if constexpr (R < 12) {
+    const uint64_t kr = k[R];
+    uint64_t al, ah;
+    mds_row_block<R>(al, ah, lo, hi, kr & EPS, kr >> 32);
+    s[R] = reduce_row(al, ah);
+    mds_rows_block_dyn<R + 1>(s, lo, hi, k);
+  }
+}
+
+// one full round (12 S-boxes + MDS folding the next round's constants, read at
+// run time) — the body of the rolled full-round loops of mode 5
+__device__ __forceinline__ void full_round_dyn(uint64_t s[12], const uint64_t *__restrict__ knext) {
+#pragma unroll
+  for (int i = 0; i < 12; i++) s[i] = sbox(s[i]);
+  uint32_t lo[12], hi[12];
+#pragma unroll
+  for (int i = 0; i < 12; i++) {
+    lo[i] = lo32(s[i]);
+    hi[i] = hi32(s[i]);
+  }
+  mds_rows_block_dyn<0>(s, lo, hi, knext);
 }
 
 template <int M, int R>
 __device__ __forceinline__ void rounds(uint64_t s[12]) {
-  if constexpr (R < 30) {
+  if constexpr (M == 5 && R == 0) {
+    // every round rolled: a ~4k-instruction permutation
+#pragma unroll 1
+    for (int r = 0; r < 4; r++) full_round_dyn(s, ps::RC_DEV + (r + 1) * 12);
+    rounds<5, 4>(s);  // rolled partial rounds, then the rolled tail
+  } else if constexpr (M == 5 && R == 26) {
+#pragma unroll 1
+    for (int r = 26; r < 29; r++) full_round_dyn(s, ps::RC_DEV + (r + 1) * 12);
+    rounds<3, 29>(s);  // the last round: MDS without a next constant
+  } else if constexpr ((M == 4 || M == 5) && R == 4) {
+    // 22 partial rounds as a loop: ~9k fewer instructions of code (the
+    // unrolled permutation is several times the instruction cache)
+#pragma unroll 1
+    for (int r = 4; r < 26; r++) {
+      s[0] = sbox(s[0]);
+      uint32_t lo[12], hi[12];
+#pragma unroll
+      for (int i = 0; i < 12; i++) {
+        lo[i] = lo32(s[i]);
+        hi[i] = hi32(s[i]);
+      }
+      mds_rows_block_dyn<0>(s, lo, hi, ps::RC_DEV + (r + 1) * 12);
+    }
+    rounds<M, 26>(s);
+  } else if constexpr (R < 30) {
     constexpr bool full = R < 4 || R >= 26;
     if constexpr (full) {
 #pragma unroll
@@ -239,7 +356,9 @@ __device__ __forceinline__ void rounds(uint64_t s[12]) {
 }
 
 // permutation; inputs in [0, 2^64), outputs in [0, 2^64) (canon() lanes read out)
-// M: 0 = asm mads, 1 = compiler mads on opaque constants, 2 = 1 + C reductions
+// M: 0 = asm mads, 1 = compiler mads on opaque constants, 2 = 1 + C reductions,
+//    3 = 0 with each MDS row's 24 mads in one asm block, 4 = 3 with the
+//    partial rounds rolled into a loop, 5 = every round rolled
 template <int M = 1>
 __device__ __forceinline__ void permute_nc(uint64_t s[12]) {
 #pragma unroll

@@ -19,7 +19,7 @@ step() {  # step <name> <timeout> <cmd...>
 pmc() {  # pmc <name> <counters...>
   local name=$1; shift
   step "pmc_$name" 300 rocprofv3 --pmc "$@" --output-format csv -d "gpurun_out/pmc_$name" -o run -- \
-    python3 bench.py --steps 1 --warmup 1 --cpu-sample 0 --batch 64
+    python3 bench.py --steps 1 --warmup 1 --cpu-sample 0 --provers 1 --batch 128
 }
 for s in "$@"; do
   case $s in

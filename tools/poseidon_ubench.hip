@@ -10,6 +10,9 @@
 //   V7: pf:: (poseidon_fast.h) mode 0: asm mads, asm reductions, folded round constants
 //   V8: pf mode 1: compiler mads on opaque constants, asm reductions
 //   V9: pf mode 2: mode 1 with C reductions
+//   V10: pf mode 3: mode 0 with each MDS row's 24 mads in one asm block
+//   V11: pf mode 4: mode 3 with the partial rounds rolled into a loop
+//   V12: pf mode 5: every round rolled
 // Build: hipcc --offload-arch=gfx950 -O3 -std=c++17 -I qp-zk-circuits-rm_amd/csrc tools/poseidon_ubench.hip
 #include <hip/hip_runtime.h>
 #include <stdint.h>
@@ -168,6 +171,9 @@ __global__ void __launch_bounds__(256) kperm(uint64_t *st, uint64_t n) {
     if (V == 7) pf::permute_nc<0>(s);
     if (V == 8) pf::permute_nc<1>(s);
     if (V == 9) pf::permute_nc<2>(s);
+    if (V == 10) pf::permute_nc<3>(s);
+    if (V == 11) pf::permute_nc<4>(s);
+    if (V == 12) pf::permute_nc<5>(s);
   }
   for (int k = 0; k < 12; k++) st[k * n + i] = V == 0 ? s[k] : psd::canon(s[k]);
 }
@@ -197,8 +203,8 @@ int main() {
   uint64_t *d;
   (void)hipMalloc(&d, n * 96);
   (void)hipMemset(d, 7, n * 96);
-  constexpr int NV = 10;
-  float t[NV] = {run<0>(d, n), run<1>(d, n), run<2>(d, n), run<3>(d, n), run<4>(d, n), run<5>(d, n), run<6>(d, n), run<7>(d, n), run<8>(d, n), run<9>(d, n)};
+  constexpr int NV = 13;
+  float t[NV] = {run<0>(d, n), run<1>(d, n), run<2>(d, n), run<3>(d, n), run<4>(d, n), run<5>(d, n), run<6>(d, n), run<7>(d, n), run<8>(d, n), run<9>(d, n), run<10>(d, n), run<11>(d, n), run<12>(d, n)};
   // check all variants agree
   uint64_t *h = new uint64_t[12 * NV];
   for (int v = 0; v < NV; v++) {
@@ -213,6 +219,9 @@ int main() {
     if (v == 7) kperm<7, 1><<<(unsigned)(n / 256), 256>>>(d, n);
     if (v == 8) kperm<8, 1><<<(unsigned)(n / 256), 256>>>(d, n);
     if (v == 9) kperm<9, 1><<<(unsigned)(n / 256), 256>>>(d, n);
+    if (v == 10) kperm<10, 1><<<(unsigned)(n / 256), 256>>>(d, n);
+    if (v == 11) kperm<11, 1><<<(unsigned)(n / 256), 256>>>(d, n);
+    if (v == 12) kperm<12, 1><<<(unsigned)(n / 256), 256>>>(d, n);
     (void)hipDeviceSynchronize();
     for (int k = 0; k < 12; k++) (void)hipMemcpy(h + v * 12 + k, d + k * n, 8, hipMemcpyDeviceToHost);
   }
