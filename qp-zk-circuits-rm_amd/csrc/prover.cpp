@@ -90,7 +90,7 @@ struct qp_prover {
   Tree cs;
   DevBuf sigmas, kis;
   Tree wires, zs, quot;
-  DevBuf chal, apow, prods, qvals, cbuf, openings, comp, fin, pow_state, pow_found, pow_pos, pow_active, qidx, qout;
+  DevBuf chal, apow, prods, qvals, cbuf, openings, comp, fin, pow_state, pow_found, pow_pos, pow_active, qidx, qout, qtab;
   std::vector<DevBuf> fvals, fdig, fcoef;
   size_t qout_words = 0;
   std::unique_ptr<qh::ThreadPool> pool;
@@ -254,6 +254,34 @@ int setup(qp_prover *P) {
   TRY(P->pow_found.alloc(B));
   TRY(P->pow_pos.alloc((B + 1) / 2));
   TRY(P->pow_active.alloc((B + 1) / 2));
+  {
+    // proof-independent point tables of the quotient, leaf order t (point
+    // x = g w_N^rev(t)): xtab[t] = x, l0tab[t] = L_0(x) = Z_H(x) / (n (x - 1))
+    // (one batch inversion here instead of a field inversion per point per proof)
+    const uint32_t logN = P->log_n + P->rate_bits;
+    const uint64_t N = 1ull << logN;
+    const uint64_t wN = gl::root_of_unity(logN);
+    std::vector<uint64_t> tab(2 * N), den(N), pre(N);
+    for (uint64_t j = 0, w = 1; j < N; j++, w = gl::mul(w, wN)) {
+      const uint64_t t = gl::rev_bits((uint32_t)j, logN);
+      tab[t] = gl::mul(gl::GEN, w);
+      den[t] = gl::mul(gl::sub(tab[t], 1), n % gl::P);
+    }
+    uint64_t acc = 1;
+    for (uint64_t t = 0; t < N; t++) {
+      pre[t] = acc;
+      acc = gl::mul(acc, den[t]);
+    }
+    uint64_t inv = gl::inv(acc);
+    for (uint64_t t = N; t-- > 0;) {
+      const uint64_t dinv = gl::mul(inv, pre[t]);
+      inv = gl::mul(inv, den[t]);
+      const uint64_t zh = gl::sub(gl::pow(tab[t], n), 1);
+      tab[N + t] = gl::mul(zh, dinv);
+    }
+    TRY(P->qtab.alloc(2 * N));
+    TRY(hipMemcpy(P->qtab.p, tab.data(), 2 * N * 8, hipMemcpyHostToDevice));
+  }
   TRY(P->qidx.alloc(((size_t)B * P->nq + 1) / 2));
   {
     size_t w = 0;
@@ -437,6 +465,8 @@ int prove_batch(qp_prover *P, const uint64_t *const *wires_host, const uint64_t 
     a.chal = P->chal.p;
     a.tw = c->tw.fwd;
     a.apow = P->apow.p;
+    a.xtab = P->qtab.p;
+    a.l0tab = P->qtab.p + N;
     const uint32_t B = 1u << P->rate_bits;
     const uint64_t wN = gl::root_of_unity(logN);
     for (uint32_t k = 0; k < B; k++) {

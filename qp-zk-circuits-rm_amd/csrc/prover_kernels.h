@@ -26,6 +26,7 @@ struct QuotientArgs {
   const uint64_t *cs_lde, *w_lde, *z_lde;
   uint64_t w_bstride, z_bstride;
   const uint64_t *chal, *tw, *apow;
+  const uint64_t *xtab, *l0tab;  // [N] leaf order: x = g w_N^rev(t), L_0(x)
   uint64_t zh[16], zh_inv[16];
   uint64_t *q_out;
   uint64_t q_bstride;

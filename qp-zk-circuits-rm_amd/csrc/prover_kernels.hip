@@ -215,7 +215,7 @@ template <int PH>
 #endif
 __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(QP_QUOTIENT_WAVES))) k_quotient(QuotientArgs a) {
   const uint32_t logN = a.log_n + a.rate_bits;
-  const uint64_t N = 1ull << logN, n = 1ull << a.log_n;
+  const uint64_t N = 1ull << logN;
   const uint32_t t = blockIdx.x * blockDim.x + threadIdx.x;
   if (t >= N) return;
   const uint32_t b = blockIdx.y;
@@ -233,10 +233,9 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(QP_QUO
   const uint32_t R = a.R, qdf = a.qdf, nchunks = (R + qdf - 1) / qdf, npp = nchunks - 1;
   if (PH != 1) {
     const uint32_t tn = gl::rev_bits((j + (1u << a.rate_bits)) & (uint32_t)(N - 1), logN);
-    const uint64_t x = gl::mul(gl::GEN, wpow_N(a.tw, j, logN));
-    const uint64_t zh = a.zh[j & ((1u << a.rate_bits) - 1)];
+    const uint64_t x = a.xtab[t];
     // L_0(x) (Z_c - 1)
-    const uint64_t l0 = gl::mul(zh, gl::inv(gl::mul(gl::sub(x, 1), n % gl::P)));
+    const uint64_t l0 = a.l0tab[t];
     for (uint32_t c = 0; c < 2; c++) A.emit(gfn::mul(l0, gfn::sub(zl[(uint64_t)c * N + t], 1)));
     // partial-product checks
     for (uint32_t c = 0; c < 2; c++) {
