@@ -205,6 +205,16 @@ def main():
         prover.kernel_stats(reset=True)
         prover.prove_wires_dev(d_wires.data_ptr(), pis[:per[0]], per[0])
         iso = prover.kernel_stats()
+    # single-proof latency (BASELINE configs[1]): one proof through the same prover
+    lat = None
+    if rank == 0:
+        prover.set_timing(False)
+        ts = []
+        for _ in range(3):
+            t1 = time.perf_counter()
+            prover.prove_wires_dev(d_wires.data_ptr(), pis[:1], 1)
+            ts.append((time.perf_counter() - t1) * 1e3)
+        lat = sorted(ts)[1]
     if rank == 0:
         total = world * B * args.steps
         lde = ks["lde_wires"]
@@ -244,6 +254,7 @@ def main():
                              "quotient_avg_launch_ms": ks["quotient"]["ms"] / max(ks["quotient"]["launches"], 1)},
             "stage_ms_per_step": {k: v / args.steps for k, v in stages.items()},
             "proof_bytes": len(proofs[0]),
+            "latency_1proof_ms": lat,
             "warmup_proof_verified": verified,
         }
         if iso is not None and iso["lde_wires"]["ms"]:
