@@ -131,6 +131,9 @@ __device__ __forceinline__ uint64_t tw_pow(const uint64_t *__restrict__ tw, uint
   return E < HALF ? tw[E] : gl::P - tw[E - HALF];  // tw entries are canonical and nonzero
 }
 
+#ifndef QP_PASS32
+#define QP_PASS32 1
+#endif
 #ifndef QP_LDS_PAD
 #define QP_LDS_PAD 1
 #endif
@@ -180,6 +183,43 @@ __device__ __forceinline__ void tail(uint64_t *a, uint32_t n) {
   __syncthreads();
 }
 
+// x * w_32^j (forward) or w_32^-j (inverse), w_32 = 2^6; j folds to a constant
+// after unrolling, so each case is a shift + short reduction
+template <bool INV>
+__device__ __forceinline__ uint64_t mul_w32(uint64_t x, int j) {
+#define QP_W32(J) \
+  case J: return INV ? mul_pow2<(192 - 6 * J) % 192>(x) : mul_pow2<(6 * J) % 192>(x);
+  switch (j) {
+    QP_W32(1) QP_W32(2) QP_W32(3) QP_W32(4) QP_W32(5) QP_W32(6) QP_W32(7) QP_W32(8)
+    QP_W32(9) QP_W32(10) QP_W32(11) QP_W32(12) QP_W32(13) QP_W32(14) QP_W32(15)
+    default: return x;
+  }
+#undef QP_W32
+}
+
+// The S = 32 radix-16 pass (q = 2): its twiddles w_32^{t brev4(m)}, t in {0,1},
+// are powers of two.  Groups are assigned so t is uniform per wave (t = bit 6
+// of g): t = 0 waves skip the twiddles, t = 1 waves shift instead of
+// multiplying.  Needs n/16 to be a multiple of 128.
+template <bool INV>
+__device__ __forceinline__ void pass32(uint64_t *a, uint32_t n) {
+  for (uint32_t g = threadIdx.x; g < (n >> 4); g += blockDim.x) {
+    const uint32_t t = (g >> 6) & 1, sp = ((g >> 7) << 6) | (g & 63);
+    uint64_t *base = a + lp((sp << 5) + t);
+    uint64_t r[16];
+#pragma unroll
+    for (int m = 0; m < 16; m++) r[m] = base[lp(2 * m)];
+    dft16<INV>(r);
+    if (t) {
+#pragma unroll
+      for (int m = 1; m < 16; m++) r[m] = mul_w32<INV>(r[m], (int)brev4(m));
+    }
+#pragma unroll
+    for (int m = 0; m < 16; m++) base[lp(2 * m)] = r[m];
+  }
+  __syncthreads();
+}
+
 // In-place DIF over LDS a[lp(0..2^log_n)), all threads of the block participate,
 // starting at sub-problem size 2^log_S (log_S = log_n: the whole transform;
 // smaller: the levels above were already done, e.g. from registers).
@@ -190,6 +230,11 @@ __device__ __forceinline__ void ntt_lds_from(uint64_t *a, uint32_t log_n, uint32
   const uint32_t T = blockDim.x;
   // radix-16 passes
   while (log_S >= 4) {
+    if (QP_PASS32 && log_S == 5 && (n >> 4) % 128 == 0 && T % 64 == 0) {
+      pass32<INV>(a, n);
+      log_S = 1;
+      continue;
+    }
     const uint32_t S = 1u << log_S, q = S >> 4, log_q = log_S - 4;
     for (uint32_t g = threadIdx.x; g < (n >> 4); g += T) {
       const uint32_t sp = g >> log_q, t = g & (q - 1);
