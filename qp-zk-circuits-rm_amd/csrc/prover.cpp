@@ -250,7 +250,7 @@ int setup(qp_prover *P) {
     lg -= P->arity[l];
     TRY(P->fcoef[l].alloc(((size_t)B * 2) << lg));
   }
-  TRY(P->pow_state.alloc((size_t)B * 12));
+  TRY(P->pow_state.alloc((size_t)B * 24));
   TRY(P->pow_found.alloc(B));
   TRY(P->pow_pos.alloc((B + 1) / 2));
   TRY(P->pow_active.alloc((B + 1) / 2));
@@ -301,7 +301,7 @@ int setup(qp_prover *P) {
   P->h_qout.assign((size_t)B * P->qout_words, 0);
   P->h_qidx.assign((size_t)B * P->nq, 0);
   P->h_pos.assign(B, 0);
-  P->h_powst.assign((size_t)B * 12, 0);
+  P->h_powst.assign((size_t)B * 24, 0);
   P->h_found.assign(B, 0);
   TRY(hipStreamSynchronize(c->stream));
   P->proof_len = proof_size(P);
@@ -618,12 +618,30 @@ int prove_batch(qp_prover *P, const uint64_t *const *wires_host, const uint64_t 
       S.t.observe(f0[i]);
       S.t.observe(f1[i]);
     }
-    uint64_t *ps_ = P->h_powst.data() + b * 12;
-    memcpy(ps_, S.t.state, 96);
-    for (uint32_t i = 0; i < S.t.nin; i++) ps_[i] = S.t.in[i];
-    P->h_pos[b] = S.t.nin;
+    // sponge state with the candidate at lane pos; round 0 of the permutation
+    // is folded here: every lane but pos is candidate-independent, so
+    //   state after round 0 (+ round-1 constants) = K + coef * sbox(cand + rc_pos)
+    // with K[r] = sum_{j != pos} M[r][j] sbox(s_j + rc_j) + rc(1)_r and
+    // coef[r] = M[r][pos] (a small circulant/diagonal entry)
+    uint64_t st12[12];
+    memcpy(st12, S.t.state, 96);
+    for (uint32_t i = 0; i < S.t.nin; i++) st12[i] = S.t.in[i];
+    const uint32_t pos = S.t.nin;
+    uint64_t y[12];
+    for (uint32_t j = 0; j < 12; j++) y[j] = j == pos ? 0 : ps::sbox(gl::add(st12[j], ps::rc(j)));
+    uint64_t *pre = P->h_powst.data() + b * 24;
+    for (uint32_t r = 0; r < 12; r++) {
+      uint64_t k = ps::rc(12 + r);
+      for (uint32_t j = 0; j < 12; j++) {
+        const uint64_t m = ps::mds_circ((j + 12 - r) % 12) + (r == 0 && j == 0 ? 8 : 0);
+        if (j != pos) k = gl::add(k, gl::mul(m, y[j]));
+        else pre[12 + r] = m;
+      }
+      pre[r] = k;
+    }
+    P->h_pos[b] = pos;
   });
-  TRY(hipMemcpyAsync(P->pow_state.p, P->h_powst.data(), (size_t)nb * 96, hipMemcpyHostToDevice, s));
+  TRY(hipMemcpyAsync(P->pow_state.p, P->h_powst.data(), (size_t)nb * 192, hipMemcpyHostToDevice, s));
   TRY(hipMemcpyAsync(P->pow_pos.p, P->h_pos.data(), (size_t)nb * 4, hipMemcpyHostToDevice, s));
   TRY(hipMemsetAsync(P->pow_found.p, 0xFF, (size_t)nb * 8, s));
   {

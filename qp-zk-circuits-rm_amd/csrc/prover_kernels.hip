@@ -577,14 +577,17 @@ __global__ void __launch_bounds__(256) k_pow(const uint64_t *__restrict__ states
                                              uint64_t base, uint32_t bits) {
   const uint32_t b = active[blockIdx.y];
   const uint64_t cand = base + (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  // round 0 precomputed on the host (prover.cpp): s = K + coef * sbox(cand + rc_pos)
+  const uint64_t *pre = states + b * 24;
+  const uint64_t y = pf::sbox(pf::add_c(cand, ps::RC_DEV[pos[b]]));
+  const uint32_t y0 = pf::lo32(y), y1 = pf::hi32(y);
   uint64_t s[12];
 #pragma unroll
-  for (int i = 0; i < 12; i++) s[i] = states[b * 12 + i];
-  const uint32_t ps_ = pos[b];
-#pragma unroll
-  for (int i = 0; i < 8; i++)
-    if ((uint32_t)i == ps_) s[i] = cand;
-  psd::permute_nc(s);
+  for (int r = 0; r < 12; r++) {
+    const uint32_t c = (uint32_t)pre[12 + r];
+    s[r] = pf::reduce_row((uint64_t)y0 * c + (pre[r] & pf::EPS), (uint64_t)y1 * c + (pre[r] >> 32));
+  }
+  pf::rounds<QP_POSEIDON_MODE, 1>(s);
   if ((psd::canon(s[7]) >> (64 - bits)) == 0) atomicMin((unsigned long long *)&found[b], (unsigned long long)cand);
 }
 
