@@ -260,27 +260,28 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(QP_QUO
   // selector filter multiplies each gate's sum once
   const uint32_t pre = 2 * (1 + nchunks);
   uint64_t acc0 = A.s0, acc1 = A.s1;  // PH 1 adds the PH 0 sums at the end
-  uint64_t consts[8];
-  for (uint32_t k = 0; k < a.num_constants && k < 8; k++) consts[k] = cs[(uint64_t)k * N];
+  // constant columns are re-read where used (L1/L2 hits) rather than held in
+  // 16 VGPRs across the Poseidon gate evaluation
+#define CONSTCOL(k) cs[(uint64_t)(k) * N]
   const uint32_t nsel = a.g.nsel;
   for (uint32_t gi = 0; gi < a.g.ngates; gi++) {
     const uint32_t kind = a.g.kind[gi];
     if (kind == GK_NOOP || (PH == 0 && kind == GK_POSEIDON) || (PH == 1 && kind != GK_POSEIDON)) continue;
     const uint32_t si = a.g.sel_index[gi];
-    const uint64_t s = consts[si];
+    const uint64_t s = CONSTCOL(si);
     uint64_t f = 1;
     for (uint32_t jj = a.g.grp_lo[si]; jj < a.g.grp_hi[si]; jj++)
       if (jj != gi) f = gfn::mul(f, gfn::sub(jj, s));
     if (nsel > 1) f = gfn::mul(f, gfn::sub(0xFFFFFFFFull, s));
     A.s0 = A.s1 = 0;
     A.i = pre;
-    const uint64_t *gc = consts + nsel;
+    const uint64_t *gc = cs + (uint64_t)nsel * N;
     if (kind == GK_POSEIDON) {
       poseidon_gate(wl, N, A);
     } else {
       switch (kind) {
         case GK_CONSTANT:
-          for (uint32_t i = 0; i < a.g.param[gi]; i++) A.emit(gfn::sub(gc[i], WV(i)));
+          for (uint32_t i = 0; i < a.g.param[gi]; i++) A.emit(gfn::sub(gc[(uint64_t)i * N], WV(i)));
           break;
         case GK_PUBLIC_INPUT:
           for (uint32_t i = 0; i < 4; i++) A.emit(gfn::sub(WV(i), ch[CH_PIH + i]));
@@ -299,7 +300,7 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(QP_QUO
         case GK_ARITHMETIC:
           for (uint32_t i = 0; i < a.g.param[gi]; i++) {
             const uint64_t comp = gfn::add(gfn::mul(gfn::mul(WV(4 * i), WV(4 * i + 1)), gc[0]),
-                                           gfn::mul(WV(4 * i + 2), gc[1]));
+                                           gfn::mul(WV(4 * i + 2), gc[N]));
             A.emit(gfn::sub(WV(4 * i + 3), comp));
           }
           break;
