@@ -25,6 +25,11 @@
 #include "kernels.h"
 #include "prover_kernels.h"
 
+// PoW search window per launch (candidates per still-searching proof), log2
+#ifndef QP_POW_WINDOW_LOG
+#define QP_POW_WINDOW_LOG 13
+#endif
+
 namespace {
 
 using gl::ext;
@@ -648,7 +653,7 @@ int prove_batch(qp_prover *P, const uint64_t *const *wires_host, const uint64_t 
     // Minimal witness per proof: every proof still searching scans the same
     // candidate window [base, base + W) per launch; only those proofs are
     // launched (compacted list), so a proof stops costing work as soon as its
-    // window holds a hit.  W = 2^14 keeps the overshoot past the minimal
+    // window holds a hit.  W = 2^13 keeps the overshoot past the minimal
     // witness ~W/2 (vs an expected 2^pow_bits search); when few proofs remain
     // W grows so a launch still covers >= 2^21 candidates (idle CUs otherwise).
     std::vector<uint32_t> active(nb);
@@ -656,7 +661,7 @@ int prove_batch(qp_prover *P, const uint64_t *const *wires_host, const uint64_t 
     uint64_t base = 0;
     while (!active.empty()) {
       const uint32_t na = (uint32_t)active.size();
-      uint64_t window = 1ull << 14;
+      uint64_t window = 1ull << QP_POW_WINDOW_LOG;
       while ((uint64_t)na * window < (1ull << 21)) window <<= 1;
       TRY(hipMemcpyAsync(P->pow_active.p, active.data(), (size_t)na * 4, hipMemcpyHostToDevice, s));
       qpk::k_pow<<<dim3((uint32_t)(window / 256), na), 256, 0, s>>>(
