@@ -9,6 +9,12 @@
 #include "poseidon_dev.h"
 #include "kernels.h"
 
+// trees narrower than 2^QP_MERKLE_FUSE_LOG nodes per level finish in one
+// launch (one wave per block at 6, so no wave idles at the level barriers)
+#ifndef QP_MERKLE_FUSE_LOG
+#define QP_MERKLE_FUSE_LOG 6
+#endif
+
 namespace qpk {
 
 __global__ void __launch_bounds__(256) k_leaf_hash(const uint64_t *__restrict__ cols, uint64_t stride, uint32_t ncols,
@@ -39,20 +45,49 @@ __global__ void __launch_bounds__(256) k_leaf_hash(const uint64_t *__restrict__ 
   o[0] = psd::canon(s[0]); o[1] = psd::canon(s[1]); o[2] = psd::canon(s[2]); o[3] = psd::canon(s[3]);
 }
 
-__global__ void __launch_bounds__(256) k_merkle_level(const uint64_t *__restrict__ prev, uint64_t *__restrict__ next,
-                                                      uint32_t count, uint64_t d_bstride) {
-  const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
-  if (i >= count) return;
-  prev += blockIdx.y * d_bstride;
-  next += blockIdx.y * d_bstride;
-  uint64_t s[12];
-  const uint64_t *l = prev + (uint64_t)i * 8;
+// 1..9 tree levels per launch: a block takes B = min(256, count) nodes of
+// level k0 (their 2B children read from HBM), then folds them level by level
+// through LDS down to one node, writing every level's digests out.  Level k
+// of a tree sits at node offset 2^(log_N+1) - 2^(log_N-k+1) (level 0 = the
+// leaf digests).  The upper levels of a tree are launch-bound (16..256 nodes
+// per proof), so they share one launch.
+__global__ void __launch_bounds__(256) k_merkle_levels(uint64_t *__restrict__ digests, uint32_t log_N, uint32_t k0,
+                                                       uint32_t nl, uint64_t d_bstride) {
+  __shared__ uint64_t sh[256 * 4];
+  digests += blockIdx.y * d_bstride;
+  const uint32_t t = threadIdx.x;
+  const uint32_t cnt = 1u << (log_N - k0);
+  const uint32_t B = cnt < 256u ? cnt : 256u;
+  const uint32_t base = blockIdx.x * B;
+  const uint64_t top = (uint64_t)1 << (log_N + 1);
+  for (uint32_t l = 0; l < nl; l++) {
+    const uint32_t k = k0 + l;
+    const uint32_t nb = B >> l;
+    uint64_t s[12];
+    if (t < nb) {
+      if (l == 0) {
+        const uint64_t *c = digests + (top - ((uint64_t)1 << (log_N - k + 2))) * 4 + (uint64_t)(base + t) * 8;
 #pragma unroll
-  for (int k = 0; k < 8; k++) s[k] = l[k];
-  s[8] = s[9] = s[10] = s[11] = 0;
-  psd::permute_nc(s);
-  uint64_t *o = next + (uint64_t)i * 4;
-  o[0] = psd::canon(s[0]); o[1] = psd::canon(s[1]); o[2] = psd::canon(s[2]); o[3] = psd::canon(s[3]);
+        for (int j = 0; j < 8; j++) s[j] = c[j];
+      } else {
+#pragma unroll
+        for (int j = 0; j < 8; j++) s[j] = sh[t * 8 + j];
+      }
+      s[8] = s[9] = s[10] = s[11] = 0;
+      psd::permute_nc(s);
+#pragma unroll
+      for (int j = 0; j < 4; j++) s[j] = psd::canon(s[j]);
+      uint64_t *o = digests + (top - ((uint64_t)1 << (log_N - k + 1))) * 4 + (uint64_t)((base >> l) + t) * 4;
+#pragma unroll
+      for (int j = 0; j < 4; j++) o[j] = s[j];
+    }
+    __syncthreads();
+    if (t < nb) {
+#pragma unroll
+      for (int j = 0; j < 4; j++) sh[t * 4 + j] = s[j];
+    }
+    __syncthreads();
+  }
 }
 
 void leaf_hash(const uint64_t *cols, uint64_t stride, uint32_t ncols, const uint64_t *salt, uint32_t nsalt,
@@ -64,14 +99,17 @@ void leaf_hash(const uint64_t *cols, uint64_t stride, uint32_t ncols, const uint
 
 void merkle_tree(uint64_t *digests, uint32_t log_N, uint32_t cap_h, uint32_t nbat, uint64_t d_bstride,
                  hipStream_t s) {
-  uint64_t off = 0;
-  for (uint32_t k = 1; k <= log_N - cap_h; k++) {
-    uint32_t count = 1u << (log_N - k);
-    uint64_t *prev = digests + off * 4;
-    off += (uint64_t)1 << (log_N - k + 1);
-    uint64_t *next = digests + off * 4;
-    dim3 grid((count + 255) / 256, nbat);
-    k_merkle_level<<<grid, 256, 0, s>>>(prev, next, count, d_bstride);
+  const uint32_t K = log_N - cap_h;  // levels above the leaves
+  for (uint32_t k0 = 1; k0 <= K;) {
+    const uint32_t lc = log_N - k0;  // log2(nodes at level k0)
+    const uint32_t lb = lc < 8 ? lc : 8;
+    // wide levels one launch each (a fused block would idle all but one
+    // wave through its lower levels: measured 165 -> 222 ms per bench run);
+    // from 2^QP_MERKLE_FUSE_LOG nodes per tree down, the rest of the tree in one launch
+    const uint32_t nl = lc > QP_MERKLE_FUSE_LOG ? 1 : ((lb + 1) < (K - k0 + 1) ? (lb + 1) : (K - k0 + 1));
+    dim3 grid(1u << (lc - lb), nbat);
+    k_merkle_levels<<<grid, 1u << lb, 0, s>>>(digests, log_N, k0, nl, d_bstride);
+    k0 += nl;
   }
 }
 
