@@ -283,14 +283,14 @@ CircuitData CircuitBuilder::build() {
   auto pih = hash_n_to_hash_no_pad(public_inputs_);
   uint32_t pi_row = add_gate(G_PUBLIC_INPUT);
   for (uint32_t i = 0; i < 4; i++) connect(pih[i], Target::wire(pi_row, i));
-  // constant gates: cfg.num_constants constants per ConstantGate row, creation order
+  // constant gates: cfg.num_constants constants per ConstantGate row, in
+  // ascending canonical value (plonky2 build(): constants_to_targets
+  // .sorted_by_key(|(c, _)| c.to_canonical_u64()) zipped with the generators)
   std::vector<std::pair<F, Target>> consts;
-  {
-    std::vector<std::pair<uint32_t, F>> order;
-    for (auto &kv : target_to_const_) order.push_back({kv.first, kv.second});
-    std::sort(order.begin(), order.end());
-    for (auto &o : order) consts.push_back({o.second, Target{o.first}});
-  }
+  for (auto &kv : const_to_target_) consts.push_back({kv.first, kv.second});
+  std::sort(consts.begin(), consts.end(), [](const std::pair<F, Target> &a, const std::pair<F, Target> &b) {
+    return a.first < b.first;
+  });
   const uint32_t ncg = cfg_.num_constants;
   for (size_t i = 0; i < consts.size(); i += ncg) {
     F c0 = consts[i].first, c1 = i + 1 < consts.size() ? consts[i + 1].first : 0;
