@@ -1,13 +1,17 @@
 """bench.py — Wormhole proofs/sec on MI355X (BASELINE.json metric).
 
-One step = prove() of one batch of B synthetic Wormhole witnesses per GPU
-(BASELINE.json configs[2]: "Batch 256 Wormhole proofs on 1xMI355X").  The
-committed wire matrices (the output of WormholeProver::commit's witness
-generation) are resident in HBM before the timed region; each step runs the
-full prover (commitments, permutation argument, quotient, openings, FRI, PoW,
-query openings) and returns serialized proofs to the host.  With N GPUs each
-rank proves its own batch (independent proofs, weak scaling) and the leaf proof
-bytes are gathered to rank 0 over RCCL (the aggregator's input).
+One step = WormholeProver::commit(inputs) + prove() for one batch of B
+synthetic Wormhole CircuitInputs per GPU (BASELINE.json configs[2]: "Batch 256
+Wormhole proofs on 1xMI355X"), end to end: commit() (the fragments'
+fill_targets) on the host threads, witness generation (generate_partial_witness)
+on the device, then the full prover (commitments, permutation argument,
+quotient, openings, FRI, PoW, query openings) and the serialized proofs back on
+the host.  Only the construction of the CircuitInputs themselves (the API's
+input) happens before the timed region.  With N GPUs each rank proves its own
+batch (independent proofs, weak scaling) and the leaf proof bytes are gathered
+to rank 0 over RCCL (the aggregator's input).  --mode wires-dev times prove()
+alone from wire matrices already resident in HBM (round-1 headline, reported as
+prove_only for comparison).
 
 Also reported (one JSON line, rank 0):
   roofline      the wires LDE (NTT) kernel: algorithmic bytes 8*(n+N) per column
@@ -64,19 +68,25 @@ def parse():
                          "one prover's host transcript phases overlap the other's kernels")
     ap.add_argument("--circuit", choices=["wormhole", "voting"], default="wormhole",
                     help="wormhole = BASELINE configs[2] (the headline); voting = configs[4]")
+    ap.add_argument("--mode", choices=["e2e", "wires-dev"], default="e2e",
+                    help="e2e: CircuitInputs -> proofs (headline); wires-dev: prove() from HBM-resident wires")
     ap.add_argument("--cpu-sample", type=int, default=2, help="min proofs in the CPU baseline sample (0 = skip)")
     ap.add_argument("--cpu-seconds", type=float, default=10.0, help="min seconds of CPU baseline proving")
     return ap.parse_args()
 
 
-def make_witnesses(circuit, first, count):
+def make_inputs(circuit, first, count):
     from qp_wormhole.synthetic import synthetic_inputs, synthetic_vote_inputs
     gen = synthetic_vote_inputs if circuit.kind == "voting" else synthetic_inputs
+    return [gen(first + i) for i in range(count)]
+
+
+def make_witnesses(circuit, inputs):
     n, W = circuit.n, circuit.num_wires
-    wires = np.empty((count, W, n), np.uint64)
-    pis = np.empty((count, circuit.num_public_inputs), np.uint64)
-    for i in range(count):
-        w = circuit.commit(gen(first + i))
+    wires = np.empty((len(inputs), W, n), np.uint64)
+    pis = np.empty((len(inputs), circuit.num_public_inputs), np.uint64)
+    for i, x in enumerate(inputs):
+        w = circuit.commit(x)
         wires[i] = w.wires()
         pis[i] = w.public_inputs()
         w.free()
@@ -130,14 +140,20 @@ def main():
     voting = args.circuit == "voting"
     circuit = qp_wormhole.Circuit.voting() if voting else qp_wormhole.Circuit.wormhole(zero_knowledge=False)
     B = args.batch or (1024 if voting else 256)
-    wires, pis = make_witnesses(circuit, rank * B, B)
+    inputs = make_inputs(circuit, rank * B, B)
     NP = max(1, min(args.provers, B))
     per = [B // NP + (1 if i < B % NP else 0) for i in range(NP)]
     first = [sum(per[:i]) for i in range(NP)]
     provers = [qp_wormhole.Prover(qp_wormhole.Context(local), circuit, max_batch=per[i]) for i in range(NP)]
     prover = provers[0]
-    d_wires = torch.from_numpy(wires.view(np.int64)).to(f"cuda:{local}")
-    wstride = wires[0].nbytes
+    # the API input marshalled once into C-ABI structs (CircuitInputs -> qp_wormhole_inputs)
+    cin = [prover.inputs_array(inputs[first[i]:first[i] + per[i]]) for i in range(NP)]
+    # prove-only comparison path: wire matrices resident in HBM (host-generated)
+    wires = pis = d_wires = None
+    if args.mode == "wires-dev" or rank == 0:
+        wires, pis = make_witnesses(circuit, inputs[:max(per[0], 2)] if args.mode == "e2e" else inputs)
+        d_wires = torch.from_numpy(wires.view(np.int64)).to(f"cuda:{local}")
+    wstride = wires[0].nbytes if wires is not None else 0
     torch.cuda.synchronize()
 
     from qp_wormhole.distributed import gather_proofs
@@ -146,8 +162,11 @@ def main():
         out = [None] * NP
 
         def run(i):
-            out[i] = provers[i].prove_wires_dev(d_wires.data_ptr() + first[i] * wstride,
-                                                pis[first[i]:first[i] + per[i]], per[i])
+            if args.mode == "e2e":
+                out[i] = provers[i].prove_inputs_array(cin[i], per[i])
+            else:
+                out[i] = provers[i].prove_wires_dev(d_wires.data_ptr() + first[i] * wstride,
+                                                    pis[first[i]:first[i] + per[i]], per[i])
         if NP == 1:
             run(0)
         else:
@@ -203,16 +222,24 @@ def main():
     iso = None
     if rank == 0 and NP > 1:
         prover.kernel_stats(reset=True)
-        prover.prove_wires_dev(d_wires.data_ptr(), pis[:per[0]], per[0])
+        prover.prove_inputs_array(cin[0], per[0])
         iso = prover.kernel_stats()
+    # prove() alone from HBM-resident wires (round-1 headline definition), one prover
+    prove_only = None
+    if rank == 0 and args.mode == "e2e":
+        prover.set_timing(False)
+        t1 = time.perf_counter()
+        prover.prove_wires_dev(d_wires.data_ptr(), pis[:per[0]], per[0])
+        prove_only = per[0] / (time.perf_counter() - t1)
     # single-proof latency (BASELINE configs[1]): one proof through the same prover
     lat = None
     if rank == 0:
         prover.set_timing(False)
         ts = []
+        one = prover.inputs_array(inputs[:1])
         for _ in range(3):
             t1 = time.perf_counter()
-            prover.prove_wires_dev(d_wires.data_ptr(), pis[:1], 1)
+            prover.prove_inputs_array(one, 1)
             ts.append((time.perf_counter() - t1) * 1e3)
         lat = sorted(ts)[1]
     if rank == 0:
@@ -232,7 +259,10 @@ def main():
             "scaling": "weak",
             "vs_baseline": None,
             "dtype": "u64 (Goldilocks field)",
-            "data": f"synthetic seeded {circuit.kind} witnesses (SURVEY 8d), native circuit, standard_recursion_config",
+            "data": f"synthetic seeded {circuit.kind} circuit inputs (SURVEY 8d), native circuit, "
+                    f"standard_recursion_config; " + ("end to end: commit (host) + witness generation (device) + prove"
+                                                      if args.mode == "e2e" else
+                                                      "prove() from HBM-resident wire matrices"),
             "config": {"workload": f"batch{B}_{circuit.kind}_proofs_per_gpu",
                        "circuit": f"{circuit.kind} deg{circuit.degree_bits} (135 wires)",
                        "batch_per_gpu": B, "provers_per_gpu": NP,
@@ -255,6 +285,7 @@ def main():
             "stage_ms_per_step": {k: v / args.steps for k, v in stages.items()},
             "proof_bytes": len(proofs[0]),
             "latency_1proof_ms": lat,
+            "prove_only_1prover_proofs_per_s": prove_only,
             "warmup_proof_verified": verified,
         }
         if iso is not None and iso["lde_wires"]["ms"]:
@@ -279,6 +310,8 @@ def main():
         rec["stage_ms_per_step"]["note"] = f"prover 0 ({per[0]} proofs), host + device"
         if world == 1 and args.cpu_sample > 0:
             rec["cpu_baseline"] = cpu_baseline(circuit, wires, pis, args.cpu_sample, args.cpu_seconds)
+            rec["cpu_baseline"]["note"] = ("times prove() from host-generated witnesses; commit + witness "
+                                           "generation are not included on the CPU side")
         print(json.dumps(rec), flush=True)
     for p in provers:
         p.free()

@@ -187,6 +187,19 @@ int qp_prover_prove(qp_prover *p, const qp_witness *const *w, uint32_t nproofs, 
 /* prove from raw wire matrices [nproofs][num_wires][n] + public inputs [nproofs][npis] */
 int qp_prover_prove_wires(qp_prover *p, const uint64_t *wires, const uint64_t *pis, uint32_t nproofs, uint8_t *out,
                           size_t stride, size_t *lens);
+/* End to end: WormholeProver::commit(inputs) + prove() (wormhole/prover/src/lib.rs:
+ * 209-237) for a batch of CircuitInputs.  commit() (the fragments' fill_targets)
+ * runs on the host thread pool; generate_partial_witness (plonky2
+ * iop/generator.rs: Poseidon, BaseSum, arithmetic, equality and constant
+ * generators) runs on the device, one workgroup per proof, level by level;
+ * then the proof.  A witness conflict returns QP_ERR_WITNESS with the
+ * reference's "set twice with different values" message naming the proof. */
+int qp_prover_prove_wormhole_inputs(qp_prover *p, const qp_wormhole_inputs *in, uint32_t nproofs, uint8_t *out,
+                                    size_t stride, size_t *lens);
+/* the same for the voting circuit: VoteCircuitData::fill_targets + prove
+ * (voting/src/lib.rs:199-261, :346-357)                                     */
+int qp_prover_prove_voting_inputs(qp_prover *p, const qp_voting_inputs *in, uint32_t nproofs, uint8_t *out,
+                                  size_t stride, size_t *lens);
 /* same, with the wire matrices already resident on the device:
  * d_wires = device pointer [nproofs][num_wires][n]; pis on the host          */
 int qp_prover_prove_wires_dev(qp_prover *p, const uint64_t *d_wires, const uint64_t *pis, uint32_t nproofs,
@@ -197,8 +210,9 @@ int qp_prover_prove_wires_dev(qp_prover *p, const uint64_t *d_wires, const uint6
  * (units = permutations), 3 = quotient evaluation (units = LDE points)     */
 int qp_prover_set_timing(qp_prover *p, int enable);
 int qp_prover_kernel_stats(qp_prover *p, double *ms, double *units, uint64_t *launches, uint32_t n, int reset);
-/* accumulated host wall time per stage (ms): commit wires, zs, quotient, openings,
- * FRI, PoW, queries, serialize; reset != 0 clears */
+/* accumulated host wall time per stage (ms): [0] commit wires, [1] zs, [2] quotient,
+ * [3] openings, [4] FRI, [5] PoW, [6] queries, [7] serialize, [8] commit() of the
+ * inputs (host), [9] device witness generation; reset != 0 clears */
 int qp_prover_stage_times(qp_prover *p, double *ms, uint32_t n, int reset);
 
 #ifdef __cplusplus

@@ -12,6 +12,7 @@
 #include <algorithm>
 #include <numeric>
 #include <stdexcept>
+#include <string.h>
 #include "field.h"
 #include "poseidon.h"
 
@@ -373,22 +374,20 @@ CircuitData CircuitBuilder::build() {
   auto tindex = [&](Target t) -> uint32_t { return t.is_virtual() ? (uint32_t)(nwires + (t.v & ~Target::VIRT)) : t.row() * W + t.col(); };
   UF uf(nwires + nvirt_);
   for (auto &cp : copies_) uf.unite(tindex(cp.first), tindex(cp.second));
-  std::vector<uint32_t> slot_of_rep(nwires + nvirt_, 0xFFFFFFFFu);
-  uint32_t nslots = 0;
-  std::vector<uint32_t> slot(nwires + nvirt_);
+  // partition id per target (dense, in target-index order of first member)
+  std::vector<uint32_t> part_of_rep(nwires + nvirt_, 0xFFFFFFFFu);
+  uint32_t nparts = 0;
+  std::vector<uint32_t> part(nwires + nvirt_);
   for (size_t i = 0; i < nwires + nvirt_; i++) {
     uint32_t r = uf.find((uint32_t)i);
-    if (slot_of_rep[r] == 0xFFFFFFFFu) slot_of_rep[r] = nslots++;
-    slot[i] = slot_of_rep[r];
+    if (part_of_rep[r] == 0xFFFFFFFFu) part_of_rep[r] = nparts++;
+    part[i] = part_of_rep[r];
   }
-  cd.num_slots = nslots;
-  cd.wire_slot.assign(slot.begin(), slot.begin() + nwires);
-  for (uint32_t v = 0; v < nvirt_; v++) cd.target_slot_virtual[v] = slot[nwires + v];
   // ---- sigma polynomials: each partition's routed wires form a cycle
   {
-    std::vector<std::vector<uint32_t>> members(nslots);
+    std::vector<std::vector<uint32_t>> members(nparts);
     for (uint32_t row = 0; row < n; row++)
-      for (uint32_t col = 0; col < R; col++) members[slot[row * W + col]].push_back(row * W + col);
+      for (uint32_t col = 0; col < R; col++) members[part[row * W + col]].push_back(row * W + col);
     const uint64_t w = gl::root_of_unity(cd.degree_bits);
     std::vector<F> wpow(n);
     wpow[0] = 1;
@@ -413,41 +412,56 @@ CircuitData CircuitBuilder::build() {
       if (max_gate_consts >= 2) cd.constants_sigmas[(size_t)(nsel + 1) * n + row] = gi.c1;
     }
   }
-  // ---- generator schedule (worklist over partition slots)
+  // ---- generator schedule (worklist over partitions) + compact value slots
   {
-    auto sl = [&](Target t) { return slot[tindex(t)]; };
-    auto wsl = [&](uint32_t row, uint32_t col) { return slot[row * W + col]; };
+    auto pt = [&](Target t) { return part[tindex(t)]; };
+    auto wpt = [&](uint32_t row, uint32_t col) { return part[row * W + col]; };
     std::vector<std::vector<uint32_t>> gin(gens_.size()), gout(gens_.size());
     for (size_t gi = 0; gi < gens_.size(); gi++) {
       const Gen &g = gens_[gi];
       switch (g.kind) {
         case GEN_CONSTANT:
-          for (uint32_t j = 0; j < ncg; j++) gout[gi].push_back(wsl(g.row, j));
+          for (uint32_t j = 0; j < ncg; j++) gout[gi].push_back(wpt(g.row, j));
           break;
         case GEN_ARITH:
-          for (uint32_t j = 0; j < 3; j++) gin[gi].push_back(wsl(g.row, 4 * g.op + j));
-          gout[gi].push_back(wsl(g.row, 4 * g.op + 3));
+          for (uint32_t j = 0; j < 3; j++) gin[gi].push_back(wpt(g.row, 4 * g.op + j));
+          gout[gi].push_back(wpt(g.row, 4 * g.op + 3));
           break;
         case GEN_POSEIDON:
-          for (uint32_t j = 0; j < 12; j++) gin[gi].push_back(wsl(g.row, j));
-          gin[gi].push_back(wsl(g.row, 24));
+          for (uint32_t j = 0; j < 12; j++) gin[gi].push_back(wpt(g.row, j));
+          gin[gi].push_back(wpt(g.row, 24));
           for (uint32_t j = 12; j < W; j++)
-            if (j != 24) gout[gi].push_back(wsl(g.row, j));
+            if (j != 24) gout[gi].push_back(wpt(g.row, j));
           break;
         case GEN_BASE_SPLIT:
-          gin[gi].push_back(wsl(g.row, 0));
-          for (uint32_t j = 1; j <= base_sum_limbs_; j++) gout[gi].push_back(wsl(g.row, j));
+          gin[gi].push_back(wpt(g.row, 0));
+          for (uint32_t j = 1; j <= base_sum_limbs_; j++) gout[gi].push_back(wpt(g.row, j));
           break;
         case GEN_EQUALITY:
-          gin[gi].push_back(sl(g.a));
-          gin[gi].push_back(sl(g.b));
-          gout[gi].push_back(sl(g.c));
-          gout[gi].push_back(sl(g.d));
+          gin[gi].push_back(pt(g.a));
+          gin[gi].push_back(pt(g.b));
+          gout[gi].push_back(pt(g.c));
+          gout[gi].push_back(pt(g.d));
           break;
       }
       std::sort(gin[gi].begin(), gin[gi].end());
       gin[gi].erase(std::unique(gin[gi].begin(), gin[gi].end()), gin[gi].end());
     }
+    // value slots: only partitions some generator or input sets; slot 0 is the
+    // never-set zero slot shared by everything else
+    std::vector<uint32_t> sid(nparts, 0);
+    uint32_t nslots = 1;
+    auto take = [&](uint32_t p) {
+      if (!sid[p]) sid[p] = nslots++;
+    };
+    for (Target t : inputs_) take(pt(t));
+    for (auto &o : gout)
+      for (uint32_t p : o) take(p);
+    cd.num_slots = nslots;
+    for (auto &v : gin)
+      for (auto &p : v) p = sid[p];
+    for (auto &v : gout)
+      for (auto &p : v) p = sid[p];
     std::vector<std::vector<uint32_t>> watchers(nslots);
     std::vector<uint32_t> remaining(gens_.size());
     for (size_t gi = 0; gi < gens_.size(); gi++) {
@@ -457,12 +471,12 @@ CircuitData CircuitBuilder::build() {
     std::vector<uint8_t> known(nslots, 0);
     std::vector<uint32_t> queue;
     auto mark = [&](uint32_t s) {
-      if (!known[s]) {
+      if (s && !known[s]) {
         known[s] = 1;
         queue.push_back(s);
       }
     };
-    for (Target t : inputs_) mark(sl(t));
+    for (Target t : inputs_) mark(sid[pt(t)]);
     std::vector<uint32_t> ready;
     for (size_t gi = 0; gi < gens_.size(); gi++)
       if (!remaining[gi]) ready.push_back((uint32_t)gi);
@@ -482,15 +496,117 @@ CircuitData CircuitBuilder::build() {
     if (cd.schedule.size() != gens_.size())
       throw std::runtime_error("witness generation cannot be scheduled: " +
                                std::to_string(gens_.size() - cd.schedule.size()) + " generators never become ready");
-    for (Target t : public_inputs_) cd.pi_slots.push_back(sl(t));
+    cd.wire_slot.resize(nwires);
+    cd.wire_slot_cm.resize(nwires);
+    for (uint32_t row = 0; row < n; row++)
+      for (uint32_t col = 0; col < W; col++) {
+        const uint32_t s = sid[part[(size_t)row * W + col]];
+        cd.wire_slot[(size_t)row * W + col] = s;
+        cd.wire_slot_cm[(size_t)col * n + row] = s;
+      }
+    cd.virt_slot.resize(nvirt_);
+    for (uint32_t v = 0; v < nvirt_; v++) cd.virt_slot[v] = sid[part[nwires + v]];
+    {
+      auto z = const_to_target_.find(0);
+      cd.zero_const_slot = z == const_to_target_.end() ? 0 : sid[pt(z->second)];
+    }
+    for (Gen &g : cd.schedule) {
+      auto ws = [&](uint32_t row, uint32_t col) { return sid[wpt(row, col)]; };
+      switch (g.kind) {
+        case GEN_ARITH:
+          for (uint32_t j = 0; j < 4; j++) g.s[j] = ws(g.row, 4 * g.op + j);
+          g.k0 = rows_[g.row].c0;
+          g.k1 = rows_[g.row].c1;
+          break;
+        case GEN_EQUALITY:
+          g.s[0] = sid[pt(g.a)];
+          g.s[1] = sid[pt(g.b)];
+          g.s[2] = sid[pt(g.c)];
+          g.s[3] = sid[pt(g.d)];
+          break;
+        case GEN_CONSTANT:
+          g.s[0] = ws(g.row, 0);
+          g.s[1] = ncg > 1 ? ws(g.row, 1) : 0;
+          g.k0 = rows_[g.row].c0;
+          g.k1 = rows_[g.row].c1;
+          break;
+        case GEN_BASE_SPLIT:
+          g.s[0] = ws(g.row, 0);
+          break;
+        default:
+          break;
+      }
+    }
+    for (Target t : public_inputs_) cd.pi_slots.push_back(sid[pt(t)]);
+    // device schedule: a generator runs at the first level where all its
+    // inputs exist; its outputs exist from the next level on
+    {
+      std::vector<uint8_t> is_in(nslots, 0);
+      for (Target t : inputs_) {
+        const uint32_t s = sid[pt(t)];
+        if (s && !is_in[s]) {
+          is_in[s] = 1;
+          cd.input_slots.push_back(s);
+        }
+      }
+      std::sort(cd.input_slots.begin(), cd.input_slots.end());
+      const uint32_t INF = 0xFFFFFFFFu;
+      std::vector<uint32_t> avail(nslots, INF);
+      avail[0] = 0;
+      for (uint32_t s : cd.input_slots) avail[s] = 0;
+      std::vector<uint32_t> lvl(cd.schedule.size());
+      uint32_t nlev = 0;
+      for (size_t i = 0; i < cd.schedule.size(); i++) {
+        const Gen &g = cd.schedule[i];
+        std::vector<uint32_t> rd, wr;
+        switch (g.kind) {
+          case GEN_CONSTANT: wr = {g.s[0], g.s[1]}; break;
+          case GEN_ARITH: rd = {g.s[0], g.s[1], g.s[2]}; wr = {g.s[3]}; break;
+          case GEN_EQUALITY: rd = {g.s[0], g.s[1]}; wr = {g.s[2], g.s[3]}; break;
+          case GEN_BASE_SPLIT:
+            rd = {g.s[0]};
+            for (uint32_t j = 1; j <= base_sum_limbs_; j++) wr.push_back(cd.wire_slot[(size_t)g.row * W + j]);
+            break;
+          case GEN_POSEIDON:
+            for (uint32_t j = 0; j < 12; j++) rd.push_back(cd.wire_slot[(size_t)g.row * W + j]);
+            rd.push_back(cd.wire_slot[(size_t)g.row * W + 24]);
+            for (uint32_t j = 12; j < W; j++)
+              if (j != 24) wr.push_back(cd.wire_slot[(size_t)g.row * W + j]);
+            break;
+        }
+        uint32_t l = 0;
+        for (uint32_t s : rd) {
+          if (avail[s] == INF) throw std::runtime_error("device witness schedule: input not available");
+          l = std::max(l, avail[s]);
+        }
+        lvl[i] = l;
+        nlev = std::max(nlev, l + 1);
+        for (uint32_t s : wr)
+          if (s) avail[s] = std::min(avail[s], l + 1);
+      }
+      cd.level_off.assign(nlev + 1, 0);
+      for (uint32_t l : lvl) cd.level_off[l + 1]++;
+      for (uint32_t l = 0; l < nlev; l++) cd.level_off[l + 1] += cd.level_off[l];
+      std::vector<uint32_t> fill(cd.level_off.begin(), cd.level_off.end() - 1);
+      cd.dev_gens.resize(cd.schedule.size());
+      for (size_t i = 0; i < cd.schedule.size(); i++) {
+        const Gen &g = cd.schedule[i];
+        DevGen &d = cd.dev_gens[fill[lvl[i]]++];
+        d.kind = g.kind;
+        d.row = g.row;
+        for (int j = 0; j < 4; j++) d.s[j] = g.s[j];
+        d.k0 = g.k0;
+        d.k1 = g.k1;
+      }
+    }
   }
   return cd;
 }
 
 uint32_t CircuitData::slot_of(Target t) const {
   if (t.is_virtual()) {
-    auto it = target_slot_virtual.find(t.v & ~Target::VIRT);
-    return it == target_slot_virtual.end() ? 0xFFFFFFFFu : it->second;
+    const uint32_t v = t.v & ~Target::VIRT;
+    return v < virt_slot.size() ? virt_slot[v] : 0xFFFFFFFFu;
   }
   return wire_slot[(size_t)t.row() * config.num_wires + t.col()];
 }
@@ -535,7 +651,10 @@ std::vector<uint8_t> CircuitData::common_bytes() const {
   w.u64(fri_arity_bits.size());
   for (auto a : fri_arity_bits) w.u64(a);
   w.u64(degree_bits);
-  w.u8(c.zero_knowledge);  // FriParams.hiding
+  // FriParams.hiding: the reference's zk config under the workspace's
+  // `no_random` feature commits without salt columns (dummy_proof_zk.bin,
+  // verified in tests/test_current_circuit_fixture.py), i.e. no hiding
+  w.u8(0);
   w.u64(selector_indices.size());
   for (auto s : selector_indices) w.u64(s);
   w.u64(groups.size());
@@ -564,19 +683,31 @@ std::vector<uint8_t> CircuitData::common_bytes() const {
 
 // ---------------------------------------------------------------- witness
 
-Witness::Witness(const CircuitData &cd) : cd_(cd), val_(cd.num_slots, 0), known_(cd.num_slots, 0) {}
+Witness::Witness(const CircuitData &cd, F *vals) : cd_(cd), known_(cd.num_slots, 0) {
+  if (vals) {
+    vals_ = vals;
+    memset(vals_, 0, (size_t)cd.num_slots * 8);
+  } else {
+    own_.assign(cd.num_slots, 0);
+    vals_ = own_.data();
+  }
+}
 
 bool Witness::set_slot(uint32_t s, F v) {
   v = gl::canon(v);
+  if (!s) {  // the shared zero slot is never settable
+    conflict_ = true;
+    return false;
+  }
   if (known_[s]) {
-    if (val_[s] != v) {
+    if (vals_[s] != v) {
       conflict_ = true;
       return false;
     }
     return true;
   }
   known_[s] = 1;
-  val_[s] = v;
+  vals_[s] = v;
   return true;
 }
 
@@ -591,64 +722,129 @@ bool Witness::set_wire(uint32_t row, uint32_t col, F v) {
 }
 
 F Witness::wire(uint32_t row, uint32_t col) const {
-  return val_[cd_.wire_slot[(size_t)row * cd_.config.num_wires + col]];
+  return vals_[cd_.wire_slot[(size_t)row * cd_.config.num_wires + col]];
 }
 
+namespace {
+
+inline F red128(unsigned __int128 x) { return gl::reduce128((uint64_t)x, (uint64_t)(x >> 64)); }
+
+// x^7 on the host (64x64->128 products)
+inline F sbox_h(F x) {
+  const F x2 = red128((unsigned __int128)x * x);
+  const F x3 = red128((unsigned __int128)x2 * x);
+  const F x4 = red128((unsigned __int128)x2 * x2);
+  return red128((unsigned __int128)x3 * x4);
+}
+
+constexpr uint64_t MDS_C[12] = {17, 15, 41, 16, 2, 28, 13, 13, 39, 18, 34, 20};
+
+// MDS layer with the small circulant constants, one 128-bit accumulation and
+// one reduction per lane (each term < 2^70, 13 terms < 2^74)
+inline void mds_h(F s[12]) {
+  F o[12];
+#pragma unroll
+  for (int r = 0; r < 12; r++) {
+    unsigned __int128 acc = 0;
+#pragma unroll
+    for (int i = 0; i < 12; i++) acc += (unsigned __int128)s[(i + r) % 12] * MDS_C[i];
+    if (r == 0) acc += (unsigned __int128)s[0] * 8;
+    o[r] = red128(acc);
+  }
+#pragma unroll
+  for (int r = 0; r < 12; r++) s[r] = o[r];
+}
+
+// inverses of the small integers 1..SMALL_INV: EqualityGenerator inverts
+// x - y, which in the reference circuits is mostly a short index distance
+constexpr uint32_t SMALL_INV = 4096;
+const F *small_inverses() {
+  static const std::vector<F> t = [] {
+    std::vector<F> v(SMALL_INV + 1, 0);
+    v[1] = 1;
+    for (uint32_t k = 2; k <= SMALL_INV; k++)  // inv(k) = -(p / k) * inv(p mod k)
+      v[k] = gl::neg(gl::mul(gl::P / k, v[gl::P % k]));
+    return v;
+  }();
+  return t.data();
+}
+
+inline F inv_diff(F x, F y) {
+  if (x >= y) {
+    const F d = x - y;
+    return d <= SMALL_INV ? small_inverses()[d] : gl::inv(d);
+  }
+  const F d = y - x;
+  return d <= SMALL_INV ? gl::neg(small_inverses()[d]) : gl::inv(gl::sub(x, y));
+}
+
+}  // namespace
+
 bool Witness::generate(std::string &err) {
-  const uint32_t ncg = cd_.config.num_constants;
+  const uint32_t W = cd_.config.num_wires;
+  const uint32_t L = cd_.config.num_routed_wires - 1 < 63 ? cd_.config.num_routed_wires - 1 : 63;
+  const uint32_t zslot = cd_.zero_const_slot;
+  F *v = vals_;
   for (const Gen &g : cd_.schedule) {
     bool ok = true;
     switch (g.kind) {
-      case GEN_CONSTANT: {
-        const GateInst &gi = cd_.rows[g.row];
-        ok = set_wire(g.row, 0, gi.c0) && (ncg < 2 || set_wire(g.row, 1, gi.c1));
+      case GEN_CONSTANT:
+        ok = set_slot(g.s[0], g.k0) && (cd_.config.num_constants < 2 || set_slot(g.s[1], g.k1));
         break;
-      }
       case GEN_ARITH: {
-        const GateInst &gi = cd_.rows[g.row];
-        F m0 = wire(g.row, 4 * g.op), m1 = wire(g.row, 4 * g.op + 1), a = wire(g.row, 4 * g.op + 2);
-        ok = set_wire(g.row, 4 * g.op + 3, gl::add(gl::mul(gl::mul(m0, m1), gi.c0), gl::mul(a, gi.c1)));
+        // output = c0 * m0 * m1 + c1 * addend
+        const F m = gl::mul(gl::mul(v[g.s[0]], v[g.s[1]]), g.k0);
+        ok = set_slot(g.s[3], gl::add(m, gl::mul(v[g.s[2]], g.k1)));
         break;
       }
       case GEN_BASE_SPLIT: {
-        F sum = wire(g.row, 0);
-        const uint32_t L = cd_.config.num_routed_wires - 1 < 63 ? cd_.config.num_routed_wires - 1 : 63;
-        for (uint32_t l = 0; l < L && ok; l++) ok = set_wire(g.row, 1 + l, (sum >> l) & 1);
+        const F sum = v[g.s[0]];
+        const uint32_t *ws = cd_.wire_slot.data() + (size_t)g.row * W + 1;
+        for (uint32_t l = 0; l < L && ok; l++) {
+          const F bit = (sum >> l) & 1;
+          // limbs past a range check's width are connected to zero(): they
+          // only need checking (a set bit there is the reference's conflict)
+          if (ws[l] == zslot && zslot) ok = bit == 0;
+          else ok = set_slot(ws[l], bit);
+        }
         break;
       }
       case GEN_EQUALITY: {
-        F x = val_[cd_.slot_of(g.a)], y = val_[cd_.slot_of(g.b)];
-        ok = set(g.c, x == y ? 1 : 0) && set(g.d, x == y ? 0 : gl::inv(gl::sub(x, y)));
+        const F x = v[g.s[0]], y = v[g.s[1]];
+        ok = set_slot(g.s[2], x == y ? 1 : 0) && set_slot(g.s[3], x == y ? 0 : inv_diff(x, y));
         break;
       }
       case GEN_POSEIDON: {
+        // PoseidonGenerator (gates/poseidon.rs): swap, deltas, S-box inputs
+        // of full rounds 1..3, partial rounds, second-half full rounds, outputs
+        const uint32_t *ws = cd_.wire_slot.data() + (size_t)g.row * W;
         F s[12];
-        for (int i = 0; i < 12; i++) s[i] = wire(g.row, i);
-        F swap = wire(g.row, 24);
-        for (int i = 0; i < 4 && ok; i++) ok = set_wire(g.row, 25 + i, gl::mul(swap, gl::sub(s[i + 4], s[i])));
+        for (int i = 0; i < 12; i++) s[i] = v[ws[i]];
+        const F swap = v[ws[24]];
+        for (int i = 0; i < 4 && ok; i++) ok = set_slot(ws[25 + i], gl::mul(swap, gl::sub(s[i + 4], s[i])));
         if (swap == 1)
           for (int i = 0; i < 4; i++) std::swap(s[i], s[i + 4]);
         int rc = 0;
         for (int r = 0; r < 4; r++, rc++) {
           for (int i = 0; i < 12; i++) s[i] = gl::add(s[i], ps::rc(rc * 12 + i));
           if (r)
-            for (int i = 0; i < 12 && ok; i++) ok = set_wire(g.row, 29 + (r - 1) * 12 + i, s[i]);
-          for (int i = 0; i < 12; i++) s[i] = ps::sbox(s[i]);
-          ps::mds(s);
+            for (int i = 0; i < 12 && ok; i++) ok = set_slot(ws[29 + (r - 1) * 12 + i], s[i]);
+          for (int i = 0; i < 12; i++) s[i] = sbox_h(s[i]);
+          mds_h(s);
         }
         for (int r = 0; r < 22; r++, rc++) {
           for (int i = 0; i < 12; i++) s[i] = gl::add(s[i], ps::rc(rc * 12 + i));
-          if (ok) ok = set_wire(g.row, 65 + r, s[0]);
-          s[0] = ps::sbox(s[0]);
-          ps::mds(s);
+          if (ok) ok = set_slot(ws[65 + r], s[0]);
+          s[0] = sbox_h(s[0]);
+          mds_h(s);
         }
         for (int r = 0; r < 4; r++, rc++) {
           for (int i = 0; i < 12; i++) s[i] = gl::add(s[i], ps::rc(rc * 12 + i));
-          for (int i = 0; i < 12 && ok; i++) ok = set_wire(g.row, 87 + r * 12 + i, s[i]);
-          for (int i = 0; i < 12; i++) s[i] = ps::sbox(s[i]);
-          ps::mds(s);
+          for (int i = 0; i < 12 && ok; i++) ok = set_slot(ws[87 + r * 12 + i], s[i]);
+          for (int i = 0; i < 12; i++) s[i] = sbox_h(s[i]);
+          mds_h(s);
         }
-        for (int i = 0; i < 12 && ok; i++) ok = set_wire(g.row, 12 + i, s[i]);
+        for (int i = 0; i < 12 && ok; i++) ok = set_slot(ws[12 + i], s[i]);
         break;
       }
     }
@@ -662,19 +858,14 @@ bool Witness::generate(std::string &err) {
 }
 
 void Witness::wires_matrix(F *out) const {
-  const uint32_t n = cd_.n, W = cd_.config.num_wires;
-  for (uint32_t row = 0; row < n; row++) {
-    const uint32_t *ws = cd_.wire_slot.data() + (size_t)row * W;
-    for (uint32_t col = 0; col < W; col++) {
-      uint32_t s = ws[col];
-      out[(size_t)col * n + row] = known_[s] ? val_[s] : 0;
-    }
-  }
+  const size_t m = (size_t)cd_.n * cd_.config.num_wires;
+  const uint32_t *cm = cd_.wire_slot_cm.data();
+  for (size_t i = 0; i < m; i++) out[i] = vals_[cm[i]];
 }
 
 std::vector<F> Witness::public_inputs() const {
   std::vector<F> v;
-  for (uint32_t s : cd_.pi_slots) v.push_back(val_[s]);
+  for (uint32_t s : cd_.pi_slots) v.push_back(vals_[s]);
   return v;
 }
 

@@ -78,7 +78,23 @@ struct Gen {
   GenKind kind;
   uint32_t row = 0, op = 0;             // gate row / arithmetic op index
   Target a, b, c, d;                    // EQUALITY: x, y, equal, inv
+  // resolved at build(): value slots the generator reads/writes
+  //   ARITH: m0, m1, addend, output   EQUALITY: x, y, equal, inv
+  //   CONSTANT: wire 0, wire 1         BASE_SPLIT: sum
+  uint32_t s[4] = {0, 0, 0, 0};
+  F k0 = 0, k1 = 0;                     // ARITH / CONSTANT gate constants
 };
+
+// Device witness generation (plonky2 iop/generator.rs generate_partial_witness
+// on the GPU): one record per generator, grouped into dependency levels so a
+// workgroup can run one proof's generators level by level (same layout as the
+// device struct in witness.hip).
+struct DevGen {
+  uint32_t kind, row;
+  uint32_t s[4];
+  uint64_t k0, k1;
+};
+static_assert(sizeof(DevGen) == 40, "DevGen layout");
 
 // everything the prover needs about a built circuit (plonky2 ProverCircuitData
 // + CommonCircuitData), kept in host memory
@@ -97,12 +113,19 @@ struct CircuitData {
   // preprocessed polynomials, column-major values over H (natural row order)
   std::vector<F> constants_sigmas;      // [num_constants + num_routed][n]
   std::vector<GateInst> rows;
-  // witness layout
+  // witness layout: one value slot per copy-constraint partition that some
+  // generator or input sets; slot 0 is the shared never-set (zero) slot of
+  // every other wire (padding rows, unused gate slots, unrouted leftovers)
   uint32_t num_slots = 0;
-  std::vector<uint32_t> wire_slot;      // [n * num_wires] row-major: slot of wire (row, col) or ~0u
+  std::vector<uint32_t> wire_slot;      // [n * num_wires] row-major: slot of wire (row, col)
+  std::vector<uint32_t> wire_slot_cm;   // [num_wires * n] column-major (wire-matrix expansion)
   std::vector<Gen> schedule;            // generators in dependency order
   std::vector<uint32_t> pi_slots;       // public input slots (in order)
-  std::map<uint32_t, uint32_t> target_slot_virtual;  // virtual target -> slot
+  std::vector<uint32_t> virt_slot;      // virtual target index -> slot
+  uint32_t zero_const_slot = 0;         // slot of builder.zero() (0 if the circuit has none)
+  std::vector<uint32_t> input_slots;    // distinct slots of the targets commit() sets
+  std::vector<DevGen> dev_gens;         // generators ordered by dependency level
+  std::vector<uint32_t> level_off;      // [levels + 1] offsets into dev_gens
   // commitments (filled by the prover backend at setup)
   F constants_sigmas_cap[64 * 4] = {0};
   F circuit_digest[4] = {0};
@@ -196,14 +219,20 @@ Target is_const_less_than(CircuitBuilder &b, uint32_t left, Target right, uint32
 // Per-proof witness: values per partition slot.
 class Witness {
  public:
-  explicit Witness(const CircuitData &cd);
+  // vals: optional caller-owned storage of cd.num_slots words (e.g. a pinned
+  // staging buffer the prover uploads directly); zeroed here
+  explicit Witness(const CircuitData &cd, F *vals = nullptr);
+  Witness(const Witness &) = delete;
+  Witness &operator=(const Witness &) = delete;
   // PartialWitness::set_target; returns false on "set twice with different values"
   bool set(Target t, F v);
   bool set_slot(uint32_t s, F v);
   bool get_slot(uint32_t s, F &v) const {
-    v = val_[s];
+    v = vals_[s];
     return known_[s];
   }
+  // slot values [num_slots] (slot 0 = 0): wire (r, c) = slot_values()[wire_slot[r * W + c]]
+  const F *slot_values() const { return vals_; }
   // run the generator schedule; returns false (and a message) on conflict / missing input
   bool generate(std::string &err);
   // full wire matrix, column-major [num_wires][n]
@@ -214,9 +243,9 @@ class Witness {
   bool set_wire(uint32_t row, uint32_t col, F v);
   F wire(uint32_t row, uint32_t col) const;
   const CircuitData &cd_;
-  std::vector<F> val_;
+  std::vector<F> own_;
+  F *vals_;
   std::vector<uint8_t> known_;
-  std::vector<F> nonrouted_;  // values of wires that are not in any slot
   bool conflict_ = false;
 };
 

@@ -9,6 +9,51 @@
 #include "circuit_obj.h"
 #include "host_util.h"
 
+std::string wormhole_fill(const qp_circuit *c, const void *vin, qc::Witness &w, int *code) {
+  const qp_wormhole_inputs *in = (const qp_wormhole_inputs *)vin;
+  *code = QP_ERR_ARG;
+  if (!c || !in || c->kind != qp_circuit::WORMHOLE) return "not a Wormhole circuit / null inputs";
+  if (in->num_nodes && (!in->nodes || !in->node_lens || !in->indices)) return "null storage-proof arrays";
+  qw::CircuitInputs ci;
+  memcpy(&ci.funding_amount_lo, in->funding_amount, 8);
+  memcpy(&ci.funding_amount_hi, in->funding_amount + 8, 8);
+  memcpy(ci.nullifier, in->nullifier, 32);
+  memcpy(ci.root_hash, in->root_hash, 32);
+  memcpy(ci.exit_account, in->exit_account, 32);
+  memcpy(ci.secret, in->secret, 32);
+  ci.transfer_count = in->transfer_count;
+  memcpy(ci.funding_account, in->funding_account, 32);
+  memcpy(ci.unspendable_account, in->unspendable_account, 32);
+  for (uint32_t i = 0; i < in->num_nodes; i++) {
+    ci.storage_proof.emplace_back(in->nodes[i], in->nodes[i] + in->node_lens[i]);
+    ci.storage_indices.push_back(in->indices[i]);
+  }
+  std::string e = qw::commit(c->wormhole, ci, w);
+  *code = e.empty() ? QP_OK : e.find("set twice") != std::string::npos ? QP_ERR_WITNESS : QP_ERR_ARG;
+  return e;
+}
+
+std::string voting_fill(const qp_circuit *c, const void *vin, qc::Witness &w, int *code) {
+  const qp_voting_inputs *in = (const qp_voting_inputs *)vin;
+  *code = QP_ERR_ARG;
+  if (!c || !in || c->kind != qp_circuit::VOTING) return "not a voting circuit / null inputs";
+  if ((in->num_siblings && !in->siblings) || (in->num_path_indices && !in->path_indices)) return "null arrays";
+  qv::VoteInputs vi;
+  memcpy(vi.proposal_id, in->proposal_id, 32);
+  memcpy(vi.merkle_root, in->merkle_root, 32);
+  memcpy(vi.nullifier, in->nullifier, 32);
+  vi.vote = in->vote != 0;
+  memcpy(vi.private_key, in->private_key, 32);
+  for (uint32_t i = 0; i < in->num_siblings; i++)
+    vi.merkle_siblings.push_back({in->siblings[4 * i], in->siblings[4 * i + 1], in->siblings[4 * i + 2],
+                                  in->siblings[4 * i + 3]});
+  for (uint32_t i = 0; i < in->num_path_indices; i++) vi.path_indices.push_back(in->path_indices[i] != 0);
+  vi.actual_merkle_depth = in->actual_merkle_depth;
+  std::string e = qv::fill_targets(c->voting, vi, w);
+  *code = e.empty() ? QP_OK : QP_ERR_ARG;
+  return e;
+}
+
 extern "C" {
 
 int qp_wormhole_circuit_new(int zk, qp_circuit **out) {
@@ -93,29 +138,14 @@ static void put_err(char *err, size_t cap, const std::string &m) {
 int qp_wormhole_commit(const qp_circuit *c, const qp_wormhole_inputs *in, qp_witness **out, char *err, size_t errcap) {
   if (!c || !in || !out || c->kind != qp_circuit::WORMHOLE) return QP_ERR_ARG;
   *out = nullptr;
-  if (in->num_nodes && (!in->nodes || !in->node_lens || !in->indices)) return QP_ERR_ARG;
   try {
-    qw::CircuitInputs ci;
-    memcpy(&ci.funding_amount_lo, in->funding_amount, 8);
-    memcpy(&ci.funding_amount_hi, in->funding_amount + 8, 8);
-    memcpy(ci.nullifier, in->nullifier, 32);
-    memcpy(ci.root_hash, in->root_hash, 32);
-    memcpy(ci.exit_account, in->exit_account, 32);
-    memcpy(ci.secret, in->secret, 32);
-    ci.transfer_count = in->transfer_count;
-    memcpy(ci.funding_account, in->funding_account, 32);
-    memcpy(ci.unspendable_account, in->unspendable_account, 32);
-    for (uint32_t i = 0; i < in->num_nodes; i++) {
-      ci.storage_proof.emplace_back(in->nodes[i], in->nodes[i] + in->node_lens[i]);
-      ci.storage_indices.push_back(in->indices[i]);
-    }
     auto w = std::make_unique<qp_witness>(c);
-    std::string e = qw::commit(c->wormhole, ci, w->w);
-    if (e.empty() && !w->w.generate(e)) {
-    }
+    int code = QP_OK;
+    std::string e = wormhole_fill(c, in, w->w, &code);
+    if (e.empty() && !w->w.generate(e)) code = QP_ERR_WITNESS;
     if (!e.empty()) {
       put_err(err, errcap, e);
-      return e.find("set twice") != std::string::npos ? QP_ERR_WITNESS : QP_ERR_ARG;
+      return code ? code : QP_ERR_ARG;
     }
     *out = w.release();
     return QP_OK;
@@ -127,28 +157,14 @@ int qp_wormhole_commit(const qp_circuit *c, const qp_wormhole_inputs *in, qp_wit
 int qp_voting_commit(const qp_circuit *c, const qp_voting_inputs *in, qp_witness **out, char *err, size_t errcap) {
   if (!c || !in || !out || c->kind != qp_circuit::VOTING) return QP_ERR_ARG;
   *out = nullptr;
-  if ((in->num_siblings && !in->siblings) || (in->num_path_indices && !in->path_indices)) return QP_ERR_ARG;
   try {
-    qv::VoteInputs vi;
-    memcpy(vi.proposal_id, in->proposal_id, 32);
-    memcpy(vi.merkle_root, in->merkle_root, 32);
-    memcpy(vi.nullifier, in->nullifier, 32);
-    vi.vote = in->vote != 0;
-    memcpy(vi.private_key, in->private_key, 32);
-    for (uint32_t i = 0; i < in->num_siblings; i++)
-      vi.merkle_siblings.push_back({in->siblings[4 * i], in->siblings[4 * i + 1], in->siblings[4 * i + 2],
-                                    in->siblings[4 * i + 3]});
-    for (uint32_t i = 0; i < in->num_path_indices; i++) vi.path_indices.push_back(in->path_indices[i] != 0);
-    vi.actual_merkle_depth = in->actual_merkle_depth;
     auto w = std::make_unique<qp_witness>(c);
-    std::string e = qv::fill_targets(c->voting, vi, w->w);
+    int code = QP_OK;
+    std::string e = voting_fill(c, in, w->w, &code);
+    if (e.empty() && !w->w.generate(e)) code = QP_ERR_WITNESS;
     if (!e.empty()) {
       put_err(err, errcap, e);
-      return QP_ERR_ARG;
-    }
-    if (!w->w.generate(e)) {
-      put_err(err, errcap, e);
-      return QP_ERR_WITNESS;
+      return code ? code : QP_ERR_ARG;
     }
     *out = w.release();
     return QP_OK;

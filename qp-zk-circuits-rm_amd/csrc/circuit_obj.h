@@ -13,6 +13,11 @@ struct qp_circuit {
   uint32_t gates_used = 0;
 };
 
+// commit(): the fragments' fill_targets into w (no generation); "" on success,
+// else the reference's message; *code receives the qp_status to return
+std::string wormhole_fill(const qp_circuit *c, const void *in /* qp_wormhole_inputs */, qc::Witness &w, int *code);
+std::string voting_fill(const qp_circuit *c, const void *in /* qp_voting_inputs */, qc::Witness &w, int *code);
+
 struct qp_witness {
   explicit qp_witness(const qp_circuit *c) : circuit(c), w(c->cd) {}
   const qp_circuit *circuit;

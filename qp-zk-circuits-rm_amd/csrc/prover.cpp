@@ -13,6 +13,7 @@
 #include <string.h>
 #include <algorithm>
 #include <chrono>
+#include <atomic>
 #include <memory>
 #include <new>
 #include <stdexcept>
@@ -24,6 +25,7 @@
 #include "host_util.h"
 #include "kernels.h"
 #include "prover_kernels.h"
+#include "witness_kernels.h"
 
 // PoW search window per launch (candidates per still-searching proof), log2
 #ifndef QP_POW_WINDOW_LOG
@@ -113,7 +115,15 @@ struct qp_prover {
     bool pending = false;
     double pend_units = 0;
   } kt[8];
-  const uint64_t *ext_wires = nullptr;  // device-resident wires for prove_wires_dev
+  // device witness generation (witness.hip): schedule + per-proof slot values
+  DevBuf wg_gens, wg_lvl, wg_wslot, wg_wslot_cm, wg_in_slots, wg_pi_slots, wg_vals, wg_in, wg_err, wg_pis;
+  uint32_t wg_nslots = 0, wg_nin = 0, wg_nlev = 0;
+  uint64_t *h_in = nullptr;  // pinned [max_batch][wg_nin] commit() values
+  std::vector<uint32_t> h_werr;
+  std::vector<uint64_t> h_wpis;
+  ~qp_prover() {
+    if (h_in) (void)hipHostFree(h_in);
+  }
 };
 
 namespace {
@@ -175,9 +185,11 @@ int setup(qp_prover *P) {
   for (auto a : P->arity) tot += a;
   P->final_len = 1u << (P->log_n - tot);
   P->common = cd.common_bytes();
-  if (P->nc != 2 || cd.config.zero_knowledge || (1u << P->rate_bits) != P->qdf || P->log_n > 14 ||
-      P->log_n < 6 || P->nchunks > 16 || P->NC > 8 || P->arity.size() > 8 || P->nq > 64) {
-    c->err = "unsupported circuit shape for the GPU prover (need 2 challenges, non-zk, qdf = blowup, 2^6 <= n <= 2^14)";
+  // zero_knowledge is accepted: under the reference's `no_random` feature the zk
+  // config adds neither blinding rows nor salt columns (see DESIGN.md "zk")
+  if (P->nc != 2 || (1u << P->rate_bits) != P->qdf || P->log_n > 14 || P->log_n < 6 || P->nchunks > 16 ||
+      P->NC > 8 || P->arity.size() > 8 || P->nq > 64) {
+    c->err = "unsupported circuit shape for the GPU prover (need 2 challenges, qdf = blowup, 2^6 <= n <= 2^14)";
     return QP_ERR_ARG;
   }
   qpk::GateDesc &g = P->gdesc;
@@ -308,6 +320,35 @@ int setup(qp_prover *P) {
   P->h_pos.assign(B, 0);
   P->h_powst.assign((size_t)B * 24, 0);
   P->h_found.assign(B, 0);
+  {
+    // device witness generation tables (structural, shared by all proofs)
+    auto up32 = [&](DevBuf &d, const std::vector<uint32_t> &v) -> hipError_t {
+      hipError_t e = d.alloc((v.size() + 1) / 2);
+      if (!e && !v.empty()) e = hipMemcpy(d.p, v.data(), v.size() * 4, hipMemcpyHostToDevice);
+      return e;
+    };
+    P->wg_nslots = cd.num_slots;
+    P->wg_nin = (uint32_t)cd.input_slots.size();
+    P->wg_nlev = (uint32_t)cd.level_off.size() - 1;
+    if (P->npis > 256) {
+      c->err = "too many public inputs for the device witness gather";
+      return QP_ERR_ARG;
+    }
+    TRY(P->wg_gens.alloc(cd.dev_gens.size() * 5));
+    TRY(hipMemcpy(P->wg_gens.p, cd.dev_gens.data(), cd.dev_gens.size() * sizeof(qc::DevGen), hipMemcpyHostToDevice));
+    TRY(up32(P->wg_lvl, cd.level_off));
+    TRY(up32(P->wg_wslot, cd.wire_slot));
+    TRY(up32(P->wg_wslot_cm, cd.wire_slot_cm));
+    TRY(up32(P->wg_in_slots, cd.input_slots));
+    TRY(up32(P->wg_pi_slots, cd.pi_slots));
+    TRY(P->wg_vals.alloc((size_t)B * P->wg_nslots));
+    TRY(P->wg_in.alloc((size_t)B * std::max<uint32_t>(P->wg_nin, 1)));
+    TRY(P->wg_err.alloc((B + 1) / 2));
+    TRY(P->wg_pis.alloc((size_t)B * std::max<uint32_t>(P->npis, 1)));
+    TRY(hipHostMalloc((void **)&P->h_in, (size_t)B * std::max<uint32_t>(P->wg_nin, 1) * 8, hipHostMallocDefault));
+    P->h_werr.assign(B, 0);
+    P->h_wpis.assign((size_t)B * std::max<uint32_t>(P->npis, 1), 0);
+  }
   TRY(hipStreamSynchronize(c->stream));
   P->proof_len = proof_size(P);
   unsigned hw = std::thread::hardware_concurrency();
@@ -374,8 +415,10 @@ struct ProofState {
 
 using Clock = std::chrono::steady_clock;
 
-int prove_batch(qp_prover *P, const uint64_t *const *wires_host, const uint64_t *const *pis_host, uint32_t nb,
-                uint8_t *out, size_t stride, size_t *lens) {
+// d_wires: device wire matrices [nb][W][n] (caller-resident or generated on
+// the device into P->wires.vals), or null to upload wires_host[b]
+int prove_batch(qp_prover *P, const uint64_t *d_wires, const uint64_t *const *wires_host,
+                const uint64_t *const *pis_host, uint32_t nb, uint8_t *out, size_t stride, size_t *lens) {
   qp_ctx *c = P->ctx;
   hipStream_t s = c->stream;
   const uint64_t n = 1ull << P->log_n;
@@ -393,18 +436,17 @@ int prove_batch(qp_prover *P, const uint64_t *const *wires_host, const uint64_t 
   TRY(hipSetDevice(c->device));
   int rc;
 
-  // ---- 1. wires commitment (values already on the device for prove_wires_dev)
-  uint64_t *vals_save = P->wires.vals.p;
-  if (P->ext_wires) {
-    P->wires.vals.p = const_cast<uint64_t *>(P->ext_wires);
-  } else {
+  // ---- 1. wires commitment
+  const uint64_t *wv = d_wires;
+  if (!wv) {
     for (uint32_t b = 0; b < nb; b++)
       TRY(hipMemcpyAsync(P->wires.vals.p + b * P->wires.cbs(), wires_host[b], P->wires.cbs() * 8,
                          hipMemcpyHostToDevice, s));
+    wv = P->wires.vals.p;
   }
   {
     Tree &t = P->wires;
-    qpk::intt(c->tw, t.vals.p, t.n(), t.coeffs.p, t.n(), t.npolys, t.log_n, nb, t.cbs(), t.cbs(), s);
+    qpk::intt(c->tw, wv, t.n(), t.coeffs.p, t.n(), t.npolys, t.log_n, nb, t.cbs(), t.cbs(), s);
     kt_begin(P, 0);
     qpk::lde(c->tw, t.coeffs.p, t.n(), t.lde.p, t.N(), t.npolys, t.log_n, t.rate_bits, gl::GEN, nb, t.cbs(), t.lbs(), s);
     kt_end(P, 0, (double)nb * t.npolys * 8.0 * (double)(t.n() + t.N()));
@@ -434,12 +476,11 @@ int prove_batch(qp_prover *P, const uint64_t *const *wires_host, const uint64_t 
 
   // ---- 2. partial products + Z (a9), commitment
   const uint64_t pbs = (uint64_t)nc * P->nchunks * n;
-  qpk::k_pp_rows<<<dim3(cdiv(n, 256), nb), 256, 0, s>>>(P->wires.vals.p, P->sigmas.p, P->kis.p, P->chal.p, P->prods.p,
+  qpk::k_pp_rows<<<dim3(cdiv(n, 256), nb), 256, 0, s>>>(wv, P->sigmas.p, P->kis.p, P->chal.p, P->prods.p,
                                                          P->log_n, P->R, P->qdf, nc, P->wires.cbs(), pbs, c->tw.fwd);
   qpk::k_z_scan<<<dim3(nc, nb), 1024, 0, s>>>(P->prods.p, P->zs.vals.p, P->log_n, nc, P->nchunks, pbs, P->zs.cbs());
   P->zs.build_from_values(c, nb);
   TRY(hipGetLastError());
-  P->wires.vals.p = vals_save;
   if ((rc = fetch_caps(P, P->zs.dig.p, P->zs.dbs(), logN, nb))) return rc;
   P->pool->parallel_for(nb, [&](size_t b) {
     ProofState &S = st[b];
@@ -792,6 +833,118 @@ int prove_batch(qp_prover *P, const uint64_t *const *wires_host, const uint64_t 
   return QP_OK;
 }
 
+
+// device witness generation for nb proofs whose commit() values are in
+// P->h_in ([nb][wg_nin], input-slot order): slot values -> generators level
+// by level -> wire matrices in P->wires.vals, public inputs in P->h_wpis
+int gen_witness_batch(qp_prover *P, uint32_t nb) {
+  qp_ctx *c = P->ctx;
+  hipStream_t s = c->stream;
+  const uint64_t nw = (uint64_t)P->W << P->log_n;
+  if (P->wg_nin)
+    TRY(hipMemcpyAsync(P->wg_in.p, P->h_in, (size_t)nb * P->wg_nin * 8, hipMemcpyHostToDevice, s));
+  qpk::k_witness_init<<<dim3(std::min<unsigned>(cdiv(P->wg_nslots, 256), 256), nb), 256, 0, s>>>(
+      P->wg_vals.p, P->wg_nslots, P->wg_nslots, nullptr, nullptr, 0);
+  if (P->wg_nin)
+    qpk::k_witness_inputs<<<dim3(cdiv(P->wg_nin, 256), nb), 256, 0, s>>>(
+        P->wg_vals.p, P->wg_nslots, (const uint32_t *)P->wg_in_slots.p, P->wg_in.p, P->wg_nin);
+  TRY(hipMemsetAsync(P->wg_err.p, 0, (size_t)nb * 4, s));
+  qpk::WitnessGenArgs a;
+  a.vals = P->wg_vals.p;
+  a.v_bstride = P->wg_nslots;
+  a.gens = P->wg_gens.p;
+  a.level_off = (const uint32_t *)P->wg_lvl.p;
+  a.nlevels = P->wg_nlev;
+  a.wslot = (const uint32_t *)P->wg_wslot.p;
+  a.W = P->W;
+  a.limbs = std::min<uint32_t>(63, P->R - 1);
+  a.zero_slot = P->circuit->cd.zero_const_slot;
+  a.num_consts = P->circuit->cd.config.num_constants;
+  a.err = (uint32_t *)P->wg_err.p;
+  qpk::k_witness_gen<<<nb, 256, 0, s>>>(a);
+  qpk::k_witness_expand<<<dim3((unsigned)std::min<uint64_t>(cdiv(nw, 256), 1024), nb), 256, 0, s>>>(
+      P->wg_vals.p, P->wg_nslots, (const uint32_t *)P->wg_wslot_cm.p, nw, P->wires.vals.p, P->wires.cbs(),
+      (const uint32_t *)P->wg_pi_slots.p, P->npis, P->wg_pis.p);
+  TRY(hipGetLastError());
+  TRY(hipMemcpyAsync(P->h_werr.data(), P->wg_err.p, (size_t)nb * 4, hipMemcpyDeviceToHost, s));
+  if (P->npis)
+    TRY(hipMemcpyAsync(P->h_wpis.data(), P->wg_pis.p, (size_t)nb * P->npis * 8, hipMemcpyDeviceToHost, s));
+  TRY(hipStreamSynchronize(s));
+  for (uint32_t b = 0; b < nb; b++)
+    if (P->h_werr[b]) {
+      c->err = "proof " + std::to_string(b) +
+               ": Partition containing a target was set twice with different values (device generator " +
+               std::to_string(P->h_werr[b] - 1) + ")";
+      return QP_ERR_WITNESS;
+    }
+  return QP_OK;
+}
+
+using FillFn = std::string (*)(const qp_circuit *, const void *, qc::Witness &, int *);
+
+// WormholeProver::commit + prove (wormhole/prover/src/lib.rs:209-237) for a
+// batch: commit() on the host pool, generation on the device, then prove
+int prove_inputs(qp_prover *P, FillFn fill, const uint8_t *inputs, size_t in_size, uint32_t nproofs, uint8_t *out,
+                 size_t stride, size_t *lens) {
+  const qc::CircuitData &cd = P->circuit->cd;
+  for (uint32_t done = 0; done < nproofs;) {
+    const uint32_t nb = std::min(P->max_batch, nproofs - done);
+    std::atomic<uint32_t> first_bad{UINT32_MAX};
+    std::vector<std::string> msgs(nb);
+    std::vector<int> codes(nb, QP_OK);
+    auto T0 = Clock::now();
+    P->pool->parallel_for(nb, [&](size_t b) {
+      thread_local std::vector<uint64_t> scratch;
+      if (scratch.size() < cd.num_slots) scratch.resize(cd.num_slots);
+      qc::Witness w(cd, scratch.data());
+      int code = QP_OK;
+      std::string e = fill(P->circuit, inputs + (done + b) * in_size, w, &code);
+      uint64_t *row = P->h_in + b * (size_t)P->wg_nin;
+      if (e.empty())
+        for (uint32_t i = 0; i < P->wg_nin; i++) {
+          uint64_t v;
+          if (!w.get_slot(cd.input_slots[i], v)) {
+            e = "a circuit input target was not set by commit";
+            code = QP_ERR_STATE;
+            break;
+          }
+          row[i] = v;
+        }
+      if (!e.empty()) {
+        msgs[b] = e;
+        codes[b] = code ? code : QP_ERR_ARG;
+        uint32_t cur = first_bad.load();
+        while (b < cur && !first_bad.compare_exchange_weak(cur, (uint32_t)b)) {
+        }
+      }
+    });
+    if (first_bad.load() != UINT32_MAX) {
+      const uint32_t b = first_bad.load();
+      P->ctx->err = "proof " + std::to_string(done + b) + ": " + msgs[b];
+      return codes[b];
+    }
+    auto T1 = Clock::now();
+    P->stage_ms[8] += std::chrono::duration<double, std::milli>(T1 - T0).count();
+    int rc = gen_witness_batch(P, nb);
+    P->stage_ms[9] += std::chrono::duration<double, std::milli>(Clock::now() - T1).count();
+    if (rc) {
+      P->ctx->err += " (batch offset " + std::to_string(done) + ")";
+      return rc;
+    }
+    std::vector<const uint64_t *> pp(nb);
+    for (uint32_t b = 0; b < nb; b++) pp[b] = P->h_wpis.data() + (size_t)b * P->npis;
+    try {
+      rc = prove_batch(P, P->wires.vals.p, nullptr, pp.data(), nb, out + (size_t)done * stride, stride,
+                       lens ? lens + done : nullptr);
+    } catch (const std::bad_alloc &) {
+      rc = QP_ERR_OOM;
+    }
+    if (rc) return rc;
+    done += nb;
+  }
+  return QP_OK;
+}
+
 }  // namespace
 
 extern "C" {
@@ -863,7 +1016,8 @@ int qp_prover_prove_wires(qp_prover *P, const uint64_t *wires, const uint64_t *p
     }
     int rc;
     try {
-      rc = prove_batch(P, wp.data(), pp.data(), nb, out + (size_t)done * stride, stride, lens ? lens + done : nullptr);
+      rc = prove_batch(P, nullptr, wp.data(), pp.data(), nb, out + (size_t)done * stride, stride,
+                       lens ? lens + done : nullptr);
     } catch (const std::bad_alloc &) {
       rc = QP_ERR_OOM;
     }
@@ -873,6 +1027,9 @@ int qp_prover_prove_wires(qp_prover *P, const uint64_t *wires, const uint64_t *p
   return QP_OK;
 }
 
+// witnesses generated on the host (qp_wormhole_commit / qp_voting_commit):
+// their partition values go up (num_slots words each, ~1/5 of the wire
+// matrix) and are expanded into the wire matrices on the device
 int qp_prover_prove(qp_prover *P, const qp_witness *const *w, uint32_t nproofs, uint8_t *out, size_t stride,
                     size_t *lens) {
   if (!P || !w || !out || !nproofs) return QP_ERR_ARG;
@@ -880,33 +1037,34 @@ int qp_prover_prove(qp_prover *P, const qp_witness *const *w, uint32_t nproofs, 
     P->ctx->err = "output stride smaller than the proof size";
     return QP_ERR_ARG;
   }
-  const uint64_t wsz = (uint64_t)P->W << P->log_n;
-  for (uint32_t done = 0; done < nproofs;) {
-    const uint32_t nb = std::min(P->max_batch, nproofs - done);
-    std::vector<uint64_t> wires((size_t)nb * wsz), pis((size_t)nb * P->npis);
-    bool bad = false;
-    P->pool->parallel_for(nb, [&](size_t b) {
-      const qp_witness *wt = w[done + b];
-      if (!wt || wt->circuit != P->circuit) {
-        bad = true;
-        return;
-      }
-      wt->w.wires_matrix(wires.data() + b * wsz);
-      auto pi = wt->w.public_inputs();
-      memcpy(pis.data() + b * P->npis, pi.data(), P->npis * 8);
-    });
-    if (bad) {
+  for (uint32_t i = 0; i < nproofs; i++)
+    if (!w[i] || w[i]->circuit != P->circuit) {
       P->ctx->err = "witness belongs to a different circuit";
       return QP_ERR_ARG;
     }
-    std::vector<const uint64_t *> wp(nb), pp(nb);
+  hipStream_t s = P->ctx->stream;
+  const uint64_t nw = (uint64_t)P->W << P->log_n;
+  for (uint32_t done = 0; done < nproofs;) {
+    const uint32_t nb = std::min(P->max_batch, nproofs - done);
+    std::vector<uint64_t> pis((size_t)nb * P->npis);
+    std::vector<const uint64_t *> pp(nb);
+    TRY(hipSetDevice(P->ctx->device));
     for (uint32_t b = 0; b < nb; b++) {
-      wp[b] = wires.data() + b * wsz;
-      pp[b] = pis.data() + b * P->npis;
+      const qc::Witness &wt = w[done + b]->w;
+      TRY(hipMemcpyAsync(P->wg_vals.p + (size_t)b * P->wg_nslots, wt.slot_values(), (size_t)P->wg_nslots * 8,
+                         hipMemcpyHostToDevice, s));
+      auto pi = wt.public_inputs();
+      memcpy(pis.data() + (size_t)b * P->npis, pi.data(), P->npis * 8);
+      pp[b] = pis.data() + (size_t)b * P->npis;
     }
+    qpk::k_witness_expand<<<dim3((unsigned)std::min<uint64_t>(cdiv(nw, 256), 1024), nb), 256, 0, s>>>(
+        P->wg_vals.p, P->wg_nslots, (const uint32_t *)P->wg_wslot_cm.p, nw, P->wires.vals.p, P->wires.cbs(),
+        (const uint32_t *)P->wg_pi_slots.p, P->npis, P->wg_pis.p);
+    TRY(hipGetLastError());
     int rc;
     try {
-      rc = prove_batch(P, wp.data(), pp.data(), nb, out + (size_t)done * stride, stride, lens ? lens + done : nullptr);
+      rc = prove_batch(P, P->wires.vals.p, nullptr, pp.data(), nb, out + (size_t)done * stride, stride,
+                       lens ? lens + done : nullptr);
     } catch (const std::bad_alloc &) {
       rc = QP_ERR_OOM;
     }
@@ -914,6 +1072,44 @@ int qp_prover_prove(qp_prover *P, const qp_witness *const *w, uint32_t nproofs, 
     done += nb;
   }
   return QP_OK;
+}
+
+int qp_prover_prove_wormhole_inputs(qp_prover *P, const qp_wormhole_inputs *in, uint32_t nproofs, uint8_t *out,
+                                    size_t stride, size_t *lens) {
+  if (!P || !in || !out || !nproofs) return QP_ERR_ARG;
+  if (P->circuit->kind != qp_circuit::WORMHOLE) {
+    P->ctx->err = "prover circuit is not the Wormhole circuit";
+    return QP_ERR_ARG;
+  }
+  if (stride < P->proof_len) {
+    P->ctx->err = "output stride smaller than the proof size";
+    return QP_ERR_ARG;
+  }
+  TRY(hipSetDevice(P->ctx->device));
+  try {
+    return prove_inputs(P, wormhole_fill, (const uint8_t *)in, sizeof(qp_wormhole_inputs), nproofs, out, stride, lens);
+  } catch (const std::bad_alloc &) {
+    return QP_ERR_OOM;
+  }
+}
+
+int qp_prover_prove_voting_inputs(qp_prover *P, const qp_voting_inputs *in, uint32_t nproofs, uint8_t *out,
+                                  size_t stride, size_t *lens) {
+  if (!P || !in || !out || !nproofs) return QP_ERR_ARG;
+  if (P->circuit->kind != qp_circuit::VOTING) {
+    P->ctx->err = "prover circuit is not the voting circuit";
+    return QP_ERR_ARG;
+  }
+  if (stride < P->proof_len) {
+    P->ctx->err = "output stride smaller than the proof size";
+    return QP_ERR_ARG;
+  }
+  TRY(hipSetDevice(P->ctx->device));
+  try {
+    return prove_inputs(P, voting_fill, (const uint8_t *)in, sizeof(qp_voting_inputs), nproofs, out, stride, lens);
+  } catch (const std::bad_alloc &) {
+    return QP_ERR_OOM;
+  }
 }
 
 int qp_prover_set_timing(qp_prover *P, int enable) {
@@ -947,16 +1143,15 @@ int qp_prover_prove_wires_dev(qp_prover *P, const uint64_t *d_wires, const uint6
   const uint64_t wsz = (uint64_t)P->W << P->log_n;
   for (uint32_t done = 0; done < nproofs;) {
     const uint32_t nb = std::min(P->max_batch, nproofs - done);
-    std::vector<const uint64_t *> wp(nb, nullptr), pp(nb);
+    std::vector<const uint64_t *> pp(nb);
     for (uint32_t b = 0; b < nb; b++) pp[b] = pis + (uint64_t)(done + b) * P->npis;
-    P->ext_wires = d_wires + (uint64_t)done * wsz;
     int rc;
     try {
-      rc = prove_batch(P, wp.data(), pp.data(), nb, out + (size_t)done * stride, stride, lens ? lens + done : nullptr);
+      rc = prove_batch(P, d_wires + (uint64_t)done * wsz, nullptr, pp.data(), nb, out + (size_t)done * stride, stride,
+                       lens ? lens + done : nullptr);
     } catch (const std::bad_alloc &) {
       rc = QP_ERR_OOM;
     }
-    P->ext_wires = nullptr;
     if (rc) return rc;
     done += nb;
   }

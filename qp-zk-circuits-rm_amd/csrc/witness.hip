@@ -1,0 +1,159 @@
+// witness.hip — witness generation on the device (plonky2 iop/generator.rs
+// generate_partial_witness), for the circuits of the
+// native builder (circuit.cpp).
+//
+// The host only runs commit() (the fragments' fill_targets: a few thousand
+// input values per proof, uploaded as one compact row); every generator —
+// Poseidon gates, BaseSum limbs, arithmetic, equality (inverse), constants —
+// runs here.  build() groups the generators into dependency levels; one
+// workgroup owns one proof and walks the levels with a barrier between them,
+// so B proofs occupy B CUs with no grid-wide synchronisation.
+//
+// Partition values live in HBM, one u64 per value slot, UNSET = 2^64 - 1 (not
+// a canonical field element) until written.  A write is a compare-and-swap
+// from UNSET: writing a different value to a written slot is the reference's
+// "Partition containing ... was set twice with different values" failure and
+// flags the proof.  Slot 0 is the shared never-set slot (value 0).
+#include <hip/hip_runtime.h>
+#include "field.h"
+#include "poseidon.h"
+#include "witness_kernels.h"
+
+namespace qpk {
+
+constexpr uint64_t UNSET = ~0ull;
+
+struct DevGenD {  // == qc::DevGen
+  uint32_t kind, row;
+  uint32_t s[4];
+  uint64_t k0, k1;
+};
+enum : uint32_t { WG_CONSTANT = 0, WG_ARITH, WG_POSEIDON, WG_BASE_SPLIT, WG_EQUALITY };
+
+__device__ __forceinline__ bool wset(uint64_t *v, uint32_t s, uint64_t x) {
+  const unsigned long long old = atomicCAS((unsigned long long *)(v + s), (unsigned long long)UNSET,
+                                           (unsigned long long)x);
+  return old == UNSET || old == x;
+}
+
+__global__ void k_witness_init(uint64_t *vals, uint64_t v_bstride, uint32_t nslots, const uint32_t *in_slots,
+                               const uint64_t *in_vals, uint32_t nin) {
+  const uint32_t b = blockIdx.y;
+  uint64_t *v = vals + (uint64_t)b * v_bstride;
+  for (uint32_t s = blockIdx.x * blockDim.x + threadIdx.x; s < nslots; s += gridDim.x * blockDim.x)
+    v[s] = s ? UNSET : 0;
+}
+
+__global__ void k_witness_inputs(uint64_t *vals, uint64_t v_bstride, const uint32_t *in_slots,
+                                 const uint64_t *in_vals, uint32_t nin) {
+  const uint32_t b = blockIdx.y;
+  const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i < nin) vals[(uint64_t)b * v_bstride + in_slots[i]] = in_vals[(uint64_t)b * nin + i];
+}
+
+__device__ bool run_gen(const DevGenD &g, uint64_t *v, const uint32_t *wslot, uint32_t W, uint32_t limbs,
+                        uint32_t zslot, uint32_t num_consts) {
+  switch (g.kind) {
+    case WG_CONSTANT:
+      return wset(v, g.s[0], g.k0) && (num_consts < 2 || wset(v, g.s[1], g.k1));
+    case WG_ARITH: {
+      const uint64_t m = gl::mul(gl::mul(v[g.s[0]], v[g.s[1]]), g.k0);
+      return wset(v, g.s[3], gl::add(m, gl::mul(v[g.s[2]], g.k1)));
+    }
+    case WG_BASE_SPLIT: {
+      const uint64_t sum = v[g.s[0]];
+      const uint32_t *ws = wslot + (uint64_t)g.row * W + 1;
+      bool ok = true;
+      for (uint32_t l = 0; l < limbs; l++) {
+        const uint64_t bit = (sum >> l) & 1;
+        if (zslot && ws[l] == zslot) ok &= bit == 0;
+        else ok &= wset(v, ws[l], bit);
+      }
+      return ok;
+    }
+    case WG_EQUALITY: {
+      const uint64_t x = v[g.s[0]], y = v[g.s[1]];
+      const bool eq = x == y;
+      return wset(v, g.s[2], eq ? 1 : 0) && wset(v, g.s[3], eq ? 0 : gl::inv(gl::sub(x, y)));
+    }
+    case WG_POSEIDON: {
+      // PoseidonGenerator (gates/poseidon.rs), wire layout SURVEY.md A.5
+      const uint32_t *ws = wslot + (uint64_t)g.row * W;
+      uint64_t s[12];
+      for (int i = 0; i < 12; i++) s[i] = v[ws[i]];
+      const uint64_t swap = v[ws[24]];
+      bool ok = true;
+      for (int i = 0; i < 4; i++) ok &= wset(v, ws[25 + i], gl::mul(swap, gl::sub(s[i + 4], s[i])));
+      if (swap == 1)
+        for (int i = 0; i < 4; i++) {
+          const uint64_t t = s[i];
+          s[i] = s[i + 4];
+          s[i + 4] = t;
+        }
+      int rc = 0;
+      for (int r = 0; r < 4; r++, rc++) {
+        for (int i = 0; i < 12; i++) s[i] = gl::add(s[i], ps::rc(rc * 12 + i));
+        if (r)
+          for (int i = 0; i < 12; i++) ok &= wset(v, ws[29 + (r - 1) * 12 + i], s[i]);
+        for (int i = 0; i < 12; i++) s[i] = ps::sbox(s[i]);
+        ps::mds(s);
+      }
+      for (int r = 0; r < 22; r++, rc++) {
+        for (int i = 0; i < 12; i++) s[i] = gl::add(s[i], ps::rc(rc * 12 + i));
+        ok &= wset(v, ws[65 + r], s[0]);
+        s[0] = ps::sbox(s[0]);
+        ps::mds(s);
+      }
+      for (int r = 0; r < 4; r++, rc++) {
+        for (int i = 0; i < 12; i++) s[i] = gl::add(s[i], ps::rc(rc * 12 + i));
+        for (int i = 0; i < 12; i++) ok &= wset(v, ws[87 + r * 12 + i], s[i]);
+        for (int i = 0; i < 12; i++) s[i] = ps::sbox(s[i]);
+        ps::mds(s);
+      }
+      for (int i = 0; i < 12; i++) ok &= wset(v, ws[12 + i], s[i]);
+      return ok;
+    }
+    default:
+      return false;
+  }
+}
+
+// one workgroup per proof; levels separated by workgroup barriers.  Every
+// wave reaches every barrier (no early exit), so the grid always drains.
+__global__ void __launch_bounds__(256) k_witness_gen(const WitnessGenArgs a) {
+  const uint32_t b = blockIdx.x;
+  uint64_t *v = a.vals + (uint64_t)b * a.v_bstride;
+  const DevGenD *gens = (const DevGenD *)a.gens;
+  bool ok = true;
+  uint32_t bad = 0;
+  for (uint32_t l = 0; l < a.nlevels; l++) {
+    const uint32_t lo = a.level_off[l], hi = a.level_off[l + 1];
+    for (uint32_t i = lo + threadIdx.x; i < hi; i += blockDim.x) {
+      if (!run_gen(gens[i], v, a.wslot, a.W, a.limbs, a.zero_slot, a.num_consts) && ok) {
+        ok = false;
+        bad = i + 1;
+      }
+    }
+    __syncthreads();
+  }
+  if (!ok) atomicCAS(a.err + b, 0u, bad);
+}
+
+// wires [b][col][row] = slot values through the column-major slot map;
+// public inputs gathered alongside
+__global__ void k_witness_expand(const uint64_t *vals, uint64_t v_bstride, const uint32_t *wslot_cm, uint64_t nwires,
+                                 uint64_t *wires, uint64_t w_bstride, const uint32_t *pi_slots, uint32_t npis,
+                                 uint64_t *pis) {
+  const uint32_t b = blockIdx.y;
+  const uint64_t *v = vals + (uint64_t)b * v_bstride;
+  for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < nwires; i += (uint64_t)gridDim.x * blockDim.x) {
+    const uint64_t x = v[wslot_cm[i]];
+    wires[(uint64_t)b * w_bstride + i] = x == UNSET ? 0 : x;
+  }
+  if (blockIdx.x == 0 && threadIdx.x < npis) {
+    const uint64_t x = v[pi_slots[threadIdx.x]];
+    pis[(uint64_t)b * npis + threadIdx.x] = x == UNSET ? 0 : x;
+  }
+}
+
+}  // namespace qpk

@@ -13,7 +13,8 @@ import numpy as np
 from ._native import Context, QpError, lib
 from .circuits import Circuit, CircuitInputs
 
-STAGES = ["commit_wires", "zs_pp", "quotient", "openings", "fri", "pow", "queries", "serialize"]
+STAGES = ["commit_wires", "zs_pp", "quotient", "openings", "fri", "pow", "queries", "serialize", "commit_inputs",
+          "witness_gen"]
 
 
 class ProofWithPublicInputs:
@@ -52,6 +53,31 @@ class Prover:
         self.ctx.check(lib().qp_prover_prove(self.h, arr, nb, out, self.proof_size, lens), "qp_prover_prove")
         raw = out.raw
         return [raw[i * self.proof_size:i * self.proof_size + lens[i]] for i in range(nb)]
+
+    def inputs_array(self, inputs):
+        """CircuitInputs / VoteCircuitData list -> contiguous C-ABI struct array."""
+        structs = [x.to_c() for x in inputs]
+        arr = (type(structs[0]) * len(structs))(*structs)
+        arr._keep = structs  # node byte strings referenced by the structs
+        return arr
+
+    def prove_inputs_array(self, arr, nb):
+        out = ctypes.create_string_buffer(self.proof_size * nb)
+        lens = (ctypes.c_size_t * nb)()
+        fn = lib().qp_prover_prove_voting_inputs if self.circuit.kind == "voting" else \
+            lib().qp_prover_prove_wormhole_inputs
+        self.ctx.check(fn(self.h, ctypes.cast(arr, ctypes.c_void_p), nb, out, self.proof_size, lens),
+                       "qp_prover_prove_inputs")
+        raw = out.raw
+        return [raw[i * self.proof_size:i * self.proof_size + lens[i]] for i in range(nb)]
+
+    def prove_inputs(self, inputs):
+        """End to end: commit(inputs) + prove() for a list of CircuitInputs (Wormhole)
+        or VoteCircuitData (voting) -- commit on the host pool, witness generation on
+        the device (qp_prover_prove_{wormhole,voting}_inputs)."""
+        if not inputs:
+            return []
+        return self.prove_inputs_array(self.inputs_array(inputs), len(inputs))
 
     def prove_wires(self, wires, pis):
         wires = np.ascontiguousarray(wires, dtype=np.uint64)
@@ -115,7 +141,9 @@ def _shared(config, device):
         if key not in _cache:
             ctx = Context(device)
             circ = Circuit.wormhole(zero_knowledge=(config == "standard_recursion_zk_config"))
-            _cache[key] = (ctx, circ, Prover(ctx, circ, 1))
+            # one lock per shared prover: its device buffers, host staging and
+            # stream serve one prove() at a time (ctypes releases the GIL)
+            _cache[key] = (ctx, circ, Prover(ctx, circ, 1), threading.Lock())
         return _cache[key]
 
 
@@ -123,7 +151,7 @@ class WormholeProver:
     def __init__(self, config="standard_recursion_config", device=0):
         if config not in ("standard_recursion_config", "standard_recursion_zk_config"):
             raise ValueError(f"unknown circuit config {config!r}")
-        self.ctx, self.circuit, self.prover = _shared(config, device)
+        self.ctx, self.circuit, self.prover, self._prove_lock = _shared(config, device)
         self._witness = None
         self._committed = False
 
@@ -139,5 +167,6 @@ class WormholeProver:
             raise QpError(4, "prover has not commited to any inputs")
         w = self._witness
         self._witness = None
-        data = self.prover.prove_witnesses([w])[0]
+        with self._prove_lock:
+            data = self.prover.prove_witnesses([w])[0]
         return ProofWithPublicInputs(data, w.public_inputs())

@@ -34,6 +34,7 @@ for s in "$@"; do
     pmc_fetch) pmc fetch FETCH_SIZE ;;
     pmc_write) pmc write WRITE_SIZE ;;
     pmc_valu) pmc valu SQ_WAVES SQ_INSTS_VALU SQ_WAVE_CYCLES SQ_BUSY_CYCLES ;;
+    test_witness) step pytest_witness 600 python -u -m pytest tests/test_gpu_witness.py -x -v --timeout 300 --timeout-method thread ;;
     test_voting) step pytest_voting 300 python -u -m pytest tests/test_gpu_voting.py -x -v --timeout 120 --timeout-method thread ;;
     bench_voting) step bench_voting 600 python bench.py --circuit voting ;;
     benchprof_voting) step rocprof_bench_voting 600 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/prof_bench_voting -o run -- python3 bench.py --circuit voting --steps 3 --warmup 1 --cpu-sample 0 ;;
