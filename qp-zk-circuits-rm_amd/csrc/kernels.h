@@ -24,8 +24,11 @@ struct Twiddles {
   // coset pre-twists of the fused LDE: for rate r (1..LDE_MAX_RATE), at
   // offset 16*(2^r - 2): ptw[16 s + m] = w_{16*2^r}^(s*m), s < 2^r, m < 16
   uint64_t *ptw = nullptr;
+  // the same for the radix-8 LDE: ptw8[8 (2^r - 2) + 8 s + m] = w_{8*2^r}^(s*m), m < 8
+  uint64_t *ptw8 = nullptr;
 };
 __host__ __device__ inline uint32_t ptw_offset(uint32_t rate_bits) { return 16u * ((1u << rate_bits) - 2u); }
+__host__ __device__ inline uint32_t ptw8_offset(uint32_t rate_bits) { return 8u * ((1u << rate_bits) - 2u); }
 
 hipError_t twiddles_init(Twiddles &t, hipStream_t s);
 void twiddles_free(Twiddles &t);

@@ -65,6 +65,16 @@ hipError_t twiddles_init(Twiddles &t, hipStream_t s) {
   if (e) return e;
   e = hipMemcpyAsync(t.ptw, ptw.data(), ptw.size() * 8, hipMemcpyHostToDevice, s);
   if (e) return e;
+  std::vector<uint64_t> ptw8(ptw8_offset(LDE_MAX_RATE + 1));
+  for (uint32_t r = 1; r <= LDE_MAX_RATE; r++) {
+    const uint64_t wr = gl::root_of_unity(3 + r);
+    for (uint32_t sc = 0; sc < (1u << r); sc++)
+      for (uint32_t m = 0; m < 8; m++) ptw8[ptw8_offset(r) + 8 * sc + m] = gl::pow(wr, (uint64_t)sc * m);
+  }
+  e = hipMalloc(&t.ptw8, ptw8.size() * 8);
+  if (e) return e;
+  e = hipMemcpyAsync(t.ptw8, ptw8.data(), ptw8.size() * 8, hipMemcpyHostToDevice, s);
+  if (e) return e;
   return hipStreamSynchronize(s);
 }
 
@@ -72,7 +82,8 @@ void twiddles_free(Twiddles &t) {
   if (t.fwd) (void)hipFree(t.fwd);
   if (t.inv) (void)hipFree(t.inv);
   if (t.ptw) (void)hipFree(t.ptw);
-  t.fwd = t.inv = t.ptw = nullptr;
+  if (t.ptw8) (void)hipFree(t.ptw8);
+  t.fwd = t.inv = t.ptw = t.ptw8 = nullptr;
 }
 
 __global__ void __launch_bounds__(512) QP_NTT_OCC k_intt(const uint64_t *__restrict__ in, uint64_t in_stride,
@@ -170,6 +181,62 @@ __global__ void __launch_bounds__(1 << LOG_T) QP_NTT_OCC k_lde_cosets(const uint
   }
 }
 
+// Radix-8 form of k_lde_cosets (n = 8 T, T = 2^LOG_T threads): thread t holds
+// a_m = c_{t+Tm} shift^{t+Tm}, m < 8; per coset one pre-twist by
+// w_{8B}^{sm}, an 8-point DFT in registers, the merged twiddle
+// w_N^{t(s + B brev3(m))}, then radix-8 passes in LDS.  Twice the threads per
+// column at the same LDS: 8 waves per SIMD.  Measured (tools/ab_round2_2.sh,
+// profiles/r02_ab_lde_radix8.log): 4.63 vs 4.48 ms per 64-proof launch — the
+// doubled occupancy turns into LDS stalls (+33 % LDS instructions, 2.2x bank-
+// conflict cycles, 3x SQ_WAIT_INST_ANY), so the radix-16 form stays the
+// default (QP_LDE_RADIX8=1 selects this one).
+#ifndef QP_LDE_RADIX8
+#define QP_LDE_RADIX8 0
+#endif
+template <int LOG_T>
+__global__ void __launch_bounds__(1 << LOG_T) __attribute__((amdgpu_waves_per_eu(8)))
+k_lde_cosets8(const uint64_t *__restrict__ coeffs, uint64_t c_stride, uint64_t c_bstride, uint64_t *__restrict__ out,
+              uint64_t o_stride, uint64_t o_bstride, uint32_t rate_bits, uint64_t shift, uint64_t shift_T,
+              const uint64_t *__restrict__ tw, const uint64_t *__restrict__ ptw8) {
+  constexpr uint32_t T = 1u << LOG_T, LOG_N = LOG_T + 3;
+  extern __shared__ __attribute__((aligned(16))) uint64_t lds[];
+  const uint32_t t = threadIdx.x;
+  const uint64_t *src = coeffs + blockIdx.y * c_bstride + (uint64_t)blockIdx.x * c_stride;
+  uint64_t *dst0 = out + blockIdx.y * o_bstride + (uint64_t)blockIdx.x * o_stride;
+  uint64_t a[8];
+#pragma unroll
+  for (int m = 0; m < 8; m++) a[m] = src[t + T * m];
+  {
+    uint64_t f = gl::pow(shift, t);
+#pragma unroll
+    for (int m = 0; m < 8; m++) {
+      a[m] = nt::mul(a[m], f);
+      f = nt::mul(f, shift_T);
+    }
+  }
+  const uint32_t logN = LOG_N + rate_bits, B = 1u << rate_bits;
+  const uint64_t *pt = ptw8 + ptw8_offset(rate_bits);
+  for (uint32_t s = 0; s < B; s++) {
+    uint64_t r[8];
+    r[0] = a[0];
+#pragma unroll
+    for (int m = 1; m < 8; m++) r[m] = nt::mul(a[m], pt[8 * s + m]);
+    nt::dft8<false>(r);
+#pragma unroll
+    for (int m = 0; m < 8; m++) {
+      const uint32_t e = t * (s + (nt::brev3(m) << rate_bits));
+      if (e) r[m] = nt::mul(r[m], nt::tw_pow(tw, e, logN));
+      lds[nt::lp(t) + nt::lp(T * m)] = r[m];
+    }
+    __syncthreads();
+    nt::ntt8_lds_from<false>(lds, LOG_N, LOG_T, tw);
+    uint64_t *dst = dst0 + ((uint64_t)gl::rev_bits(s, rate_bits) << LOG_N);
+#pragma unroll
+    for (int m = 0; m < 8; m++) dst[t + T * m] = nt::canon(lds[nt::lp(t) + nt::lp(T * m)]);
+    __syncthreads();
+  }
+}
+
 static unsigned ntt_threads(uint32_t log_n) {
   uint32_t half = log_n ? (1u << (log_n - 1)) : 1;
   return half < 64 ? 64 : (half > 512 ? 512 : half);
@@ -190,10 +257,16 @@ void lde(const Twiddles &t, const uint64_t *coeffs, uint64_t c_stride, uint64_t 
   if (!ncols || !nbat) return;
   if (rate_bits >= 1 && rate_bits <= LDE_MAX_RATE && log_n >= 10 && log_n <= 13 && log_n + rate_bits <= TW_LOG &&
       !getenv_flag("QPGPU_LDE_PERCOSET")) {
-    const uint32_t T = 1u << (log_n - 4);
-    const uint64_t shift_T = gl::pow(shift, T);
     dim3 g(ncols, nbat);
     const size_t lds_bytes = (size_t)8 * qpk::ntt_lds_words(1u << log_n);
+    if (QP_LDE_RADIX8 && log_n == 13) {
+      const uint64_t shift_T8 = gl::pow(shift, 1u << (log_n - 3));
+      k_lde_cosets8<10><<<g, 1024, lds_bytes, s>>>(coeffs, c_stride, c_bstride, out, o_stride, o_bstride, rate_bits,
+                                                   shift, shift_T8, t.fwd, t.ptw8);
+      return;
+    }
+    const uint32_t T = 1u << (log_n - 4);
+    const uint64_t shift_T = gl::pow(shift, T);
 #define QP_LDE_COSETS(LT)                                                                                      \
   k_lde_cosets<LT><<<g, 1u << LT, lds_bytes, s>>>(coeffs, c_stride, c_bstride, out, o_stride, o_bstride, rate_bits, \
                                                   shift, shift_T, t.fwd, t.ptw)

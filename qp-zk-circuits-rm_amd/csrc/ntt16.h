@@ -24,27 +24,41 @@
 #include "field.h"
 #include "kernels.h"
 #include "poseidon_fast.h"
+#include "field_nc.h"
 
 namespace nt {
 
 constexpr uint64_t EPS = 0xFFFFFFFFull;
 
+// QP_NTT_CARRY (default 1): branch-free 32-bit carry chains (field_nc.h); 0:
+// the 64-bit compare-and-branch forms (A/B)
+#ifndef QP_NTT_CARRY
+#define QP_NTT_CARRY 1
+#endif
 __device__ __forceinline__ uint64_t add(uint64_t a, uint64_t b) {
+#if QP_NTT_CARRY
+  return gfn::add(a, b);
+#else
   uint64_t s = a + b;
   if (s < b) {
     s += EPS;
     if (s < EPS) s += EPS;
   }
   return s;
+#endif
 }
 
 __device__ __forceinline__ uint64_t sub(uint64_t a, uint64_t b) {
+#if QP_NTT_CARRY
+  return gfn::sub(a, b);
+#else
   uint64_t d = a - b;
   if (a < b) {
     uint64_t d1 = d - EPS;
     d = d1 > d ? d1 - EPS : d1;  // second wrap when b - a > p (b non-canonical)
   }
   return d;
+#endif
 }
 
 __device__ __forceinline__ uint64_t reduce(uint64_t lo, uint64_t hi) {
@@ -262,6 +276,84 @@ __device__ __forceinline__ void ntt_lds_from(uint64_t *a, uint32_t log_n, uint32
 template <bool INV>
 __device__ __forceinline__ void ntt_lds(uint64_t *a, uint32_t log_n, const uint64_t *__restrict__ tw) {
   ntt_lds_from<INV>(a, log_n, log_n, tw);
+}
+
+// ---- radix-8 variant: 8 elements per thread (n/8 threads per transform), so
+// a size-2^13 transform is a 1024-thread workgroup whose LDS (67.6 KB) still
+// fits twice per CU: 8 waves per SIMD instead of 4 (VALU issue at 8 waves/SIMD
+// measured 2.56 vs 3.12 cycles per instruction, tools/isa_rates.hip).
+
+__device__ __forceinline__ uint32_t brev3(uint32_t m) { return __builtin_bitreverse32(m) >> 29; }
+
+template <bool INV>
+__device__ __forceinline__ void dft8(uint64_t a[8]) {
+  stage_small<INV, 4, 8>(a);
+  stage_small<INV, 2, 8>(a);
+  stage_small<INV, 1, 8>(a);
+}
+
+// x * w_16^j (forward) or w_16^-j (inverse) for a runtime j < 16 that folds to
+// a constant after unrolling
+template <bool INV>
+__device__ __forceinline__ uint64_t mul_w16_rt(uint64_t x, int j) {
+#define QP_W16(J) \
+  case J: return mul_w16<INV, J>(x);
+  switch (j) {
+    QP_W16(1) QP_W16(2) QP_W16(3) QP_W16(4) QP_W16(5) QP_W16(6) QP_W16(7)
+    default: return x;
+  }
+#undef QP_W16
+}
+
+// radix-8 DIF passes over LDS from sub-problem size 2^log_S down to 2, then the
+// last radix-2 level; every thread of the block participates (n/8 groups per
+// pass).  The S = 16 pass (twiddles w_16^{t brev3(m)}, t in {0,1}: shifts) maps
+// t to bit 6 of the group index so it is wave-uniform.  Ends with a barrier.
+template <bool INV>
+__device__ __forceinline__ void ntt8_lds_from(uint64_t *a, uint32_t log_n, uint32_t log_S,
+                                              const uint64_t *__restrict__ tw) {
+  const uint32_t n = 1u << log_n;
+  const uint32_t T = blockDim.x;
+  while (log_S >= 3) {
+    if (log_S == 4 && (n >> 3) % 128 == 0 && T % 64 == 0) {
+      for (uint32_t g = threadIdx.x; g < (n >> 3); g += T) {
+        const uint32_t t = (g >> 6) & 1, sp = ((g >> 7) << 6) | (g & 63);
+        uint64_t *base = a + lp((sp << 4) + t);
+        uint64_t r[8];
+#pragma unroll
+        for (int m = 0; m < 8; m++) r[m] = base[lp(2 * m)];
+        dft8<INV>(r);
+        if (t) {
+#pragma unroll
+          for (int m = 1; m < 8; m++) r[m] = mul_w16_rt<INV>(r[m], (int)brev3(m));
+        }
+#pragma unroll
+        for (int m = 0; m < 8; m++) base[lp(2 * m)] = r[m];
+      }
+      __syncthreads();
+      log_S = 1;
+      break;
+    }
+    const uint32_t q = 1u << (log_S - 3), log_q = log_S - 3;
+    for (uint32_t g = threadIdx.x; g < (n >> 3); g += T) {
+      const uint32_t sp = g >> log_q, t = g & (q - 1);
+      uint64_t *base = a + lp((sp << log_S) + t);
+      uint64_t r[8];
+#pragma unroll
+      for (int m = 0; m < 8; m++) r[m] = base[lp(m * q)];
+      dft8<INV>(r);
+      if (t) {
+#pragma unroll
+        for (int m = 1; m < 8; m++) r[m] = mul(r[m], tw_pow(tw, t * brev3(m), log_S));
+      }
+#pragma unroll
+      for (int m = 0; m < 8; m++) base[lp(m * q)] = r[m];
+    }
+    __syncthreads();
+    log_S -= 3;
+  }
+  if (log_S == 1) tail<INV, 1>(a, n);
+  else if (log_S == 2) tail<INV, 2>(a, n);
 }
 
 }  // namespace nt

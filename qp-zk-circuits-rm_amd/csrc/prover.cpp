@@ -118,6 +118,7 @@ struct qp_prover {
   // device witness generation (witness.hip): schedule + per-proof slot values
   DevBuf wg_gens, wg_lvl, wg_wslot, wg_wslot_cm, wg_in_slots, wg_pi_slots, wg_vals, wg_in, wg_err, wg_pis;
   uint32_t wg_nslots = 0, wg_nin = 0, wg_nlev = 0;
+  bool quotient_rereads = false;
   uint64_t *h_in = nullptr;  // pinned [max_batch][wg_nin] commit() values
   std::vector<uint32_t> h_werr;
   std::vector<uint64_t> h_wpis;
@@ -351,6 +352,10 @@ int setup(qp_prover *P) {
   }
   TRY(hipStreamSynchronize(c->stream));
   P->proof_len = proof_size(P);
+  {
+    const char *qv = getenv("QPGPU_QUOTIENT");
+    P->quotient_rereads = qv && !strcmp(qv, "rereads");
+  }
   unsigned hw = std::thread::hardware_concurrency();
   unsigned nthreads = std::min<unsigned>(hw ? hw : 4, 16);
   P->pool.reset(new qh::ThreadPool(nthreads > 1 ? nthreads - 1 : 0));
@@ -529,7 +534,10 @@ int prove_batch(qp_prover *P, const uint64_t *d_wires, const uint64_t *const *wi
     a.num_constants = P->NC;
     a.g = P->gdesc;
     kt_begin(P, 3);
-    qpk::k_quotient<2><<<dim3(cdiv(N, 256), nb), 256, 0, s>>>(a);
+    if (P->quotient_rereads)  // A/B: the round-1 kernel (QPGPU_QUOTIENT=rereads)
+      qpk::k_quotient<2><<<dim3(cdiv(N, 256), nb), 256, 0, s>>>(a);
+    else
+      qpk::k_quotient_1r<<<dim3(cdiv(N, 256), nb), 256, 0, s>>>(a);
     kt_end(P, 3, (double)nb * N);
     const uint64_t n_inv = gl::inv(n);
     qpk::k_qintt_blocks<<<dim3(B, nc, nb), 512, 8u * qpk::ntt_lds_words(1u << P->log_n), s>>>(P->qvals.p, P->cbuf.p, P->log_n, P->rate_bits,

@@ -50,6 +50,7 @@ __global__ void k_z_scan(const uint64_t *prods, uint64_t *zs, uint32_t log_n, ui
                          uint64_t p_bstride, uint64_t z_bstride);
 template <int PH>
 __global__ void k_quotient(QuotientArgs a);
+__global__ void k_quotient_1r(QuotientArgs a);
 __global__ void k_qintt_blocks(const uint64_t *vals, uint64_t *out, uint32_t log_n, uint32_t rate_bits,
                                uint64_t v_bstride, uint64_t o_bstride, const uint64_t *tw, const uint64_t *tw_inv,
                                uint64_t n_inv, uint64_t ginv);

@@ -324,6 +324,165 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(QP_QUO
     q[N + t] = gfn::canon(gfn::mul(acc1, zh_inv));
   }
 }
+// Single-read form (the default): every LDE column is read once per point,
+// wires 0..23 a second time by the Poseidon gate (its inputs and outputs).
+// While wires 0..R-1 stream by, the permutation checks of BOTH challenges
+// (sigma columns read once), and the Constant, PublicInput, BaseSum and
+// Arithmetic constraints accumulate, each term at its own alpha power (the
+// alpha-weighted sums do not depend on evaluation order); then the Poseidon
+// gate.  Per point: 135 + 24 wire, 84 constants/sigmas and 20 + 2 zs reads
+// against 241 distinct values (the PH 2 form re-read the wires per challenge
+// and per gate: 3.0x the algorithmic HBM bytes, profiles/r01_v5_pmc_hbm_b128.json).
+__device__ __forceinline__ void emit_at(const uint64_t *__restrict__ p0, const uint64_t *__restrict__ p1, uint32_t i,
+                                        uint64_t t, uint64_t &s0, uint64_t &s1) {
+  s0 = gfn::add(s0, gfn::mul(t, p0[i]));
+  s1 = gfn::add(s1, gfn::mul(t, p1[i]));
+}
+
+// x * 2^e, 0 <= e < 64, x in [0, 2^64) -> [0, 2^64)
+__device__ __forceinline__ uint64_t mul_pow2_rt(uint64_t x, uint32_t e) {
+  return e ? gfn::reduce(x << e, x >> (64 - e)) : x;
+}
+
+__global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(QP_QUOTIENT_WAVES)))
+k_quotient_1r(QuotientArgs a) {
+  const uint32_t logN = a.log_n + a.rate_bits;
+  const uint64_t N = 1ull << logN;
+  const uint32_t t = blockIdx.x * blockDim.x + threadIdx.x;
+  if (t >= N) return;
+  const uint32_t b = blockIdx.y;
+  const uint64_t *ch = a.chal + b * CHAL_STRIDE;
+  const uint64_t *cs = a.cs_lde + t;                       // [ncs][N]
+  const uint64_t *wl = a.w_lde + b * a.w_bstride + t;      // [W][N]
+  const uint64_t *zl = a.z_lde + b * a.z_bstride;          // [nzs][N]
+  const uint32_t j = gl::rev_bits(t, logN);
+  uint64_t *q = a.q_out + b * a.q_bstride;
+  const uint64_t *p0 = a.apow + (uint64_t)b * 2 * APOW_STRIDE, *p1 = p0 + APOW_STRIDE;
+  const uint32_t R = a.R, qdf = a.qdf, nchunks = (R + qdf - 1) / qdf, npp = nchunks - 1;
+  const uint32_t tn = gl::rev_bits((j + (1u << a.rate_bits)) & (uint32_t)(N - 1), logN);
+  const uint32_t nsel = a.g.nsel;
+  const uint64_t *gc = cs + (uint64_t)nsel * N;  // gate-constant columns
+  // gates of the circuit by kind (kernel arguments: uniform)
+  int g_const = -1, g_pi = -1, g_bs = -1, g_ar = -1, g_pos = -1;
+  for (uint32_t gi = 0; gi < a.g.ngates; gi++) {
+    switch (a.g.kind[gi]) {
+      case GK_CONSTANT: g_const = (int)gi; break;
+      case GK_PUBLIC_INPUT: g_pi = (int)gi; break;
+      case GK_BASE_SUM: g_bs = (int)gi; break;
+      case GK_ARITHMETIC: g_ar = (int)gi; break;
+      case GK_POSEIDON: g_pos = (int)gi; break;
+      default: break;
+    }
+  }
+  const uint32_t pre = 2 * (1 + nchunks);
+  const uint32_t n_const = g_const >= 0 ? a.g.param[g_const] : 0;
+  const uint32_t n_pi = g_pi >= 0 ? 4 : 0;
+  const uint32_t L = g_bs >= 0 ? a.g.param[g_bs] : 0;
+  const uint32_t n_ar = g_ar >= 0 ? a.g.param[g_ar] : 0;
+  // vanishing terms 0..pre-1 go straight into the totals
+  uint64_t acc0 = 0, acc1 = 0;
+  const uint64_t x = a.xtab[t], l0 = a.l0tab[t];
+  uint64_t z[2], prev[2];
+  for (uint32_t c = 0; c < 2; c++) {
+    z[c] = zl[(uint64_t)c * N + t];
+    prev[c] = z[c];
+    emit_at(p0, p1, c, gfn::mul(l0, gfn::sub(z[c], 1)), acc0, acc1);
+  }
+  const uint64_t beta0 = ch[CH_BETA], beta1 = ch[CH_BETA + 1], gamma0 = ch[CH_GAMMA], gamma1 = ch[CH_GAMMA + 1];
+  uint64_t bkx0 = gfn::mul(beta0, x), bkx1 = gfn::mul(beta1, x);
+  uint64_t num0 = 1, den0 = 1, num1 = 1, den1 = 1;
+  // per-gate alpha sums (multiplied by the gate's filter at the end)
+  uint64_t sc0 = 0, sc1 = 0, sp0 = 0, sp1 = 0, sb0 = 0, sb1 = 0, sa0 = 0, sa1 = 0;
+  uint64_t bs_acc = 0, w0 = 0, wa0 = 0, wa1 = 0, wa2 = 0;
+  for (uint32_t jj = 0; jj < R; jj++) {
+    const uint64_t w = WV(jj);
+    // permutation argument, both challenges (k_j = g^j folded into bkx)
+    const uint64_t sg = cs[(uint64_t)(a.num_constants + jj) * N];
+    num0 = gfn::mul(num0, gfn::add(gfn::add_c(w, gamma0), bkx0));
+    den0 = gfn::mul(den0, gfn::add(gfn::add_c(w, gamma0), gfn::mul(beta0, sg)));
+    num1 = gfn::mul(num1, gfn::add(gfn::add_c(w, gamma1), bkx1));
+    den1 = gfn::mul(den1, gfn::add(gfn::add_c(w, gamma1), gfn::mul(beta1, sg)));
+    bkx0 = gfn::mul(bkx0, gl::GEN);
+    bkx1 = gfn::mul(bkx1, gl::GEN);
+    if ((jj + 1) % qdf == 0 || jj + 1 == R) {
+      const uint32_t k = jj / qdf;
+      for (uint32_t c = 0; c < 2; c++) {
+        const uint64_t nx = k == nchunks - 1 ? zl[(uint64_t)c * N + tn] : zl[((uint64_t)2 + c * npp + k) * N + t];
+        const uint64_t num = c ? num1 : num0, den = c ? den1 : den0;
+        emit_at(p0, p1, 2 + c * nchunks + k, gfn::sub(gfn::mul(prev[c], num), gfn::mul(nx, den)), acc0, acc1);
+        prev[c] = nx;
+      }
+      num0 = den0 = num1 = den1 = 1;
+    }
+    if (jj < n_const) emit_at(p0, p1, pre + jj, gfn::sub(gc[(uint64_t)jj * N], w), sc0, sc1);
+    if (jj < n_pi) emit_at(p0, p1, pre + jj, gfn::sub(w, ch[CH_PIH + jj]), sp0, sp1);
+    if (L) {
+      if (jj == 0) {
+        w0 = w;
+      } else if (jj <= L) {
+        bs_acc = gfn::add(bs_acc, mul_pow2_rt(w, jj - 1));
+        emit_at(p0, p1, pre + jj, gfn::mul(w, gfn::sub(w, 1)), sb0, sb1);
+        if (jj == L) emit_at(p0, p1, pre, gfn::sub(bs_acc, w0), sb0, sb1);
+      }
+    }
+    if (jj < 4 * n_ar) {
+      switch (jj & 3) {
+        case 0: wa0 = w; break;
+        case 1: wa1 = w; break;
+        case 2: wa2 = w; break;
+        default: {
+          const uint64_t comp = gfn::add(gfn::mul(gfn::mul(wa0, wa1), gc[0]), gfn::mul(wa2, gc[N]));
+          emit_at(p0, p1, pre + jj / 4, gfn::sub(w, comp), sa0, sa1);
+        }
+      }
+    }
+  }
+  // selector filters: prod_{j in group, j != gate}(j - s) * (UNUSED - s)
+  auto filter = [&](int gi) -> uint64_t {
+    const uint32_t si = a.g.sel_index[gi];
+    const uint64_t sv = cs[(uint64_t)si * N];
+    uint64_t f = 1;
+    for (uint32_t jg = a.g.grp_lo[si]; jg < a.g.grp_hi[si]; jg++)
+      if (jg != (uint32_t)gi) f = gfn::mul(f, gfn::sub(jg, sv));
+    if (nsel > 1) f = gfn::mul(f, gfn::sub(0xFFFFFFFFull, sv));
+    return f;
+  };
+  if (g_const >= 0) {
+    const uint64_t f = filter(g_const);
+    acc0 = gfn::add(acc0, gfn::mul(f, sc0));
+    acc1 = gfn::add(acc1, gfn::mul(f, sc1));
+  }
+  if (g_pi >= 0) {
+    const uint64_t f = filter(g_pi);
+    acc0 = gfn::add(acc0, gfn::mul(f, sp0));
+    acc1 = gfn::add(acc1, gfn::mul(f, sp1));
+  }
+  if (g_bs >= 0) {
+    const uint64_t f = filter(g_bs);
+    acc0 = gfn::add(acc0, gfn::mul(f, sb0));
+    acc1 = gfn::add(acc1, gfn::mul(f, sb1));
+  }
+  if (g_ar >= 0) {
+    const uint64_t f = filter(g_ar);
+    acc0 = gfn::add(acc0, gfn::mul(f, sa0));
+    acc1 = gfn::add(acc1, gfn::mul(f, sa1));
+  }
+  if (g_pos >= 0) {
+    TermAcc A;
+    A.p0 = p0;
+    A.p1 = p1;
+    A.s0 = A.s1 = 0;
+    A.i = pre;
+    poseidon_gate(wl, N, A);
+    const uint64_t f = filter(g_pos);
+    acc0 = gfn::add(acc0, gfn::mul(f, A.s0));
+    acc1 = gfn::add(acc1, gfn::mul(f, A.s1));
+  }
+  const uint64_t zh_inv = a.zh_inv[j & ((1u << a.rate_bits) - 1)];
+  q[t] = gfn::canon(gfn::mul(acc0, zh_inv));
+  q[N + t] = gfn::canon(gfn::mul(acc1, zh_inv));
+}
+
 template __global__ void k_quotient<0>(QuotientArgs);
 template __global__ void k_quotient<1>(QuotientArgs);
 template __global__ void k_quotient<2>(QuotientArgs);
