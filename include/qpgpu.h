@@ -215,6 +215,74 @@ int qp_prover_kernel_stats(qp_prover *p, double *ms, double *units, uint64_t *la
  * inputs (host), [9] device witness generation; reset != 0 clears */
 int qp_prover_stage_times(qp_prover *p, double *ms, uint32_t n, int reset);
 
+/* ---- routine-level seams ---------------------------------
+ * The pieces of plonky2's prove() (qp-plonky2 1.1.1 plonk/prover.rs,
+ * fri/prover.rs) a patched crate routes to the GPU for ANY circuit over the
+ * supported gate set — e.g. the aggregator's per-chunk circuits
+ * (wormhole/aggregator/src/circuits/tree.rs:127-136), which the built-in
+ * circuit path does not cover.  The Fiat-Shamir transcript stays with the
+ * caller (INTEGRATION.md shows the call sequence).                            */
+
+/* gate kinds of CommonCircuitData.gates (DefaultGateSerializer ids 9, 3, 12, 2, 0, 11) */
+enum { QP_GATE_NOOP = 0, QP_GATE_CONSTANT = 1, QP_GATE_PUBLIC_INPUT = 2, QP_GATE_BASE_SUM = 3,
+       QP_GATE_ARITHMETIC = 4, QP_GATE_POSEIDON = 5 };
+
+/* the parts of CommonCircuitData the vanishing polynomial reads */
+typedef struct {
+    uint32_t num_gates;            /* <= 8, in CommonCircuitData.gates order */
+    uint32_t kind[8];              /* QP_GATE_* */
+    uint32_t param[8];             /* ConstantGate num_consts / BaseSumGate num_limbs / ArithmeticGate num_ops */
+    uint32_t selector_index[8];    /* selectors_info.selector_indices */
+    uint32_t num_selectors;        /* selectors_info.groups.len() */
+    uint32_t group_lo[8], group_hi[8];
+    uint32_t num_constants;        /* selectors + gate constants */
+    uint32_t num_routed_wires, num_wires, quotient_degree_factor, num_challenges, num_gate_constraints;
+} qp_gate_desc;
+
+/* fill a qp_gate_desc from a built circuit of this library */
+int qp_circuit_gate_desc(const qp_circuit *c, qp_gate_desc *g);
+
+/* compute_quotient_polys (plonk/prover.rs): vanishing polynomial at every
+ * point of the LDE coset from the committed batches (constants||sigmas, wires,
+ * zs||partial products; qp_commit_values batches of one, kept), alpha-reduced
+ * per challenge, divided by Z_H, coset-iFFT'd and split:
+ * quotient_coeffs_out [num_challenges * quotient_degree_factor][n].
+ * betas/gammas/alphas [num_challenges] (num_challenges == 2), pi_hash =
+ * hash_no_pad(public inputs).  Replaces prover.rs:compute_quotient_polys as
+ * reached from CircuitData::prove (tree.rs:136, lib.rs:233-237).            */
+int qp_quotient(qp_ctx *ctx, const qp_batch *cs, const qp_batch *wires, const qp_batch *zs_pp, const qp_gate_desc *g,
+                const uint64_t *betas, const uint64_t *gammas, const uint64_t *alphas, const uint64_t pi_hash[4],
+                uint64_t *quotient_coeffs_out);
+
+/* one reduction layer of fri_committed_trees (fri/prover.rs): values =
+ * coeffs.coset_fft(shift) of size 2^log_values, reverse_index_bits, leaves of
+ * 2^arity_bits ext values, MerkleTree -> cap_out [2^cap_height][4].  coeffs are
+ * ext coefficients as two rows [2][2^log_coeffs] (c0, c1); the reference keeps
+ * them full length with a zero tail, so log_coeffs may equal log_values: only
+ * the nonzero prefix (at most 2^13 coefficients) is transformed.  The caller
+ * observes the cap, draws beta and calls qp_fri_fold; out (optional) keeps the
+ * layer for qp_fri_layer_open in the query rounds.                          */
+typedef struct qp_fri_layer qp_fri_layer;
+int qp_fri_layer_commit(qp_ctx *ctx, const uint64_t *coeffs, uint32_t log_coeffs, uint32_t log_values, uint64_t shift,
+                        uint32_t arity_bits, uint32_t cap_height, uint64_t *cap_out, qp_fri_layer **out);
+/* leaf evals_out [nidx][2^arity_bits][2] (ext, c0 c1) and Merkle siblings
+ * [nidx][log_leaves - cap_height][4] of layer leaves idx[]                 */
+int qp_fri_layer_open(qp_fri_layer *layer, const uint32_t *idx, uint32_t nidx, uint64_t *evals_out,
+                      uint64_t *siblings_out);
+void qp_fri_layer_free(qp_fri_layer *layer);
+/* coeffs_out[k] = sum_{i < 2^arity_bits} beta^i coeffs[2^arity_bits k + i]
+ * (reduce_with_powers over chunks), ext rows [2][2^(log_coeffs - arity_bits)] */
+int qp_fri_fold(qp_ctx *ctx, const uint64_t *coeffs, uint32_t log_coeffs, uint32_t arity_bits, const uint64_t beta[2],
+                uint64_t *coeffs_out);
+
+/* fri_proof_of_work (fri/prover.rs) for n transcripts: states [n][12] are the
+ * duplex intermediate states (sponge_state with the pending input_buffer
+ * written into lanes 0..pos-1), pos[b] = input_buffer.len() < 8.  Returns the
+ * MINIMAL witness w with leading_zeros(permute(state with lane pos = w)[7])
+ * >= pow_bits (the reference's rayon find_any returns any such w).         */
+int qp_pow_grind(qp_ctx *ctx, const uint64_t *states, const uint32_t *pos, uint32_t n, uint32_t pow_bits,
+                 uint64_t *witness_out);
+
 #ifdef __cplusplus
 }
 #endif

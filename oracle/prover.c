@@ -76,6 +76,77 @@ static void batch_inv(gl_t *v, size_t n) {
     free(pre);
 }
 
+/* compute_quotient_polys (plonk/prover.rs): the vanishing polynomial at every
+ * point of the LDE coset from the leaf-order rows of the three committed
+ * batches (constants||sigmas, wires, zs||partial products), alpha-reduced per
+ * challenge, divided by Z_H, coset-iFFT'd and split: qcoeffs [nc*qdf][n]. */
+static void quotient_coeffs(const or_common_t *cp, unsigned log_n, const gl_t *cs_leaves, const gl_t *w_leaves,
+                            const gl_t *z_leaves, const gl_t *betas, const gl_t *gammas, const gl_t *alphas,
+                            const gl_t *pih, gl_t *qcoeffs) {
+    const or_common_t c = *cp;
+    const unsigned rb = (unsigned)c.fri_params_config.rate_bits;
+    const size_t n = (size_t)1 << log_n, N = n << rb;
+    const unsigned logN = log_n + rb;
+    const unsigned nc = (unsigned)c.num_challenges, R = (unsigned)c.num_routed_wires, W = (unsigned)c.num_wires;
+    const unsigned NCONST = (unsigned)c.num_constants, npp = (unsigned)c.num_partial_products;
+    const unsigned qdf = (unsigned)c.quotient_degree_factor;
+    const unsigned ncs = NCONST + R, nzs = nc * (1 + npp);
+    gl_t *qvals = malloc((size_t)nc * N * sizeof(gl_t)); /* natural point order */
+    {
+        const gl_t wN = gl_root_of_unity(logN);
+        const unsigned nterms = nc + nc * (npp + 1) + (unsigned)c.num_gate_constraints;
+        const unsigned nchunks = (R + qdf - 1) / qdf;
+        /* 1/(x^n - 1) is 2^rb-periodic: x^n = g^n w_N^{i n} */
+        gl_t zh_inv[64];
+        for (size_t i = 0; i < ((size_t)1 << rb); i++)
+            zh_inv[i] = gl_inv(gl_sub(gl_pow(gl_mul(GL_GEN, gl_pow(wN, i)), n), 1));
+        const gl_t ninv = gl_inv(gl_from_u64(n));
+#pragma omp parallel for schedule(static)
+        for (size_t i = 0; i < N; i++) {
+            gl_t terms[512];
+            gl_t x = gl_mul(GL_GEN, gl_pow(wN, i));
+            size_t li = rev_bits(i, logN), lin = rev_bits((i + ((size_t)1 << rb)) % N, logN);
+            const gl_t *lc = cs_leaves + li * ncs;
+            const gl_t *lw = w_leaves + li * W;
+            const gl_t *lz = z_leaves + li * nzs;
+            const gl_t *lzn = z_leaves + lin * nzs;
+            unsigned k = 0;
+            gl_t zh = gl_sub(gl_pow(x, n), 1);
+            gl_t l0 = gl_mul(zh, gl_inv(gl_mul(gl_sub(x, 1), gl_from_u64(n))));
+            (void)ninv;
+            for (unsigned ch = 0; ch < nc; ch++) terms[k++] = gl_mul(l0, gl_sub(lz[ch], 1));
+            for (unsigned ch = 0; ch < nc; ch++) {
+                const gl_t *pp = lz + nc + ch * npp;
+                for (unsigned ck = 0; ck < nchunks; ck++) {
+                    gl_t num = 1, den = 1;
+                    for (unsigned j = ck * qdf; j < (ck + 1) * qdf && j < R; j++) {
+                        num = gl_mul(num, gl_add(gl_add(lw[j], gl_mul(betas[ch], gl_mul(c.k_is[j], x))), gammas[ch]));
+                        den = gl_mul(den, gl_add(gl_add(lw[j], gl_mul(betas[ch], lc[NCONST + j])), gammas[ch]));
+                    }
+                    gl_t prev = ck == 0 ? lz[ch] : pp[ck - 1];
+                    gl_t next = ck == nchunks - 1 ? lzn[ch] : pp[ck];
+                    terms[k++] = gl_sub(gl_mul(prev, num), gl_mul(next, den));
+                }
+            }
+            or_eval_gate_constraints_base(&c, lc, lw, pih, terms + k);
+            k += (unsigned)c.num_gate_constraints;
+            (void)nterms;
+            gl_t zi = zh_inv[i & (((size_t)1 << rb) - 1)];
+            for (unsigned ch = 0; ch < nc; ch++) {
+                gl_t acc = 0;
+                for (unsigned j = k; j-- > 0;) acc = gl_add(gl_mul(acc, alphas[ch]), terms[j]);
+                qvals[(size_t)ch * N + i] = gl_mul(acc, zi);
+            }
+        }
+    }
+    for (unsigned ch = 0; ch < nc; ch++) {
+        or_coset_ifft(qvals + (size_t)ch * N, logN, GL_GEN);
+        for (unsigned j = 0; j < qdf; j++)
+            memcpy(qcoeffs + ((size_t)ch * qdf + j) * n, qvals + (size_t)ch * N + (size_t)j * n, n * sizeof(gl_t));
+    }
+    free(qvals);
+}
+
 int or_prove(const uint8_t *common_bytes, size_t clen, const gl_t *consts_sigmas, const gl_t *wires,
              const gl_t *pis, size_t npis, uint8_t *proof_out, size_t out_cap, size_t *out_len,
              gl_t *cs_cap_out, gl_t *digest_out) {
@@ -172,61 +243,8 @@ int or_prove(const uint8_t *common_bytes, size_t clen, const gl_t *consts_sigmas
     for (unsigned i = 0; i < nc; i++) alphas[i] = or_chal_get(&t);
 
     /* 3. quotient polys (plonk/prover.rs compute_quotient_polys) */
-    gl_t *qvals = malloc((size_t)nc * N * sizeof(gl_t)); /* natural point order */
-    {
-        const gl_t wN = gl_root_of_unity(logN);
-        const unsigned nterms = nc + nc * (npp + 1) + (unsigned)c.num_gate_constraints;
-        const unsigned nchunks = (R + qdf - 1) / qdf;
-        /* 1/(x^n - 1) is 2^rb-periodic: x^n = g^n w_N^{i n} */
-        gl_t zh_inv[64];
-        for (size_t i = 0; i < ((size_t)1 << rb); i++)
-            zh_inv[i] = gl_inv(gl_sub(gl_pow(gl_mul(GL_GEN, gl_pow(wN, i)), n), 1));
-        const gl_t ninv = gl_inv(gl_from_u64(n));
-#pragma omp parallel for schedule(static)
-        for (size_t i = 0; i < N; i++) {
-            gl_t terms[512];
-            gl_t x = gl_mul(GL_GEN, gl_pow(wN, i));
-            size_t li = rev_bits(i, logN), lin = rev_bits((i + ((size_t)1 << rb)) % N, logN);
-            const gl_t *lc = bcs.leaves + li * ncs;
-            const gl_t *lw = bw.leaves + li * W;
-            const gl_t *lz = bz.leaves + li * nzs;
-            const gl_t *lzn = bz.leaves + lin * nzs;
-            unsigned k = 0;
-            gl_t zh = gl_sub(gl_pow(x, n), 1);
-            gl_t l0 = gl_mul(zh, gl_inv(gl_mul(gl_sub(x, 1), gl_from_u64(n))));
-            (void)ninv;
-            for (unsigned ch = 0; ch < nc; ch++) terms[k++] = gl_mul(l0, gl_sub(lz[ch], 1));
-            for (unsigned ch = 0; ch < nc; ch++) {
-                const gl_t *pp = lz + nc + ch * npp;
-                for (unsigned ck = 0; ck < nchunks; ck++) {
-                    gl_t num = 1, den = 1;
-                    for (unsigned j = ck * qdf; j < (ck + 1) * qdf && j < R; j++) {
-                        num = gl_mul(num, gl_add(gl_add(lw[j], gl_mul(betas[ch], gl_mul(c.k_is[j], x))), gammas[ch]));
-                        den = gl_mul(den, gl_add(gl_add(lw[j], gl_mul(betas[ch], lc[NCONST + j])), gammas[ch]));
-                    }
-                    gl_t prev = ck == 0 ? lz[ch] : pp[ck - 1];
-                    gl_t next = ck == nchunks - 1 ? lzn[ch] : pp[ck];
-                    terms[k++] = gl_sub(gl_mul(prev, num), gl_mul(next, den));
-                }
-            }
-            or_eval_gate_constraints_base(&c, lc, lw, pih, terms + k);
-            k += (unsigned)c.num_gate_constraints;
-            (void)nterms;
-            gl_t zi = zh_inv[i & (((size_t)1 << rb) - 1)];
-            for (unsigned ch = 0; ch < nc; ch++) {
-                gl_t acc = 0;
-                for (unsigned j = k; j-- > 0;) acc = gl_add(gl_mul(acc, alphas[ch]), terms[j]);
-                qvals[(size_t)ch * N + i] = gl_mul(acc, zi);
-            }
-        }
-    }
     gl_t *qcoeffs = malloc((size_t)nq * n * sizeof(gl_t));
-    for (unsigned ch = 0; ch < nc; ch++) {
-        or_coset_ifft(qvals + (size_t)ch * N, logN, GL_GEN);
-        for (unsigned j = 0; j < qdf; j++)
-            memcpy(qcoeffs + ((size_t)ch * qdf + j) * n, qvals + (size_t)ch * N + (size_t)j * n, n * sizeof(gl_t));
-    }
-    free(qvals);
+    quotient_coeffs(&c, log_n, bcs.leaves, bw.leaves, bz.leaves, betas, gammas, alphas, pih, qcoeffs);
     batch_from_coeffs(&bq, qcoeffs, nq, log_n, rb, cap_h);
     or_merkle_cap(bq.tree, p->quot_cap);
     or_chal_observe_n(&t, p->quot_cap, cap_len * 4);
@@ -376,4 +394,80 @@ int or_prove(const uint8_t *common_bytes, size_t clen, const gl_t *consts_sigmas
     }
     or_proof_free(p);
     return rc;
+}
+
+/* qp_quotient checker: commits the three value batches like or_prove and
+ * returns quotient coefficients [nc*qdf][n] (plonk/prover.rs compute_quotient_polys) */
+int ora_quotient(const uint8_t *common_bytes, size_t clen, const gl_t *consts_sigmas, const gl_t *wires,
+                 const gl_t *zs_vals, const gl_t *betas, const gl_t *gammas, const gl_t *alphas, const gl_t *pih,
+                 gl_t *qcoeffs_out) {
+    or_common_t c;
+    size_t used;
+    if (or_parse_common(common_bytes, clen, &used, &c) || used != clen) return -1;
+    or_dims_t d;
+    or_dims(&c, &d);
+    const unsigned log_n = d.log_n, rb = (unsigned)c.fri_params_config.rate_bits;
+    const unsigned nc = (unsigned)c.num_challenges, R = (unsigned)c.num_routed_wires;
+    const unsigned ncs = (unsigned)c.num_constants + R, nzs = nc * (1 + (unsigned)c.num_partial_products);
+    batch_t bcs, bw, bz;
+    batch_from_values(&bcs, consts_sigmas, ncs, log_n, rb, 0);
+    batch_from_values(&bw, wires, (unsigned)c.num_wires, log_n, rb, 0);
+    batch_from_values(&bz, zs_vals, nzs, log_n, rb, 0);
+    quotient_coeffs(&c, log_n, bcs.leaves, bw.leaves, bz.leaves, betas, gammas, alphas, pih, qcoeffs_out);
+    batch_free(&bcs); batch_free(&bw); batch_free(&bz);
+    return 0;
+}
+
+/* one fri_committed_trees layer (fri/prover.rs): values = coset_fft(coeffs
+ * zero-padded to 2^log_values, shift), reverse_index_bits, leaves of 2^ab ext
+ * values; cap, and for leaf indices idx[] the leaf evals [2^ab][2] and siblings.
+ * coeffs is [2][2^log_coeffs] (c0 row, c1 row) like the C ABI. */
+int ora_fri_layer(const gl_t *coeffs, unsigned log_coeffs, unsigned log_values, gl_t shift, unsigned ab,
+                  unsigned cap_h, gl_t *cap_out, const uint32_t *idx, unsigned nidx, gl_t *evals_out,
+                  gl_t *sibs_out) {
+    if (log_coeffs > log_values || ab + cap_h > log_values) return -1;
+    const size_t Lc = (size_t)1 << log_coeffs, Lv = (size_t)1 << log_values;
+    glx_t *vals = calloc(Lv, sizeof(glx_t));
+    for (size_t i = 0; i < Lc; i++) vals[i] = glx(coeffs[i], coeffs[Lc + i]);
+    or_coset_fft_ext(vals, log_values, shift);
+    gl_t *leaves = malloc(Lv * 2 * sizeof(gl_t));
+    for (size_t j = 0; j < Lv; j++) {
+        glx_t v = vals[rev_bits(j, log_values)];
+        leaves[2 * j] = v.c0; leaves[2 * j + 1] = v.c1;
+    }
+    free(vals);
+    const size_t W = (size_t)2 << ab;
+    const unsigned depth = log_values - ab - cap_h;
+    or_merkle_t *t = or_merkle_build(leaves, log_values - ab, W, cap_h);
+    free(leaves);
+    or_merkle_cap(t, cap_out);
+    for (unsigned q = 0; q < nidx; q++) {
+        memcpy(evals_out + q * W, t->leaves + (size_t)idx[q] * W, W * sizeof(gl_t));
+        or_merkle_prove(t, idx[q], sibs_out + (size_t)q * depth * 4);
+    }
+    or_merkle_free(t);
+    return 0;
+}
+
+/* the coefficient fold of fri_committed_trees: chunks of 2^ab reduced with powers of beta */
+void ora_fri_fold(const gl_t *coeffs, unsigned log_coeffs, unsigned ab, const gl_t *beta, gl_t *out) {
+    const size_t L = (size_t)1 << log_coeffs, Lo = L >> ab, ar = (size_t)1 << ab;
+    const glx_t b = glx(beta[0], beta[1]);
+    for (size_t j = 0; j < Lo; j++) {
+        glx_t a = glx(0, 0);
+        for (size_t k = ar; k-- > 0;) a = glx_add(glx_mul(a, b), glx(coeffs[j * ar + k], coeffs[L + j * ar + k]));
+        out[j] = a.c0; out[Lo + j] = a.c1;
+    }
+}
+
+/* fri_proof_of_work: minimal witness for one duplex state (lanes 0..pos-1 hold
+ * the pending inputs) */
+gl_t ora_pow_grind(const gl_t *state, unsigned pos, unsigned bits) {
+    for (gl_t cand = 0;; cand++) {
+        gl_t s[12];
+        memcpy(s, state, sizeof(s));
+        s[pos] = cand;
+        ps_permute(s);
+        if ((s[7] >> (64 - bits)) == 0) return cand;
+    }
 }

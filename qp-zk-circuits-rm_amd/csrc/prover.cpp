@@ -127,6 +127,57 @@ struct qp_prover {
   }
 };
 
+namespace qpk {
+
+// proof-independent point tables of the quotient, leaf order t (point
+// x = g w_N^rev(t)): xtab[t] = x, l0tab[t] = L_0(x) = Z_H(x) / (n (x - 1))
+// (one batch inversion here instead of a field inversion per point per proof)
+std::vector<uint64_t> quotient_point_tables(uint32_t log_n, uint32_t rate_bits) {
+  const uint32_t logN = log_n + rate_bits;
+  const uint64_t n = 1ull << log_n, N = 1ull << logN;
+  const uint64_t wN = gl::root_of_unity(logN);
+  std::vector<uint64_t> tab(2 * N), den(N), pre(N);
+  for (uint64_t j = 0, w = 1; j < N; j++, w = gl::mul(w, wN)) {
+    const uint64_t t = gl::rev_bits((uint32_t)j, logN);
+    tab[t] = gl::mul(gl::GEN, w);
+    den[t] = gl::mul(gl::sub(tab[t], 1), n % gl::P);
+  }
+  uint64_t acc = 1;
+  for (uint64_t t = 0; t < N; t++) {
+    pre[t] = acc;
+    acc = gl::mul(acc, den[t]);
+  }
+  uint64_t inv = gl::inv(acc);
+  for (uint64_t t = N; t-- > 0;) {
+    const uint64_t dinv = gl::mul(inv, pre[t]);
+    inv = gl::mul(inv, den[t]);
+    const uint64_t zh = gl::sub(gl::pow(tab[t], n), 1);
+    tab[N + t] = gl::mul(zh, dinv);
+  }
+  return tab;
+}
+
+// PoW search state with the candidate at lane pos; round 0 of the permutation
+// is folded here: every lane but pos is candidate-independent, so
+//   state after round 0 (+ round-1 constants) = K + coef * sbox(cand + rc_pos)
+// with K[r] = sum_{j != pos} M[r][j] sbox(s_j + rc_j) + rc(1)_r and
+// coef[r] = M[r][pos] (a small circulant/diagonal entry): pre = K[12] || coef[12]
+void pow_prestate(const uint64_t st12[12], uint32_t pos, uint64_t pre[24]) {
+  uint64_t y[12];
+  for (uint32_t j = 0; j < 12; j++) y[j] = j == pos ? 0 : ps::sbox(gl::add(st12[j], ps::rc(j)));
+  for (uint32_t r = 0; r < 12; r++) {
+    uint64_t k = ps::rc(12 + r);
+    for (uint32_t j = 0; j < 12; j++) {
+      const uint64_t m = ps::mds_circ((j + 12 - r) % 12) + (r == 0 && j == 0 ? 8 : 0);
+      if (j != pos) k = gl::add(k, gl::mul(m, y[j]));
+      else pre[12 + r] = m;
+    }
+    pre[r] = k;
+  }
+}
+
+}  // namespace qpk
+
 namespace {
 
 #define TRY(expr)                                                              \
@@ -273,32 +324,9 @@ int setup(qp_prover *P) {
   TRY(P->pow_pos.alloc((B + 1) / 2));
   TRY(P->pow_active.alloc((B + 1) / 2));
   {
-    // proof-independent point tables of the quotient, leaf order t (point
-    // x = g w_N^rev(t)): xtab[t] = x, l0tab[t] = L_0(x) = Z_H(x) / (n (x - 1))
-    // (one batch inversion here instead of a field inversion per point per proof)
-    const uint32_t logN = P->log_n + P->rate_bits;
-    const uint64_t N = 1ull << logN;
-    const uint64_t wN = gl::root_of_unity(logN);
-    std::vector<uint64_t> tab(2 * N), den(N), pre(N);
-    for (uint64_t j = 0, w = 1; j < N; j++, w = gl::mul(w, wN)) {
-      const uint64_t t = gl::rev_bits((uint32_t)j, logN);
-      tab[t] = gl::mul(gl::GEN, w);
-      den[t] = gl::mul(gl::sub(tab[t], 1), n % gl::P);
-    }
-    uint64_t acc = 1;
-    for (uint64_t t = 0; t < N; t++) {
-      pre[t] = acc;
-      acc = gl::mul(acc, den[t]);
-    }
-    uint64_t inv = gl::inv(acc);
-    for (uint64_t t = N; t-- > 0;) {
-      const uint64_t dinv = gl::mul(inv, pre[t]);
-      inv = gl::mul(inv, den[t]);
-      const uint64_t zh = gl::sub(gl::pow(tab[t], n), 1);
-      tab[N + t] = gl::mul(zh, dinv);
-    }
-    TRY(P->qtab.alloc(2 * N));
-    TRY(hipMemcpy(P->qtab.p, tab.data(), 2 * N * 8, hipMemcpyHostToDevice));
+    std::vector<uint64_t> tab = qpk::quotient_point_tables(P->log_n, P->rate_bits);
+    TRY(P->qtab.alloc(tab.size()));
+    TRY(hipMemcpy(P->qtab.p, tab.data(), tab.size() * 8, hipMemcpyHostToDevice));
   }
   TRY(P->qidx.alloc(((size_t)B * P->nq + 1) / 2));
   {
@@ -672,27 +700,12 @@ int prove_batch(qp_prover *P, const uint64_t *d_wires, const uint64_t *const *wi
       S.t.observe(f0[i]);
       S.t.observe(f1[i]);
     }
-    // sponge state with the candidate at lane pos; round 0 of the permutation
-    // is folded here: every lane but pos is candidate-independent, so
-    //   state after round 0 (+ round-1 constants) = K + coef * sbox(cand + rc_pos)
-    // with K[r] = sum_{j != pos} M[r][j] sbox(s_j + rc_j) + rc(1)_r and
-    // coef[r] = M[r][pos] (a small circulant/diagonal entry)
+    // sponge state with the candidate at lane pos (round 0 folded on the host)
     uint64_t st12[12];
     memcpy(st12, S.t.state, 96);
     for (uint32_t i = 0; i < S.t.nin; i++) st12[i] = S.t.in[i];
     const uint32_t pos = S.t.nin;
-    uint64_t y[12];
-    for (uint32_t j = 0; j < 12; j++) y[j] = j == pos ? 0 : ps::sbox(gl::add(st12[j], ps::rc(j)));
-    uint64_t *pre = P->h_powst.data() + b * 24;
-    for (uint32_t r = 0; r < 12; r++) {
-      uint64_t k = ps::rc(12 + r);
-      for (uint32_t j = 0; j < 12; j++) {
-        const uint64_t m = ps::mds_circ((j + 12 - r) % 12) + (r == 0 && j == 0 ? 8 : 0);
-        if (j != pos) k = gl::add(k, gl::mul(m, y[j]));
-        else pre[12 + r] = m;
-      }
-      pre[r] = k;
-    }
+    qpk::pow_prestate(st12, pos, P->h_powst.data() + b * 24);
     P->h_pos[b] = pos;
   });
   TRY(hipMemcpyAsync(P->pow_state.p, P->h_powst.data(), (size_t)nb * 192, hipMemcpyHostToDevice, s));

@@ -5,7 +5,13 @@
 #include "kernels.h"
 #include "ntt_device.h"
 
+#include <vector>
+
 namespace qpk {
+
+// host helpers shared by the prover and the routine-level seams (prover.cpp)
+std::vector<uint64_t> quotient_point_tables(uint32_t log_n, uint32_t rate_bits);
+void pow_prestate(const uint64_t st12[12], uint32_t pos, uint64_t pre[24]);
 
 // per-proof challenge block (device, u64 words)
 enum : uint32_t {

@@ -5,12 +5,13 @@ Mirrors qp-wormhole-prover's WormholeProver (wormhole/prover/src/lib.rs:74-237)
 and plonky2's PolynomialBatch for the parity tests.  The HIP library is the
 only backend: importing the native pieces raises if it is not built.
 """
-from ._native import (Context, PolynomialBatch, QpError, header_symbols, ifft, lde, lib,  # noqa: F401
-                      poseidon_permute)
+from ._native import (Context, FriLayer, GateDesc, PolynomialBatch, QpError, fri_fold, gate_desc,  # noqa: F401
+                      header_symbols, ifft, lde, lib, poseidon_permute, pow_grind, quotient)
 
 from .circuits import (Circuit, CircuitInputs, PrivateCircuitInputs, ProcessedStorageProof,  # noqa: F401,E402
                        PublicCircuitInputs, VoteCircuitData, VotePrivateInputs, VotePublicInputs, Witness)
 from .prover import Prover, ProofWithPublicInputs, WormholeProver  # noqa: F401,E402
 
 __all__ = ["Circuit", "CircuitInputs", "PrivateCircuitInputs", "ProcessedStorageProof", "PublicCircuitInputs",
-           "Witness", "VoteCircuitData", "VotePrivateInputs", "VotePublicInputs", "Prover", "ProofWithPublicInputs", "WormholeProver", "Context", "PolynomialBatch", "QpError", "ifft", "lde", "poseidon_permute", "lib", "header_symbols"]
+           "Witness", "VoteCircuitData", "VotePrivateInputs", "VotePublicInputs", "Prover", "ProofWithPublicInputs", "WormholeProver", "Context", "PolynomialBatch", "QpError", "ifft", "lde", "poseidon_permute", "lib", "header_symbols",
+           "GateDesc", "gate_desc", "quotient", "FriLayer", "fri_fold", "pow_grind"]

@@ -22,6 +22,16 @@ STATUS = {0: "QP_OK", 1: "QP_ERR_ARG", 2: "QP_ERR_HIP", 3: "QP_ERR_OOM", 4: "QP_
           5: "QP_ERR_WITNESS", 6: "QP_ERR_FORMAT"}
 
 
+class GateDesc(ctypes.Structure):
+    """qp_gate_desc: the parts of CommonCircuitData the vanishing polynomial reads."""
+    _fields_ = [("num_gates", ctypes.c_uint32), ("kind", ctypes.c_uint32 * 8), ("param", ctypes.c_uint32 * 8),
+                ("selector_index", ctypes.c_uint32 * 8), ("num_selectors", ctypes.c_uint32),
+                ("group_lo", ctypes.c_uint32 * 8), ("group_hi", ctypes.c_uint32 * 8),
+                ("num_constants", ctypes.c_uint32), ("num_routed_wires", ctypes.c_uint32),
+                ("num_wires", ctypes.c_uint32), ("quotient_degree_factor", ctypes.c_uint32),
+                ("num_challenges", ctypes.c_uint32), ("num_gate_constraints", ctypes.c_uint32)]
+
+
 class QpError(RuntimeError):
     def __init__(self, code, msg=""):
         self.code = code
@@ -97,6 +107,14 @@ def lib():
         "qp_prover_kernel_stats": (ctypes.c_int, [VP, ctypes.POINTER(ctypes.c_double), ctypes.POINTER(ctypes.c_double),
                                                   ctypes.POINTER(ctypes.c_uint64), ctypes.c_uint32, ctypes.c_int]),
         "qp_prover_stage_times": (ctypes.c_int, [VP, ctypes.POINTER(ctypes.c_double), ctypes.c_uint32, ctypes.c_int]),
+        "qp_circuit_gate_desc": (ctypes.c_int, [VP, ctypes.POINTER(GateDesc)]),
+        "qp_quotient": (ctypes.c_int, [VP, VP, VP, VP, ctypes.POINTER(GateDesc), U64P, U64P, U64P, U64P, U64P]),
+        "qp_fri_layer_commit": (ctypes.c_int, [VP, U64P, ctypes.c_uint32, ctypes.c_uint32, ctypes.c_uint64,
+                                               ctypes.c_uint32, ctypes.c_uint32, U64P, PP]),
+        "qp_fri_layer_open": (ctypes.c_int, [VP, U32P, ctypes.c_uint32, U64P, U64P]),
+        "qp_fri_layer_free": (None, [VP]),
+        "qp_fri_fold": (ctypes.c_int, [VP, U64P, ctypes.c_uint32, ctypes.c_uint32, U64P, U64P]),
+        "qp_pow_grind": (ctypes.c_int, [VP, U64P, U32P, ctypes.c_uint32, ctypes.c_uint32, U64P]),
     }
     for name, (res, args) in sig.items():
         f = getattr(L, name)
@@ -233,3 +251,80 @@ def hash_no_pad(values):
     if rc:
         raise QpError(rc, "qp_hash_no_pad")
     return [int(x) for x in out]
+
+
+# ---- routine-level seams (include/qpgpu.h "routine-level seams") ----------
+
+def gate_desc(circuit):
+    """qp_circuit_gate_desc for a built Circuit."""
+    g = GateDesc()
+    rc = lib().qp_circuit_gate_desc(circuit.h, ctypes.byref(g))
+    if rc:
+        raise QpError(rc, "qp_circuit_gate_desc")
+    return g
+
+
+def _u64(v, n=None):
+    a = np.ascontiguousarray([int(x) for x in v] if not isinstance(v, np.ndarray) else v, dtype=np.uint64)
+    if n is not None and a.size != n:
+        raise ValueError(f"expected {n} values, got {a.size}")
+    return a
+
+
+def quotient(ctx, cs, wires, zs_pp, gd, betas, gammas, alphas, pi_hash):
+    """compute_quotient_polys: returns quotient coefficients [nc * qdf][n]."""
+    nc, qdf = gd.num_challenges, gd.quotient_degree_factor
+    out = np.zeros((nc * qdf, 1 << cs.log_n), np.uint64)
+    ctx.check(lib().qp_quotient(ctx.h, cs.h, wires.h, zs_pp.h, ctypes.byref(gd), _u64(betas, nc), _u64(gammas, nc),
+                                _u64(alphas, nc), _u64(pi_hash, 4), out), "qp_quotient")
+    return out
+
+
+class FriLayer:
+    """One committed FRI reduction layer (fri_committed_trees)."""
+
+    def __init__(self, ctx, coeffs, log_values, shift, arity_bits, cap_height):
+        c = np.ascontiguousarray(coeffs, dtype=np.uint64)
+        if c.ndim != 2 or c.shape[0] != 2:
+            raise ValueError("coeffs must be [2][2^k] (ext c0 row, c1 row)")
+        self.ctx, self.log_values, self.arity_bits, self.cap_height = ctx, log_values, arity_bits, cap_height
+        self.cap = np.zeros((1 << cap_height, 4), np.uint64)
+        h = ctypes.c_void_p()
+        ctx.check(lib().qp_fri_layer_commit(ctx.h, c, c.shape[1].bit_length() - 1, log_values, shift, arity_bits,
+                                            cap_height, self.cap, ctypes.byref(h)), "qp_fri_layer_commit")
+        self.h = h
+
+    def open(self, indices):
+        idx = np.ascontiguousarray(indices, dtype=np.uint32)
+        depth = self.log_values - self.arity_bits - self.cap_height
+        evals = np.zeros((len(idx), 1 << self.arity_bits, 2), np.uint64)
+        sibs = np.zeros((len(idx), depth, 4), np.uint64)
+        self.ctx.check(lib().qp_fri_layer_open(self.h, idx, len(idx), evals, sibs), "qp_fri_layer_open")
+        return evals, sibs
+
+    def free(self):
+        if self.h:
+            lib().qp_fri_layer_free(self.h)
+            self.h = None
+
+    def __del__(self):
+        try:
+            self.free()
+        except Exception:
+            pass
+
+
+def fri_fold(ctx, coeffs, arity_bits, beta):
+    c = np.ascontiguousarray(coeffs, dtype=np.uint64)
+    out = np.zeros((2, c.shape[1] >> arity_bits), np.uint64)
+    ctx.check(lib().qp_fri_fold(ctx.h, c, c.shape[1].bit_length() - 1, arity_bits, _u64(beta, 2), out), "qp_fri_fold")
+    return out
+
+
+def pow_grind(ctx, states, pos, pow_bits):
+    """fri_proof_of_work for n duplex states [n][12] with pending-input counts pos[n]."""
+    st = np.ascontiguousarray(states, dtype=np.uint64).reshape(-1, 12)
+    p = np.ascontiguousarray(pos, dtype=np.uint32)
+    out = np.zeros(st.shape[0], np.uint64)
+    ctx.check(lib().qp_pow_grind(ctx.h, st, p, st.shape[0], pow_bits, out), "qp_pow_grind")
+    return out

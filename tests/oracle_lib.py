@@ -53,6 +53,13 @@ def lib():
         L.ora_common_roundtrip.argtypes = [ctypes.c_char_p, ctypes.c_size_t, ctypes.c_char_p]
         L.ora_challenges.argtypes = [ctypes.c_char_p, ctypes.c_size_t, ctypes.c_char_p, ctypes.c_size_t, U64P]
         L.ora_circuit_digest.argtypes = [U64P, ctypes.c_size_t, ctypes.c_uint64, U64P]
+        L.ora_quotient.argtypes = [ctypes.c_char_p, ctypes.c_size_t, U64P, U64P, U64P, U64P, U64P, U64P, U64P, U64P]
+        L.ora_fri_layer.argtypes = [U64P, ctypes.c_uint, ctypes.c_uint, ctypes.c_uint64, ctypes.c_uint, ctypes.c_uint,
+                                    U64P, np.ctypeslib.ndpointer(np.uint32, flags="C_CONTIGUOUS"), ctypes.c_uint,
+                                    U64P, U64P]
+        L.ora_fri_fold.argtypes = [U64P, ctypes.c_uint, ctypes.c_uint, U64P, U64P]
+        L.ora_pow_grind.restype = ctypes.c_uint64
+        L.ora_pow_grind.argtypes = [U64P, ctypes.c_uint, ctypes.c_uint]
         _lib = L
     return _lib
 
