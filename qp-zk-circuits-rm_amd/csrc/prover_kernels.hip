@@ -691,6 +691,11 @@ __global__ void __launch_bounds__(256) k_fri_leaf(const uint64_t *__restrict__ v
   const uint64_t *c0 = vals + b * v_bstride + ((uint64_t)i << ab);
   const uint64_t *c1 = c0 + L;
   const uint32_t W = 2u << ab;
+  uint64_t *o = dig + b * d_bstride + (uint64_t)i * 4;
+  if (W <= 4) {  // hash_or_noop: a leaf of <= 4 elements is its own digest (arity 2)
+    o[0] = psd::canon(c0[0]); o[1] = psd::canon(c1[0]); o[2] = psd::canon(c0[1]); o[3] = psd::canon(c1[1]);
+    return;
+  }
   uint64_t s[12] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0};
   for (uint32_t off = 0; off < W; off += 8) {
 #pragma unroll
@@ -703,7 +708,6 @@ __global__ void __launch_bounds__(256) k_fri_leaf(const uint64_t *__restrict__ v
     }
     psd::permute_nc(s);
   }
-  uint64_t *o = dig + b * d_bstride + (uint64_t)i * 4;
   o[0] = psd::canon(s[0]); o[1] = psd::canon(s[1]); o[2] = psd::canon(s[2]); o[3] = psd::canon(s[3]);
 }
 

@@ -89,11 +89,11 @@ def test_quotient_rejects_bad_shapes(ctx, circuit):
 
 # (nonzero coefficients log, buffer log, values log, shift, arity bits, cap height)
 FRI_CASES = [
-    (13, 16, 16, G, 2, 4),            # wormhole layer 0: final poly of degree < n, zero tail to N
-    (11, 14, 14, gpow(G, 4), 2, 4),    # layer 1 (arity 4 = 2 bits)
-    (13, 13, 16, G, 4, 4),            # arity 16, unpadded buffer
+    (13, 16, 16, G, 4, 4),            # wormhole layer 0: degree < n, zero tail to N (arity 16)
+    (9, 12, 12, gpow(G, 16), 4, 4),    # wormhole layer 1
+    (13, 13, 16, G, 2, 4),            # arity 4, unpadded buffer
     (9, 9, 12, gpow(G, 16), 3, 2),
-    (3, 4, 6, 7, 1, 0),               # tiny: generic per-coset LDE path, cap height 0
+    (3, 4, 6, 7, 1, 0),               # arity 2: hash_or_noop leaves; generic per-coset LDE; cap height 0
     (1, 1, 5, G, 2, 3),
 ]
 
