@@ -37,10 +37,10 @@ HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec peak (MI355X_MICROARCH.md)
 # HBM traffic of the roofline kernel from rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE
 # passes (tools/pmc_summary.py applies the gfx950 corrections); per proof, scaled
 # to the bench's per-launch proof count
-PMC_FILE = os.path.join(ROOT, "profiles", "r01_v5_pmc_hbm_b128.json")
+PMC_FILE = os.path.join(ROOT, "profiles", "r02_pmc_hbm_b128.json")
 
 
-def pmc_traffic(kernel, ncols, log_n, proofs):
+def pmc_traffic(kernel, ncols, log_n, proofs, lanes_per_proof=None):
     """HBM bytes per launch of `kernel` for `proofs` proofs of `ncols` columns, or None."""
     try:
         recs = json.load(open(PMC_FILE))
@@ -49,7 +49,8 @@ def pmc_traffic(kernel, ncols, log_n, proofs):
     for r in recs:
         if r.get("kernel") != kernel or not r.get("hbm_bytes"):
             continue
-        lanes_per_proof = ncols * (1 << log_n) // 16  # one 2^(log_n - 4)-lane workgroup per column
+        if lanes_per_proof is None:
+            lanes_per_proof = ncols * (1 << log_n) // 16  # one 2^(log_n - 4)-lane workgroup per column
         if r["grid_lanes"] % lanes_per_proof:
             continue
         return r["hbm_bytes"] / (r["grid_lanes"] // lanes_per_proof) * proofs
@@ -275,13 +276,18 @@ def main():
                                                 per[0]) if circuit.degree_bits == 13 else None,
                          "traffic_unit": "bytes per launch",
                          "algorithmic_bytes_per_launch": lde["units"] / max(lde["launches"], 1),
-                         "traffic_source": "profiles/r01_v5_pmc_hbm_b128.json (rocprofv3 --pmc FETCH_SIZE, WRITE_SIZE "
+                         "traffic_source": "profiles/r02_pmc_hbm_b128.json (rocprofv3 --pmc FETCH_SIZE, WRITE_SIZE "
                                            "passes of this bench at batch 128), per proof x proofs per launch",
                          "avg_launch_ms": lde["ms"] / max(lde["launches"], 1),
                          "note": "HIP events on the prover stream around each launch of the kernel"},
             "valu_kernels": {"leaf_hash_wires_perms_per_s": leaf["units"] / (leaf["ms"] * 1e-3) if leaf["ms"] else None,
                              "avg_launch_ms": leaf["ms"] / max(leaf["launches"], 1),
-                             "quotient_avg_launch_ms": ks["quotient"]["ms"] / max(ks["quotient"]["launches"], 1)},
+                             "quotient_avg_launch_ms": ks["quotient"]["ms"] / max(ks["quotient"]["launches"], 1),
+                             # k_quotient_1r: one lane per LDE point; algorithmic = 8 (241 reads + 2 writes) per point
+                             "quotient_hbm_bytes_per_launch": pmc_traffic(
+                                 "qpk::k_quotient_1r", 0, 0, per[0], lanes_per_proof=8 << circuit.degree_bits)
+                             if circuit.degree_bits == 13 else None,
+                             "quotient_algorithmic_bytes_per_launch": per[0] * 8 * 243 * (8 << circuit.degree_bits)},
             "stage_ms_per_step": {k: v / args.steps for k, v in stages.items()},
             "proof_bytes": len(proofs[0]),
             "latency_1proof_ms": lat,

@@ -511,7 +511,7 @@ int prove_batch(qp_prover *P, const uint64_t *d_wires, const uint64_t *const *wi
   const uint64_t pbs = (uint64_t)nc * P->nchunks * n;
   qpk::k_pp_rows<<<dim3(cdiv(n, 256), nb), 256, 0, s>>>(wv, P->sigmas.p, P->kis.p, P->chal.p, P->prods.p,
                                                          P->log_n, P->R, P->qdf, nc, P->wires.cbs(), pbs, c->tw.fwd);
-  qpk::k_z_scan<<<dim3(nc, nb), 1024, 0, s>>>(P->prods.p, P->zs.vals.p, P->log_n, nc, P->nchunks, pbs, P->zs.cbs());
+  qpk::k_z_scan<<<dim3(nc, nb), 1024, 8u * (qpk::ntt_lds_words(n) + 1024), s>>>(P->prods.p, P->zs.vals.p, P->log_n, nc, P->nchunks, pbs, P->zs.cbs());
   P->zs.build_from_values(c, nb);
   TRY(hipGetLastError());
   if ((rc = fetch_caps(P, P->zs.dig.p, P->zs.dbs(), logN, nb))) return rc;
@@ -675,7 +675,8 @@ int prove_batch(qp_prover *P, const uint64_t *d_wires, const uint64_t *const *wi
       if ((rc = push_chal(P, nb))) return rc;
       // fold: next coefficients (length 2^(lg-ab)); only the low 2^(coef_log-ab) can be nonzero
       qpk::k_fold<<<dim3(cdiv(1ull << (lg - ab), 256), nb), 256, 0, s>>>(coef, P->fcoef[l].p, lg, ab, (uint32_t)l,
-                                                                        P->chal.p, coef_bs, 2ull << (lg - ab));
+                                                                        P->chal.p, coef_bs, 2ull << (lg - ab),
+                                                                        coef_log);
       TRY(hipGetLastError());
       coef = P->fcoef[l].p;
       lg -= ab;

@@ -79,36 +79,48 @@ __global__ void __launch_bounds__(256) k_pp_rows(const uint64_t *__restrict__ wi
   }
 }
 
-// exclusive prefix product of the full-row products -> Z; pp_j = Z * P_j
+// exclusive prefix product of the full-row products -> Z; pp_j = Z * P_j.
+// The row products go through LDS (coalesced in, each thread's contiguous
+// chunk scanned from LDS, Z written back over them), so every HBM access is a
+// coalesced row sweep: n reads of the full products, (npp) reads of the
+// partial products, (1 + npp) n writes per challenge.
 __global__ void __launch_bounds__(1024) k_z_scan(const uint64_t *__restrict__ prods, uint64_t *__restrict__ zs,
                                                  uint32_t log_n, uint32_t nc, uint32_t nchunks, uint64_t p_bstride,
                                                  uint64_t z_bstride) {
-  __shared__ uint64_t sh[1024];
+  extern __shared__ __attribute__((aligned(16))) uint64_t zbuf[];  // [lp(n)] rows, then [T] partials
   const uint32_t n = 1u << log_n;
   const uint32_t c = blockIdx.x, b = blockIdx.y;
   prods += b * p_bstride + (uint64_t)c * nchunks * n;
   zs += b * z_bstride;
   const uint64_t *full = prods + (uint64_t)(nchunks - 1) * n;
-  const uint32_t T = blockDim.x, per = (n + T - 1) / T;
-  const uint32_t lo = threadIdx.x * per, hi = min(lo + per, n);
+  const uint32_t T = blockDim.x, t = threadIdx.x, per = (n + T - 1) / T;
+  uint64_t *part = zbuf + nt::lp(n);
+  for (uint32_t i = t; i < n; i += T) zbuf[nt::lp(i)] = full[i];
+  __syncthreads();
+  const uint32_t lo = min(t * per, n), hi = min(lo + per, n);
   uint64_t local = 1;
-  for (uint32_t i = lo; i < hi; i++) local = gl::mul(local, full[i]);
-  sh[threadIdx.x] = local;
+  for (uint32_t i = lo; i < hi; i++) local = gl::mul(local, zbuf[nt::lp(i)]);
+  part[t] = local;
   __syncthreads();
   // inclusive Hillis-Steele scan over T partial products
   for (uint32_t off = 1; off < T; off <<= 1) {
-    uint64_t v = threadIdx.x >= off ? sh[threadIdx.x - off] : 1;
+    uint64_t v = t >= off ? part[t - off] : 1;
     __syncthreads();
-    sh[threadIdx.x] = gl::mul(sh[threadIdx.x], v);
+    part[t] = gl::mul(part[t], v);
     __syncthreads();
   }
-  uint64_t z = threadIdx.x ? sh[threadIdx.x - 1] : 1;
-  const uint32_t npp = nchunks - 1;
+  uint64_t z = t ? part[t - 1] : 1;
   for (uint32_t i = lo; i < hi; i++) {
-    zs[(uint64_t)c * n + i] = z;
-    for (uint32_t j = 0; j < npp; j++)
-      zs[((uint64_t)nc + c * npp + j) * n + i] = gl::mul(z, prods[(uint64_t)j * n + i]);
-    z = gl::mul(z, full[i]);
+    const uint64_t f = zbuf[nt::lp(i)];
+    zbuf[nt::lp(i)] = z;
+    z = gl::mul(z, f);
+  }
+  __syncthreads();
+  const uint32_t npp = nchunks - 1;
+  for (uint32_t i = t; i < n; i += T) {
+    const uint64_t zi = zbuf[nt::lp(i)];
+    zs[(uint64_t)c * n + i] = zi;
+    for (uint32_t j = 0; j < npp; j++) zs[((uint64_t)nc + c * npp + j) * n + i] = gl::mul(zi, prods[(uint64_t)j * n + i]);
   }
 }
 
@@ -711,15 +723,24 @@ __global__ void __launch_bounds__(256) k_fri_leaf(const uint64_t *__restrict__ v
   o[0] = psd::canon(s[0]); o[1] = psd::canon(s[1]); o[2] = psd::canon(s[2]); o[3] = psd::canon(s[3]);
 }
 
-// fold: out[k] = sum_{i<2^ab} beta^i c[2^ab k + i]  (coefficients, ext as 2 columns)
+// fold: out[k] = sum_{i<2^ab} beta^i c[2^ab k + i]  (coefficients, ext as 2 columns).
+// Only the first 2^log_nz input coefficients can be nonzero (the layer-0
+// polynomial has degree < n in a length-N buffer): outputs past them are
+// written as zeros without reading the zero tail.
 __global__ void __launch_bounds__(256) k_fold(const uint64_t *__restrict__ cin, uint64_t *__restrict__ cout,
                                               uint32_t log_len, uint32_t ab, uint32_t layer,
                                               const uint64_t *__restrict__ chal, uint64_t i_bstride,
-                                              uint64_t o_bstride) {
+                                              uint64_t o_bstride, uint32_t log_nz) {
   const uint32_t nout = 1u << (log_len - ab);
   const uint32_t k = blockIdx.x * blockDim.x + threadIdx.x;
   if (k >= nout) return;
   const uint32_t b = blockIdx.y;
+  uint64_t *o = cout + b * o_bstride;
+  if (((uint64_t)k << ab) >= (1ull << log_nz)) {
+    o[k] = 0;
+    o[nout + k] = 0;
+    return;
+  }
   const uint64_t *ch = chal + b * CHAL_STRIDE;
   const ext beta{ch[CH_FRI_BETA + 2 * layer], ch[CH_FRI_BETA + 2 * layer + 1]};
   const uint64_t L = 1ull << log_len;
@@ -729,7 +750,6 @@ __global__ void __launch_bounds__(256) k_fold(const uint64_t *__restrict__ cin, 
     const uint64_t idx = ((uint64_t)k << ab) + i;
     acc = gl::ext_add(gl::ext_mul(acc, beta), ext{c0[idx], c1[idx]});
   }
-  uint64_t *o = cout + b * o_bstride;
   o[k] = acc.c0;
   o[nout + k] = acc.c1;
 }

@@ -299,7 +299,7 @@ int qp_fri_fold(qp_ctx *ctx, const uint64_t *coeffs, uint32_t log_coeffs, uint32
   QP_HIP_TRY(ctx, hipMemcpyAsync(d_in.p, coeffs, 2 * L * 8, hipMemcpyHostToDevice, s));
   QP_HIP_TRY(ctx, hipMemcpyAsync(d_chal.p, chal.data(), chal.size() * 8, hipMemcpyHostToDevice, s));
   qpk::k_fold<<<dim3(cdiv(Lo, 256), 1), 256, 0, s>>>(d_in.p, d_out.p, log_coeffs, arity_bits, 0, d_chal.p, 2 * L,
-                                                     2 * Lo);
+                                                     2 * Lo, log_coeffs);
   QP_HIP_TRY(ctx, hipGetLastError());
   QP_HIP_TRY(ctx, hipMemcpyAsync(coeffs_out, d_out.p, 2 * Lo * 8, hipMemcpyDeviceToHost, s));
   QP_HIP_TRY(ctx, hipStreamSynchronize(s));

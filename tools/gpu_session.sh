@@ -31,6 +31,7 @@ for s in "$@"; do
     prof) step rocprof 600 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/prof -o run -- python3 tools/kbench.py 8 3 ;;
     bench) step bench 900 python bench.py ;;
     benchprof) step rocprof_bench 900 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/prof_bench -o run -- python3 bench.py --steps 2 --warmup 1 --cpu-sample 0 ;;
+    benchprof1) step rocprof_bench1 600 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/prof_bench1 -o run -- python3 bench.py --steps 2 --warmup 1 --cpu-sample 0 --provers 1 ;;
     pmc_fetch) pmc fetch FETCH_SIZE ;;
     pmc_write) pmc write WRITE_SIZE ;;
     pmc_valu) pmc valu SQ_WAVES SQ_INSTS_VALU SQ_WAVE_CYCLES SQ_BUSY_CYCLES ;;
