@@ -24,6 +24,7 @@
 #include <stdint.h>
 #include <hip/hip_runtime.h>
 #include "poseidon.h"
+#include "poseidon_mds_asm.h"
 
 namespace pf {
 
@@ -275,6 +276,38 @@ __device__ __forceinline__ void mds_rows_block(uint64_t s[12], const uint32_t lo
   }
 }
 
+// modes 6-9: blocks of NR = 2, 3, 4, 6 rows, their 2*NR accumulate chains
+// interleaved in one asm block (poseidon_mds_asm.h) so a wave keeps 2*NR
+// independent v_mad_u64_u32 chains in flight instead of 2
+template <int M>
+constexpr int mds_block_rows() { return M == 6 ? 2 : M == 7 ? 3 : M == 8 ? 4 : 6; }
+
+template <int NR, int R>
+__device__ __forceinline__ void mds_asm_rows(uint64_t acc[2 * NR], const uint32_t lo[12], const uint32_t hi[12],
+                                             const uint64_t k[2 * NR]) {
+  if constexpr (NR == 2) mds_asm_rows2<R>(acc, lo, hi, k);
+  else if constexpr (NR == 3) mds_asm_rows3<R>(acc, lo, hi, k);
+  else if constexpr (NR == 4) mds_asm_rows4<R>(acc, lo, hi, k);
+  else mds_asm_rows6<R>(acc, lo, hi, k);
+}
+
+template <int NR, int R, int RC>
+__device__ __forceinline__ void mds_rows_multi(uint64_t s[12], const uint32_t lo[12], const uint32_t hi[12]) {
+  if constexpr (R < 12) {
+    uint64_t k[2 * NR], acc[2 * NR];
+#pragma unroll
+    for (int r = 0; r < NR; r++) {
+      const uint64_t kk = RC >= 0 ? ps::rc_cx(RC * 12 + R + r) : 0;
+      k[2 * r] = kk & EPS;
+      k[2 * r + 1] = kk >> 32;
+    }
+    mds_asm_rows<NR, R>(acc, lo, hi, k);
+#pragma unroll
+    for (int r = 0; r < NR; r++) s[R + r] = reduce_row(acc[2 * r], acc[2 * r + 1]);
+    mds_rows_multi<NR, R + NR, RC>(s, lo, hi);
+  }
+}
+
 // s <- MDS(s) + RC[next] (next < 0: no constant)
 template <int M, int NEXT>
 __device__ __forceinline__ void mds(uint64_t s[12]) {
@@ -284,7 +317,8 @@ __device__ __forceinline__ void mds(uint64_t s[12]) {
     lo[i] = lo32(s[i]);
     hi[i] = hi32(s[i]);
   }
-  if constexpr (M >= 3) mds_rows_block<0, NEXT>(s, lo, hi);
+  if constexpr (M >= 6) mds_rows_multi<mds_block_rows<M>(), 0, NEXT>(s, lo, hi);
+  else if constexpr (M >= 3) mds_rows_block<0, NEXT>(s, lo, hi);
   else mds_rows<M, 0, NEXT>(s, lo, hi);
 }
 
@@ -358,7 +392,8 @@ __device__ __forceinline__ void rounds(uint64_t s[12]) {
 // permutation; inputs in [0, 2^64), outputs in [0, 2^64) (canon() lanes read out)
 // M: 0 = asm mads, 1 = compiler mads on opaque constants, 2 = 1 + C reductions,
 //    3 = 0 with each MDS row's 24 mads in one asm block, 4 = 3 with the
-//    partial rounds rolled into a loop, 5 = every round rolled
+//    partial rounds rolled into a loop, 5 = every round rolled,
+//    6..9 = MDS in blocks of 2 / 3 / 4 / 6 rows with interleaved chains
 template <int M = 1>
 __device__ __forceinline__ void permute_nc(uint64_t s[12]) {
 #pragma unroll

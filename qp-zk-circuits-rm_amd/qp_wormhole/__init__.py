@@ -10,8 +10,9 @@ from ._native import (Context, FriLayer, GateDesc, PolynomialBatch, QpError, fri
 
 from .circuits import (Circuit, CircuitInputs, PrivateCircuitInputs, ProcessedStorageProof,  # noqa: F401,E402
                        PublicCircuitInputs, VoteCircuitData, VotePrivateInputs, VotePublicInputs, Witness)
-from .prover import Prover, ProofWithPublicInputs, WormholeProver  # noqa: F401,E402
+from .prover import (Prover, ProofWithPublicInputs, WormholeProver, generate_circuit_binaries,  # noqa: F401,E402
+                     prover_only_bytes)
 
 __all__ = ["Circuit", "CircuitInputs", "PrivateCircuitInputs", "ProcessedStorageProof", "PublicCircuitInputs",
            "Witness", "VoteCircuitData", "VotePrivateInputs", "VotePublicInputs", "Prover", "ProofWithPublicInputs", "WormholeProver", "Context", "PolynomialBatch", "QpError", "ifft", "lde", "poseidon_permute", "lib", "header_symbols",
-           "GateDesc", "gate_desc", "quotient", "FriLayer", "fri_fold", "pow_grind"]
+           "generate_circuit_binaries", "prover_only_bytes", "GateDesc", "gate_desc", "quotient", "FriLayer", "fri_fold", "pow_grind"]

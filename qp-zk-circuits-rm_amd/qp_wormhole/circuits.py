@@ -174,6 +174,7 @@ class Circuit:
 
     def __init__(self, handle, kind):
         self.h, self.kind = handle, kind
+        self.zk = False
         info = (ctypes.c_uint32 * 8)()
         lib().qp_circuit_info(self.h, info)
         (self.degree_bits, self.num_wires, self.num_routed_wires, self.num_constants, self.num_public_inputs,
@@ -186,7 +187,9 @@ class Circuit:
         rc = lib().qp_wormhole_circuit_new(int(zero_knowledge), ctypes.byref(h))
         if rc:
             raise QpError(rc, "qp_wormhole_circuit_new")
-        return cls(h, "wormhole")
+        c = cls(h, "wormhole")
+        c.zk = bool(zero_knowledge)
+        return c
 
     @classmethod
     def voting(cls, zero_knowledge=False):
@@ -195,7 +198,9 @@ class Circuit:
         rc = lib().qp_voting_circuit_new(int(zero_knowledge), ctypes.byref(h))
         if rc:
             raise QpError(rc, "qp_voting_circuit_new")
-        return cls(h, "voting")
+        c = cls(h, "voting")
+        c.zk = bool(zero_knowledge)
+        return c
 
     def common_data(self):
         ln = ctypes.c_size_t()

@@ -3,9 +3,14 @@
 `Prover` wraps qp_prover (include/qpgpu.h): B proofs of one circuit per call on
 one MI355X.  `WormholeProver` mirrors qp-wormhole-prover's API
 (wormhole/prover/src/lib.rs:74-237): new(config) -> commit(inputs) -> prove(),
-single use, commit twice is an error, prove before commit is an error.
+single use, commit twice is an error, prove before commit is an error;
+new_from_bytes / new_from_files / default() load the circuit binaries that
+`generate_circuit_binaries` writes (wormhole/circuit-builder/src/lib.rs:11-66).
 """
 import ctypes
+import hashlib
+import os
+import struct
 import threading
 
 import numpy as np
@@ -147,13 +152,138 @@ def _shared(config, device):
         return _cache[key]
 
 
+CONFIGS = ("standard_recursion_config", "standard_recursion_zk_config")
+
+# prover.bin of this backend.  plonky2's ProverOnlyCircuitData::to_bytes
+# (generators through DefaultGeneratorSerializer, the constants||sigmas
+# PolynomialBatch, fft root table, ...) has no fixture in the reference
+# (generated-bins/ is empty) and would be rebuilt by the device preprocessing
+# anyway, so the file records the circuit identity and its preprocessed
+# commitment: magic, version, circuit kind, zk flag, degree bits, SHA-256 of
+# common.bin, then the VerifierOnlyCircuitData bytes (constants||sigmas cap +
+# circuit digest).  Loading rebuilds the native circuit for that identity and
+# refuses data whose commitment differs.
+PROVER_MAGIC = b"QPGPU-PROVER-ONLY\0"
+PROVER_VERSION = 1
+_KINDS = {"wormhole": 0, "voting": 1}
+
+
+def _config_of_common(common_bytes):
+    """The Wormhole circuit config whose CommonCircuitData::to_bytes equals common_bytes."""
+    for cfg in CONFIGS:
+        if Circuit.wormhole(zero_knowledge=(cfg == CONFIGS[1])).common_data() == bytes(common_bytes):
+            return cfg
+    return None
+
+
+def _verifier_only(circuit, prover):
+    """VerifierOnlyCircuitData::to_bytes (constants||sigmas cap + circuit digest):
+    qp_prover_verifier_data returns it followed by the common data."""
+    full = prover.verifier_data()
+    common = circuit.common_data()
+    assert full.endswith(common)
+    return full[:len(full) - len(common)]
+
+
+def prover_only_bytes(circuit, prover):
+    """This backend's prover.bin for a built circuit and its device prover."""
+    common = circuit.common_data()
+    head = PROVER_MAGIC + struct.pack("<IBBI", PROVER_VERSION, _KINDS[circuit.kind], int(circuit.zk),
+                                      circuit.degree_bits)
+    return head + hashlib.sha256(common).digest() + _verifier_only(circuit, prover)
+
+
+def _parse_prover_only(data, common_bytes):
+    data = bytes(data)
+    n = len(PROVER_MAGIC)
+    if len(data) < n + 10 + 32 or data[:n] != PROVER_MAGIC:
+        raise ValueError("bad magic")
+    version, kind, zk, degree_bits = struct.unpack_from("<IBBI", data, n)
+    if version != PROVER_VERSION:
+        raise ValueError(f"unsupported version {version}")
+    if kind != _KINDS["wormhole"]:
+        raise ValueError("not a Wormhole circuit")
+    off = n + 10
+    if data[off:off + 32] != hashlib.sha256(bytes(common_bytes)).digest():
+        raise ValueError("prover data was written for different common data")
+    return bool(zk), degree_bits, data[off + 32:]
+
+
+def generate_circuit_binaries(output_dir, include_prover=True, config="standard_recursion_config", device=0):
+    """wormhole/circuit-builder/src/lib.rs:11-66: build the circuit and write
+    common.bin (CommonCircuitData::to_bytes), verifier.bin
+    (VerifierOnlyCircuitData::to_bytes) and, if asked, prover.bin (this
+    backend's format, see PROVER_MAGIC)."""
+    ctx, circ, prover, lock = _shared(config, device)
+    os.makedirs(output_dir, exist_ok=True)
+    with open(os.path.join(output_dir, "common.bin"), "wb") as f:
+        f.write(circ.common_data())
+    with lock:
+        vd = _verifier_only(circ, prover)
+        pb = prover_only_bytes(circ, prover) if include_prover else None
+    with open(os.path.join(output_dir, "verifier.bin"), "wb") as f:
+        f.write(vd)
+    if include_prover:
+        with open(os.path.join(output_dir, "prover.bin"), "wb") as f:
+            f.write(pb)
+
+
 class WormholeProver:
     def __init__(self, config="standard_recursion_config", device=0):
-        if config not in ("standard_recursion_config", "standard_recursion_zk_config"):
+        if config not in CONFIGS:
             raise ValueError(f"unknown circuit config {config!r}")
+        self.config = config
         self.ctx, self.circuit, self.prover, self._prove_lock = _shared(config, device)
         self._witness = None
         self._committed = False
+
+    @classmethod
+    def new_from_bytes(cls, prover_only_bytes, common_bytes, device=0):
+        """WormholeProver::new_from_bytes (lib.rs:105-138): the config comes from
+        the common data; errors carry the reference's messages."""
+        cfg = _config_of_common(common_bytes)
+        if cfg is None:
+            raise ValueError("Failed to deserialize common circuit data")
+        try:
+            _, _, vd = _parse_prover_only(prover_only_bytes, common_bytes)
+        except ValueError as e:
+            raise ValueError(f"Failed to deserialize prover only data: {e}") from None
+        self = cls(cfg, device)
+        with self._prove_lock:
+            mine = _verifier_only(self.circuit, self.prover)
+        if mine != vd:
+            raise ValueError("Failed to deserialize prover only data: preprocessed commitment differs")
+        return self
+
+    @classmethod
+    def new_from_files(cls, prover_data_path, common_data_path, device=0):
+        """WormholeProver::new_from_files (lib.rs:141-187)."""
+        with open(common_data_path, "rb") as f:
+            common = f.read()
+        cfg = _config_of_common(common)
+        if cfg is None:
+            raise ValueError(f"Failed to deserialize common circuit data from {str(common_data_path)!r}")
+        with open(prover_data_path, "rb") as f:
+            pb = f.read()
+        try:
+            _, _, vd = _parse_prover_only(pb, common)
+        except ValueError as e:
+            raise ValueError(f"Failed to deserialize prover only data from {str(prover_data_path)!r}: {e}") from None
+        self = cls(cfg, device)
+        with self._prove_lock:
+            if _verifier_only(self.circuit, self.prover) != vd:
+                raise ValueError(f"Failed to deserialize prover only data from {str(prover_data_path)!r}: "
+                                 "preprocessed commitment differs")
+        return self
+
+    @classmethod
+    def default(cls, device=0):
+        """WormholeProver::default (lib.rs:81-101): generated-bins/ if loadable, else build."""
+        try:
+            return cls.new_from_files(os.path.join("generated-bins", "prover.bin"),
+                                      os.path.join("generated-bins", "common.bin"), device)
+        except (OSError, ValueError):
+            return cls("standard_recursion_config", device)
 
     def commit(self, inputs: CircuitInputs):
         if self._committed:

@@ -39,6 +39,7 @@ for s in "$@"; do
     test_voting) step pytest_voting 300 python -u -m pytest tests/test_gpu_voting.py -x -v --timeout 120 --timeout-method thread ;;
     bench_voting) step bench_voting 600 python bench.py --circuit voting ;;
     benchprof_voting) step rocprof_bench_voting 600 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/prof_bench_voting -o run -- python3 bench.py --circuit voting --steps 3 --warmup 1 --cpu-sample 0 ;;
+    test_bins) step pytest_bins 600 python -u -m pytest tests/test_gpu_circuit_bins.py -x -v --timeout 300 --timeout-method thread ;;
     test_seams) step pytest_seams 600 python -u -m pytest tests/test_gpu_seams.py -x -v --timeout 300 --timeout-method thread ;;
     test_commit) step pytest_commit 600 python -u -m pytest tests/test_gpu_commit.py -x -v --timeout 300 --timeout-method thread ;;
     lde_ab) step prof_lde_new 300 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/prof_lde_new -o run -- python3 tools/kbench.py 16 3 &&

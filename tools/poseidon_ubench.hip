@@ -13,6 +13,7 @@
 //   V10: pf mode 3: mode 0 with each MDS row's 24 mads in one asm block
 //   V11: pf mode 4: mode 3 with the partial rounds rolled into a loop
 //   V12: pf mode 5: every round rolled
+//   V13-V16: pf modes 6-9: MDS rows in interleaved asm blocks of 2 / 3 / 4 / 6 rows
 // Build: hipcc --offload-arch=gfx950 -O3 -std=c++17 -I qp-zk-circuits-rm_amd/csrc tools/poseidon_ubench.hip
 #include <hip/hip_runtime.h>
 #include <stdint.h>
@@ -174,6 +175,10 @@ __global__ void __launch_bounds__(256) kperm(uint64_t *st, uint64_t n) {
     if (V == 10) pf::permute_nc<3>(s);
     if (V == 11) pf::permute_nc<4>(s);
     if (V == 12) pf::permute_nc<5>(s);
+    if (V == 13) pf::permute_nc<6>(s);
+    if (V == 14) pf::permute_nc<7>(s);
+    if (V == 15) pf::permute_nc<8>(s);
+    if (V == 16) pf::permute_nc<9>(s);
   }
   for (int k = 0; k < 12; k++) st[k * n + i] = V == 0 ? s[k] : psd::canon(s[k]);
 }
@@ -203,8 +208,9 @@ int main() {
   uint64_t *d;
   (void)hipMalloc(&d, n * 96);
   (void)hipMemset(d, 7, n * 96);
-  constexpr int NV = 13;
-  float t[NV] = {run<0>(d, n), run<1>(d, n), run<2>(d, n), run<3>(d, n), run<4>(d, n), run<5>(d, n), run<6>(d, n), run<7>(d, n), run<8>(d, n), run<9>(d, n), run<10>(d, n), run<11>(d, n), run<12>(d, n)};
+  constexpr int NV = 17;
+  float t[NV] = {run<0>(d, n), run<1>(d, n), run<2>(d, n), run<3>(d, n), run<4>(d, n), run<5>(d, n), run<6>(d, n), run<7>(d, n), run<8>(d, n), run<9>(d, n), run<10>(d, n), run<11>(d, n), run<12>(d, n),
+                 run<13>(d, n), run<14>(d, n), run<15>(d, n), run<16>(d, n)};
   // check all variants agree
   uint64_t *h = new uint64_t[12 * NV];
   for (int v = 0; v < NV; v++) {
@@ -222,6 +228,10 @@ int main() {
     if (v == 10) kperm<10, 1><<<(unsigned)(n / 256), 256>>>(d, n);
     if (v == 11) kperm<11, 1><<<(unsigned)(n / 256), 256>>>(d, n);
     if (v == 12) kperm<12, 1><<<(unsigned)(n / 256), 256>>>(d, n);
+    if (v == 13) kperm<13, 1><<<(unsigned)(n / 256), 256>>>(d, n);
+    if (v == 14) kperm<14, 1><<<(unsigned)(n / 256), 256>>>(d, n);
+    if (v == 15) kperm<15, 1><<<(unsigned)(n / 256), 256>>>(d, n);
+    if (v == 16) kperm<16, 1><<<(unsigned)(n / 256), 256>>>(d, n);
     (void)hipDeviceSynchronize();
     for (int k = 0; k < 12; k++) (void)hipMemcpy(h + v * 12 + k, d + k * n, 8, hipMemcpyDeviceToHost);
   }
