@@ -223,19 +223,32 @@ int qp_prover_stage_times(qp_prover *p, double *ms, uint32_t n, int reset);
  * circuit path does not cover.  The Fiat-Shamir transcript stays with the
  * caller (INTEGRATION.md shows the call sequence).                            */
 
-/* gate kinds of CommonCircuitData.gates (DefaultGateSerializer ids 9, 3, 12, 2, 0, 11) */
-enum { QP_GATE_NOOP = 0, QP_GATE_CONSTANT = 1, QP_GATE_PUBLIC_INPUT = 2, QP_GATE_BASE_SUM = 3,
-       QP_GATE_ARITHMETIC = 4, QP_GATE_POSEIDON = 5 };
+/* gate kinds of CommonCircuitData.gates (DefaultGateSerializer ids in brackets).
+ * 0-5: the leaf circuits' gates (fast single-read quotient kernel); 6-13: the
+ * recursive-verifier gates of the aggregator circuits (tree.rs:106-143; generic
+ * quotient kernel; parity unpinned: no reference fixture holds such a circuit). */
+enum { QP_GATE_NOOP = 0 /* 9 */, QP_GATE_CONSTANT = 1 /* 3 */, QP_GATE_PUBLIC_INPUT = 2 /* 12 */,
+       QP_GATE_BASE_SUM = 3 /* 2, BaseSumGate<2> */, QP_GATE_ARITHMETIC = 4 /* 0 */, QP_GATE_POSEIDON = 5 /* 11 */,
+       QP_GATE_ARITHMETIC_EXTENSION = 6 /* 1 */, QP_GATE_MUL_EXTENSION = 7 /* 8 */,
+       QP_GATE_RANDOM_ACCESS = 8 /* 13 */, QP_GATE_EXPONENTIATION = 9 /* 5 */, QP_GATE_REDUCING = 10 /* 15 */,
+       QP_GATE_REDUCING_EXTENSION = 11 /* 14 */, QP_GATE_POSEIDON_MDS = 12 /* 10 */,
+       QP_GATE_COSET_INTERPOLATION = 13 /* 4 */ };
+#define QP_MAX_GATES 16
 
 /* the parts of CommonCircuitData the vanishing polynomial reads */
 typedef struct {
-    uint32_t num_gates;            /* <= 8, in CommonCircuitData.gates order */
-    uint32_t kind[8];              /* QP_GATE_* */
-    uint32_t param[8];             /* ConstantGate num_consts / BaseSumGate num_limbs / ArithmeticGate num_ops */
-    uint32_t selector_index[8];    /* selectors_info.selector_indices */
-    uint32_t num_selectors;        /* selectors_info.groups.len() */
-    uint32_t group_lo[8], group_hi[8];
-    uint32_t num_constants;        /* selectors + gate constants */
+    uint32_t num_gates;                    /* <= QP_MAX_GATES, in CommonCircuitData.gates order */
+    uint32_t kind[QP_MAX_GATES];           /* QP_GATE_* */
+    uint32_t param[QP_MAX_GATES];          /* Constant num_consts, BaseSum num_limbs, Arithmetic(Extension) /
+                                              MulExtension num_ops, RandomAccess bits, Exponentiation
+                                              num_power_bits, Reducing(Extension) num_coeffs,
+                                              CosetInterpolation subgroup_bits */
+    uint32_t param2[QP_MAX_GATES];         /* RandomAccess num_copies, CosetInterpolation degree */
+    uint32_t param3[QP_MAX_GATES];         /* RandomAccess num_extra_constants */
+    uint32_t selector_index[QP_MAX_GATES]; /* selectors_info.selector_indices */
+    uint32_t num_selectors;                /* selectors_info.groups.len() */
+    uint32_t group_lo[QP_MAX_GATES], group_hi[QP_MAX_GATES];
+    uint32_t num_constants;                /* selectors + gate constants */
     uint32_t num_routed_wires, num_wires, quotient_degree_factor, num_challenges, num_gate_constraints;
 } qp_gate_desc;
 

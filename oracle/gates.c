@@ -10,6 +10,13 @@ unsigned or_gate_num_constraints(const or_gate_t *g) {
     case G_BASE_SUM: return (unsigned)g->p0 + 1;
     case G_ARITHMETIC: return (unsigned)g->p0;
     case G_POSEIDON: return 123;
+    case G_ARITH_EXT: return 2 * (unsigned)g->p0;
+    case G_MUL_EXT: return 2 * (unsigned)g->p0;
+    case G_REDUCING: case G_REDUCING_EXT: return 2 * (unsigned)g->p0;
+    case G_EXPONENTIATION: return (unsigned)g->p0 + 1;
+    case G_POSEIDON_MDS: return 24;
+    case G_RANDOM_ACCESS: return (unsigned)((g->p0 + 2) * g->p1 + g->p2);
+    case G_COSET_INTERP: return 4 + 4 * (unsigned)(((1u << g->p0) - 2) / (g->p1 - 1));
     default: return 0;
     }
 }
@@ -47,4 +54,9 @@ void or_eval_gate_constraints_ext(const or_common_t *c, const glx_t *lc, const g
 }
 void or_eval_gate_constraints_base(const or_common_t *c, const gl_t *lc, const gl_t *lw, const gl_t pi[4], gl_t *out) {
     base_or_eval_gate_constraints(c, lc, lw, pi, out);
+}
+
+/* one gate's unfiltered constraints in the base field (tests of the gate formulas) */
+unsigned or_gate_eval_base(const or_gate_t *g, const gl_t *c, const gl_t *w, const gl_t pi[4], gl_t *out) {
+    return base_gate_unfiltered(g, c, w, pi, out);
 }

@@ -106,6 +106,7 @@ void or_eval_gate_constraints_ext(const or_common_t *c, const glx_t *local_const
 void or_eval_gate_constraints_base(const or_common_t *c, const gl_t *local_constants,
                                    const gl_t *local_wires, const gl_t pi_hash[4], gl_t *out);
 unsigned or_gate_num_constraints(const or_gate_t *g);
+unsigned or_gate_eval_base(const or_gate_t *g, const gl_t *c, const gl_t *w, const gl_t pi[4], gl_t *out);
 
 /* verifier: 0 = ok, else a failing-check code (see or_verify_error) */
 int or_verify(const or_common_t *c, const or_verifier_only_t *v, const or_proof_t *p);

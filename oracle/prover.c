@@ -471,3 +471,69 @@ gl_t ora_pow_grind(const gl_t *state, unsigned pos, unsigned bits) {
         if ((s[7] >> (64 - bits)) == 0) return cand;
     }
 }
+
+/* qp_quotient checker for an arbitrary gate description (the layout of
+ * include/qpgpu.h qp_gate_desc, mirrored here so the oracle includes nothing
+ * of the product): builds the CommonCircuitData fields the vanishing
+ * polynomial reads (k_is = g^j, plonky2's get_unique_coset_shifts) and runs
+ * quotient_coeffs.  Values: consts_sigmas [num_constants + R][n], wires
+ * [num_wires][n], zs_pp [2 * nchunks][n]. */
+typedef struct {
+    uint32_t num_gates, kind[16], param[16], param2[16], param3[16], selector_index[16];
+    uint32_t num_selectors, group_lo[16], group_hi[16];
+    uint32_t num_constants, num_routed_wires, num_wires, quotient_degree_factor, num_challenges,
+        num_gate_constraints;
+} ora_gate_desc_t;
+
+static const uint32_t ORA_ID_OF_KIND[14] = {G_NOOP, G_CONSTANT, G_PUBLIC_INPUT, G_BASE_SUM, G_ARITHMETIC, G_POSEIDON,
+                                            G_ARITH_EXT, G_MUL_EXT, G_RANDOM_ACCESS, G_EXPONENTIATION, G_REDUCING,
+                                            G_REDUCING_EXT, G_POSEIDON_MDS, G_COSET_INTERP};
+
+/* unfiltered constraints of gate gi of a description at one row: returns the
+ * count (constants = the gate constants after the selector columns) */
+long ora_gate_eval(const ora_gate_desc_t *g, unsigned gi, const gl_t *constants, const gl_t *wires,
+                   const gl_t *pih, gl_t *out) {
+    if (gi >= g->num_gates || g->kind[gi] >= 14) return -1;
+    or_gate_t gt = {ORA_ID_OF_KIND[g->kind[gi]], g->param[gi], g->param2[gi], g->param3[gi]};
+    return (long)or_gate_eval_base(&gt, constants, wires, pih, out);
+}
+
+int ora_quotient_desc(const ora_gate_desc_t *g, unsigned log_n, unsigned rate_bits, const gl_t *consts_sigmas,
+                      const gl_t *wires, const gl_t *zs_vals, const gl_t *betas, const gl_t *gammas,
+                      const gl_t *alphas, const gl_t *pih, gl_t *qcoeffs_out) {
+    if (g->num_gates == 0 || g->num_gates > 16 || g->num_challenges != 2 || g->num_routed_wires > 256) return -1;
+    or_common_t *c = calloc(1, sizeof(or_common_t));
+    c->fri_params_config.rate_bits = rate_bits;
+    c->degree_bits = log_n;
+    c->num_challenges = 2;
+    c->num_wires = g->num_wires;
+    c->num_routed_wires = g->num_routed_wires;
+    c->num_constants = g->num_constants;
+    c->quotient_degree_factor = g->quotient_degree_factor;
+    const unsigned nchunks = (g->num_routed_wires + g->quotient_degree_factor - 1) / g->quotient_degree_factor;
+    c->num_partial_products = nchunks - 1;
+    c->num_gate_constraints = g->num_gate_constraints;
+    c->num_k_is = g->num_routed_wires;
+    for (unsigned j = 0; j < g->num_routed_wires; j++) c->k_is[j] = gl_pow(GL_GEN, j);
+    c->num_gates = g->num_gates;
+    c->num_selector_indices = g->num_gates;
+    for (unsigned i = 0; i < g->num_gates; i++) {
+        if (g->kind[i] >= 14) { free(c); return -1; }
+        c->gates[i].id = ORA_ID_OF_KIND[g->kind[i]];
+        c->gates[i].p0 = g->param[i];
+        c->gates[i].p1 = g->param2[i];
+        c->gates[i].p2 = g->param3[i];
+        c->selector_indices[i] = g->selector_index[i];
+    }
+    c->num_groups = g->num_selectors;
+    for (unsigned i = 0; i < g->num_selectors; i++) { c->groups[i][0] = g->group_lo[i]; c->groups[i][1] = g->group_hi[i]; }
+    const unsigned ncs = g->num_constants + g->num_routed_wires, nzs = 2 * nchunks;
+    batch_t bcs, bw, bz;
+    batch_from_values(&bcs, consts_sigmas, ncs, log_n, rate_bits, 0);
+    batch_from_values(&bw, wires, g->num_wires, log_n, rate_bits, 0);
+    batch_from_values(&bz, zs_vals, nzs, log_n, rate_bits, 0);
+    quotient_coeffs(c, log_n, bcs.leaves, bw.leaves, bz.leaves, betas, gammas, alphas, pih, qcoeffs_out);
+    batch_free(&bcs); batch_free(&bw); batch_free(&bz);
+    free(c);
+    return 0;
+}

@@ -21,11 +21,19 @@ enum : uint32_t {
 constexpr uint32_t OPEN_STRIDE = 520;  // 257 ext openings per proof (+pad)
 constexpr uint32_t APOW_STRIDE = 256;  // alpha_c^i, i < #vanishing terms (per challenge)
 
-enum GateKindDev : uint32_t { GK_NOOP = 0, GK_CONSTANT, GK_PUBLIC_INPUT, GK_BASE_SUM, GK_ARITHMETIC, GK_POSEIDON };
+// = QP_GATE_* (include/qpgpu.h)
+enum GateKindDev : uint32_t {
+  GK_NOOP = 0, GK_CONSTANT, GK_PUBLIC_INPUT, GK_BASE_SUM, GK_ARITHMETIC, GK_POSEIDON,
+  GK_ARITH_EXT, GK_MUL_EXT, GK_RANDOM_ACCESS, GK_EXPONENTIATION, GK_REDUCING, GK_REDUCING_EXT, GK_POSEIDON_MDS,
+  GK_COSET_INTERP, GK_COUNT
+};
+constexpr uint32_t MAX_GATES_DEV = 16;
 
 struct GateDesc {
   uint32_t ngates = 0, nsel = 0;
-  uint32_t kind[8] = {0}, param[8] = {0}, sel_index[8] = {0}, grp_lo[8] = {0}, grp_hi[8] = {0};
+  uint32_t kind[MAX_GATES_DEV] = {0}, param[MAX_GATES_DEV] = {0}, param2[MAX_GATES_DEV] = {0},
+           param3[MAX_GATES_DEV] = {0}, sel_index[MAX_GATES_DEV] = {0}, grp_lo[MAX_GATES_DEV] = {0},
+           grp_hi[MAX_GATES_DEV] = {0};
 };
 
 struct QuotientArgs {

@@ -211,6 +211,159 @@ __device__ __forceinline__ void poseidon_gate(const uint64_t *__restrict__ wl, u
   for (int i = 0; i < 12; i++) A.emit(gfn::sub(s[i], WV(12 + i)));
 }
 
+// Recursive-verifier gates (the aggregator circuits, tree.rs:106-143), evaluated
+// in the order of upstream plonky2's eval_unfiltered (oracle/gates_impl.h
+// gate_recursion restates the same; parity unpinned).  Extension-algebra
+// values are wire pairs (c0, c1) over F[Y]/(Y^2 - 7).  Generic and read-as-
+// you-go: these circuits are off the Wormhole hot path.
+__device__ __forceinline__ void alg_mul(uint64_t a0, uint64_t a1, uint64_t b0, uint64_t b1, uint64_t &r0,
+                                        uint64_t &r1) {
+  r0 = gfn::add(gfn::mul(a0, b0), gfn::mul(7, gfn::mul(a1, b1)));
+  r1 = gfn::add(gfn::mul(a0, b1), gfn::mul(a1, b0));
+}
+
+__device__ __noinline__ void recursion_gate(uint32_t kind, uint32_t q0, uint32_t q1, uint32_t q2,
+                                            const uint64_t *__restrict__ wl, const uint64_t *__restrict__ gc,
+                                            uint64_t N, TermAcc &A) {
+  switch (kind) {
+    case GK_ARITH_EXT:  // per op: multiplicand_0, multiplicand_1, addend, output
+      for (uint32_t i = 0; i < q0; i++) {
+        const uint32_t o = 8 * i;
+        uint64_t p0, p1;
+        alg_mul(WV(o), WV(o + 1), WV(o + 2), WV(o + 3), p0, p1);
+        const uint64_t c0 = gc[0], c1 = gc[N];
+        A.emit(gfn::sub(WV(o + 6), gfn::add(gfn::mul(p0, c0), gfn::mul(WV(o + 4), c1))));
+        A.emit(gfn::sub(WV(o + 7), gfn::add(gfn::mul(p1, c0), gfn::mul(WV(o + 5), c1))));
+      }
+      break;
+    case GK_MUL_EXT:  // per op: multiplicand_0, multiplicand_1, output
+      for (uint32_t i = 0; i < q0; i++) {
+        const uint32_t o = 6 * i;
+        uint64_t p0, p1;
+        alg_mul(WV(o), WV(o + 1), WV(o + 2), WV(o + 3), p0, p1);
+        A.emit(gfn::sub(WV(o + 4), gfn::mul(p0, gc[0])));
+        A.emit(gfn::sub(WV(o + 5), gfn::mul(p1, gc[0])));
+      }
+      break;
+    case GK_REDUCING:
+    case GK_REDUCING_EXT: {
+      // output 0..2, alpha 2..4, old_acc 4..6, coeffs from 6, then accumulators
+      const uint32_t cw = kind == GK_REDUCING ? 1 : 2, start_accs = 6 + cw * q0;
+      uint64_t a0 = WV(4), a1 = WV(5);
+      const uint64_t al0 = WV(2), al1 = WV(3);
+      for (uint32_t i = 0; i < q0; i++) {
+        uint64_t m0, m1;
+        alg_mul(a0, a1, al0, al1, m0, m1);
+        m0 = gfn::add(m0, WV(6 + cw * i));
+        if (cw == 2) m1 = gfn::add(m1, WV(7 + 2 * i));
+        const uint32_t ai = i == q0 - 1 ? 0 : start_accs + 2 * i;
+        a0 = WV(ai);
+        a1 = WV(ai + 1);
+        A.emit(gfn::sub(m0, a0));
+        A.emit(gfn::sub(m1, a1));
+      }
+      break;
+    }
+    case GK_EXPONENTIATION: {  // base 0, power bits 1.. (LE), output 1+nb, intermediates 2+nb..
+      const uint64_t base = WV(0);
+      uint64_t prev = 1;
+      for (uint32_t i = 0; i < q0; i++) {
+        const uint64_t bit = WV(1 + q0 - 1 - i);
+        const uint64_t comp = gfn::mul(prev, gfn::add(gfn::mul(bit, base), gfn::sub(1, bit)));
+        const uint64_t iv = WV(2 + q0 + i);
+        A.emit(gfn::sub(comp, iv));
+        prev = gfn::mul(iv, iv);
+      }
+      A.emit(gfn::sub(WV(1 + q0), WV(2 + q0 + q0 - 1)));
+      break;
+    }
+    case GK_POSEIDON_MDS:  // inputs 0..24, outputs 24..48 (ext pairs)
+      for (uint32_t r = 0; r < 12; r++) {
+        uint64_t a0 = 0, a1 = 0;
+        for (uint32_t i = 0; i < 12; i++) {
+          const uint32_t e = (i + r) % 12;
+          const uint64_t m = ps::mds_circ(i) + (r == 0 && i == 0 ? 8 : 0);
+          a0 = gfn::add(a0, gfn::mul(WV(2 * e), m));
+          a1 = gfn::add(a1, gfn::mul(WV(2 * e + 1), m));
+        }
+        A.emit(gfn::sub(WV(24 + 2 * r), a0));
+        A.emit(gfn::sub(WV(25 + 2 * r), a1));
+      }
+      break;
+    case GK_RANDOM_ACCESS: {  // q0 bits, q1 copies, q2 extra constants
+      const uint32_t vec = 1u << q0, routed = (2 + vec) * q1 + q2;
+      for (uint32_t cp = 0; cp < q1; cp++) {
+        const uint32_t base = (2 + vec) * cp, bw = routed + cp * q0;
+        for (uint32_t i = 0; i < q0; i++) {
+          const uint64_t b = WV(bw + i);
+          A.emit(gfn::mul(b, gfn::sub(b, 1)));
+        }
+        uint64_t idx = 0;
+        for (uint32_t i = q0; i-- > 0;) idx = gfn::add(gfn::add(idx, idx), WV(bw + i));
+        A.emit(gfn::sub(idx, WV(base)));
+        // the bit-by-bit fold of the list equals sum_i item_i prod_k (bit_k(i) ? b_k : 1 - b_k)
+        uint64_t sel = 0;
+        for (uint32_t i = 0; i < vec; i++) {
+          uint64_t wgt = 1;
+          for (uint32_t k = 0; k < q0; k++) {
+            const uint64_t b = WV(bw + k);
+            wgt = gfn::mul(wgt, (i >> k) & 1 ? b : gfn::sub(1, b));
+          }
+          sel = gfn::add(sel, gfn::mul(wgt, WV(base + 2 + i)));
+        }
+        A.emit(gfn::sub(sel, WV(base + 1)));
+      }
+      for (uint32_t i = 0; i < q2; i++) A.emit(gfn::sub(gc[(uint64_t)i * N], WV((2 + vec) * q1 + i)));
+      break;
+    }
+    case GK_COSET_INTERP: {  // q0 subgroup bits, q1 degree
+      const uint32_t np = 1u << q0, deg = q1, nint = (np - 2) / (deg - 1);
+      const uint32_t sv = 1, sep = sv + 2 * np, sev = sep + 2, si = sev + 2, ssh = si + 4 * nint;
+      const uint64_t om = gl::root_of_unity(q0), inv_n = gl::inv(np);
+      const uint64_t shift = WV(0), sp0 = WV(ssh), sp1 = WV(ssh + 1);
+      A.emit(gfn::sub(WV(sep), gfn::mul(sp0, shift)));
+      A.emit(gfn::sub(WV(sep + 1), gfn::mul(sp1, shift)));
+      uint64_t e0 = 0, e1 = 0, p0 = 1, p1 = 0, x = 1;
+      uint32_t lo = 0, hi = deg;
+      for (uint32_t it = 0;; it++) {
+        for (uint32_t i = lo; i < hi; i++) {
+          // barycentric weight over the whole subgroup: 1 / prod_{j != i}(x_i - x_j) = x_i / n
+          const uint64_t wt = gfn::mul(x, inv_n);
+          const uint64_t t0 = gfn::sub(sp0, x), t1 = sp1;
+          const uint64_t v0 = gfn::mul(WV(sv + 2 * i), wt), v1 = gfn::mul(WV(sv + 2 * i + 1), wt);
+          uint64_t a0, a1, b0, b1, n0, n1;
+          alg_mul(e0, e1, t0, t1, a0, a1);
+          alg_mul(v0, v1, p0, p1, b0, b1);
+          alg_mul(p0, p1, t0, t1, n0, n1);
+          e0 = gfn::add(a0, b0);
+          e1 = gfn::add(a1, b1);
+          p0 = n0;
+          p1 = n1;
+          x = gfn::mul(x, om);
+        }
+        if (it == nint) break;
+        const uint64_t ie0 = WV(si + 2 * it), ie1 = WV(si + 2 * it + 1);
+        const uint64_t ip0 = WV(si + 2 * (nint + it)), ip1 = WV(si + 2 * (nint + it) + 1);
+        A.emit(gfn::sub(ie0, e0));
+        A.emit(gfn::sub(ie1, e1));
+        A.emit(gfn::sub(ip0, p0));
+        A.emit(gfn::sub(ip1, p1));
+        e0 = ie0;
+        e1 = ie1;
+        p0 = ip0;
+        p1 = ip1;
+        lo = 1 + (deg - 1) * (it + 1);
+        hi = lo + deg - 1 < np ? lo + deg - 1 : np;
+      }
+      A.emit(gfn::sub(WV(sev), e0));
+      A.emit(gfn::sub(WV(sev + 1), e1));
+      break;
+    }
+    default:
+      break;
+  }
+}
+
 // Two phases with separate register allocation (the Poseidon gate alone is
 // a permutation's worth of live state; fused, the kernel needed 184 VGPRs =
 // 2 waves/SIMD):
@@ -317,6 +470,7 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(QP_QUO
           }
           break;
         default:
+          recursion_gate(kind, a.g.param[gi], a.g.param2[gi], a.g.param3[gi], wl, gc, N, A);
           break;
       }
     }

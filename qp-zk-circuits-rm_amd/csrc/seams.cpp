@@ -2,13 +2,16 @@
 // pieces of plonky2's prove() a patched qp-plonky2 routes to the GPU for ANY
 // circuit over the supported gate set, not only the built-in ones (the
 // aggregator's CircuitData::prove, wormhole/aggregator/src/circuits/tree.rs:136):
-//   qp_quotient          plonk/prover.rs compute_quotient_polys
+//   qp_quotient          plonk/prover.rs compute_quotient_polys (leaf gates: the
+//                        single-read kernel; any gate list: the generic one)
 //   qp_fri_layer_commit  fri/prover.rs fri_committed_trees, one reduction layer
 //   qp_fri_fold          the same loop's coefficient fold with beta
 //   qp_pow_grind         fri/prover.rs fri_proof_of_work (minimal witness)
 // The transcript stays with the caller: each seam consumes the challenges the
 // caller's Challenger drew and returns what it must observe next.
+#include <stdlib.h>
 #include <string.h>
+#include <string>
 #include <algorithm>
 #include <new>
 #include <vector>
@@ -31,6 +34,11 @@ struct DMem {  // device allocation owned by one call
 
 inline unsigned cdiv(uint64_t a, unsigned b) { return (unsigned)((a + b - 1) / b); }
 
+bool getenv_flag_eq(const char *name, const char *value) {
+  const char *v = getenv(name);
+  return v && !strcmp(v, value);
+}
+
 }  // namespace
 
 struct qp_fri_layer {
@@ -50,7 +58,7 @@ int qp_circuit_gate_desc(const qp_circuit *c, qp_gate_desc *g) {
   if (!c || !g) return QP_ERR_ARG;
   const qc::CircuitData &cd = c->cd;
   memset(g, 0, sizeof(*g));
-  if (cd.gate_kinds.size() > 8 || cd.groups.size() > 8) return QP_ERR_ARG;
+  if (cd.gate_kinds.size() > QP_MAX_GATES || cd.groups.size() > QP_MAX_GATES) return QP_ERR_ARG;
   g->num_gates = (uint32_t)cd.gate_kinds.size();
   for (uint32_t i = 0; i < g->num_gates; i++) {
     switch (cd.gate_kinds[i]) {
@@ -88,19 +96,65 @@ int qp_quotient(qp_ctx *ctx, const qp_batch *cs, const qp_batch *wires, const qp
   const uint32_t R = g->num_routed_wires, qdf = g->quotient_degree_factor, nc = g->num_challenges;
   const uint32_t nchunks = qdf ? (R + qdf - 1) / qdf : 0;
   const uint32_t nterms = nc + nc * nchunks + g->num_gate_constraints;
-  if (nc != 2 || g->num_gates == 0 || g->num_gates > 8 || g->num_selectors == 0 || g->num_selectors > 8 ||
-      qdf != (1u << rb) || logN > qpk::TW_LOG || log_n < 6 || nterms > qpk::APOW_STRIDE ||
-      wires->log_n != log_n || zs_pp->log_n != log_n || wires->rate_bits != rb || zs_pp->rate_bits != rb ||
-      cs->nbat != 1 || wires->nbat != 1 || zs_pp->nbat != 1 || cs->npolys != g->num_constants + R ||
-      wires->npolys != g->num_wires || zs_pp->npolys != nc * nchunks || wires->nsalt || zs_pp->nsalt || cs->nsalt) {
+  if (nc != 2 || g->num_gates == 0 || g->num_gates > QP_MAX_GATES || g->num_selectors == 0 ||
+      g->num_selectors > QP_MAX_GATES || qdf != (1u << rb) || logN > qpk::TW_LOG || log_n < 6 ||
+      nterms > qpk::APOW_STRIDE || wires->log_n != log_n || zs_pp->log_n != log_n || wires->rate_bits != rb ||
+      zs_pp->rate_bits != rb || cs->nbat != 1 || wires->nbat != 1 || zs_pp->nbat != 1 ||
+      cs->npolys != g->num_constants + R || wires->npolys != g->num_wires || zs_pp->npolys != nc * nchunks ||
+      wires->nsalt || zs_pp->nsalt || cs->nsalt || R > g->num_wires) {
     ctx->err = "qp_quotient: unsupported shape (2 challenges, qdf = 2^rate_bits, unsalted batches of one)";
     return QP_ERR_ARG;
   }
-  for (uint32_t i = 0; i < g->num_gates; i++)
-    if (g->kind[i] > QP_GATE_POSEIDON || g->selector_index[i] >= g->num_selectors) {
-      ctx->err = "qp_quotient: unknown gate kind or selector";
+  // per-gate checks: known kind, selector in range, parameters inside the
+  // kernels' bounds, every wire a gate reads < num_wires, every gate constant
+  // < num_constants - num_selectors, constraint count <= num_gate_constraints
+  const uint32_t W = g->num_wires, n_gc = g->num_constants - g->num_selectors;
+  bool fast = g->num_gates <= 8 && !getenv_flag_eq("QPGPU_QUOTIENT", "generic");
+  uint32_t seen = 0;
+  for (uint32_t i = 0; i < g->num_gates; i++) {
+    const uint32_t k = g->kind[i], p = g->param[i], p2 = g->param2[i], p3 = g->param3[i];
+    uint64_t wires_used = 0, consts_used = 0, ncons = 0;
+    bool ok = g->selector_index[i] < g->num_selectors;
+    switch (k) {
+      case QP_GATE_NOOP: break;
+      case QP_GATE_CONSTANT: wires_used = p; consts_used = p; ncons = p; break;
+      case QP_GATE_PUBLIC_INPUT: wires_used = 4; ncons = 4; break;
+      case QP_GATE_BASE_SUM: wires_used = 1ull + p; ncons = 1ull + p; break;
+      case QP_GATE_ARITHMETIC: wires_used = 4ull * p; consts_used = 2; ncons = p; break;
+      case QP_GATE_POSEIDON: wires_used = 135; ncons = 123; break;
+      case QP_GATE_ARITHMETIC_EXTENSION: wires_used = 8ull * p; consts_used = 2; ncons = 2ull * p; break;
+      case QP_GATE_MUL_EXTENSION: wires_used = 6ull * p; consts_used = 1; ncons = 2ull * p; break;
+      case QP_GATE_RANDOM_ACCESS:
+        ok = ok && p >= 1 && p <= 6;
+        wires_used = (2ull + (1ull << (p & 63))) * p2 + p3 + (uint64_t)p2 * p;
+        consts_used = p3;
+        ncons = (p + 2ull) * p2 + p3;
+        break;
+      case QP_GATE_EXPONENTIATION: ok = ok && p >= 1; wires_used = 2ull + 2ull * p; ncons = p + 1ull; break;
+      case QP_GATE_REDUCING: ok = ok && p >= 1; wires_used = 6ull + p + 2ull * (p - 1); ncons = 2ull * p; break;
+      case QP_GATE_REDUCING_EXTENSION:
+        ok = ok && p >= 1;
+        wires_used = 6ull + 2ull * p + 2ull * (p - 1);
+        ncons = 2ull * p;
+        break;
+      case QP_GATE_POSEIDON_MDS: wires_used = 48; ncons = 24; break;
+      case QP_GATE_COSET_INTERPOLATION: {
+        ok = ok && p >= 2 && p <= 6 && p2 >= 2 && p2 <= (1u << p);
+        const uint64_t np = 1ull << (p & 63), nint = ok ? (np - 2) / (p2 - 1) : 0;
+        wires_used = 1 + 2 * np + 4 + 4 * nint + 2;
+        ncons = 4 + 4 * nint;
+        break;
+      }
+      default: ok = false; break;
+    }
+    if (!ok || wires_used > W || consts_used > n_gc || ncons > g->num_gate_constraints) {
+      ctx->err = "qp_quotient: gate " + std::to_string(i) + ": unknown gate kind, selector or parameters";
       return QP_ERR_ARG;
     }
+    // the single-read kernel: the six leaf-circuit kinds, each at most once
+    if (k > QP_GATE_POSEIDON || (seen >> k) & 1) fast = false;
+    seen |= 1u << k;
+  }
   const uint64_t n = 1ull << log_n, N = 1ull << logN;
   QP_HIP_TRY(ctx, hipSetDevice(ctx->device));
   hipStream_t s = ctx->stream;
@@ -156,13 +210,16 @@ int qp_quotient(qp_ctx *ctx, const qp_batch *cs, const qp_batch *wires, const qp
     for (uint32_t i = 0; i < g->num_gates; i++) {
       a.g.kind[i] = g->kind[i];
       a.g.param[i] = g->param[i];
+      a.g.param2[i] = g->param2[i];
+      a.g.param3[i] = g->param3[i];
       a.g.sel_index[i] = g->selector_index[i];
     }
     for (uint32_t i = 0; i < g->num_selectors; i++) {
       a.g.grp_lo[i] = g->group_lo[i];
       a.g.grp_hi[i] = g->group_hi[i];
     }
-    qpk::k_quotient_1r<<<dim3(cdiv(N, 256), 1), 256, 0, s>>>(a);
+    if (fast) qpk::k_quotient_1r<<<dim3(cdiv(N, 256), 1), 256, 0, s>>>(a);
+    else qpk::k_quotient<2><<<dim3(cdiv(N, 256), 1), 256, 0, s>>>(a);  // any gate list
     const uint64_t n_inv = gl::inv(n);
     qpk::k_qintt_blocks<<<dim3(B, nc, 1), 512, 8u * qpk::ntt_lds_words(1u << log_n), s>>>(
         d_q.p, d_cbuf.p, log_n, rb, 2 * N, 2 * N, ctx->tw.fwd, ctx->tw.inv, n_inv, gl::inv(gl::GEN));

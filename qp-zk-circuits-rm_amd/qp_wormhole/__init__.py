@@ -5,7 +5,7 @@ Mirrors qp-wormhole-prover's WormholeProver (wormhole/prover/src/lib.rs:74-237)
 and plonky2's PolynomialBatch for the parity tests.  The HIP library is the
 only backend: importing the native pieces raises if it is not built.
 """
-from ._native import (Context, FriLayer, GateDesc, PolynomialBatch, QpError, fri_fold, gate_desc,  # noqa: F401
+from ._native import (GATE_KINDS, Context, FriLayer, GateDesc, PolynomialBatch, QpError, fri_fold, gate_desc,  # noqa: F401
                       header_symbols, ifft, lde, lib, poseidon_permute, pow_grind, quotient)
 
 from .circuits import (Circuit, CircuitInputs, PrivateCircuitInputs, ProcessedStorageProof,  # noqa: F401,E402

@@ -22,14 +22,42 @@ STATUS = {0: "QP_OK", 1: "QP_ERR_ARG", 2: "QP_ERR_HIP", 3: "QP_ERR_OOM", 4: "QP_
           5: "QP_ERR_WITNESS", 6: "QP_ERR_FORMAT"}
 
 
+MAX_GATES = 16
+GATE_KINDS = ["noop", "constant", "public_input", "base_sum", "arithmetic", "poseidon", "arithmetic_extension",
+              "mul_extension", "random_access", "exponentiation", "reducing", "reducing_extension", "poseidon_mds",
+              "coset_interpolation"]  # QP_GATE_* order
+
+
 class GateDesc(ctypes.Structure):
     """qp_gate_desc: the parts of CommonCircuitData the vanishing polynomial reads."""
-    _fields_ = [("num_gates", ctypes.c_uint32), ("kind", ctypes.c_uint32 * 8), ("param", ctypes.c_uint32 * 8),
-                ("selector_index", ctypes.c_uint32 * 8), ("num_selectors", ctypes.c_uint32),
-                ("group_lo", ctypes.c_uint32 * 8), ("group_hi", ctypes.c_uint32 * 8),
-                ("num_constants", ctypes.c_uint32), ("num_routed_wires", ctypes.c_uint32),
-                ("num_wires", ctypes.c_uint32), ("quotient_degree_factor", ctypes.c_uint32),
-                ("num_challenges", ctypes.c_uint32), ("num_gate_constraints", ctypes.c_uint32)]
+    _fields_ = [("num_gates", ctypes.c_uint32), ("kind", ctypes.c_uint32 * MAX_GATES),
+                ("param", ctypes.c_uint32 * MAX_GATES), ("param2", ctypes.c_uint32 * MAX_GATES),
+                ("param3", ctypes.c_uint32 * MAX_GATES), ("selector_index", ctypes.c_uint32 * MAX_GATES),
+                ("num_selectors", ctypes.c_uint32), ("group_lo", ctypes.c_uint32 * MAX_GATES),
+                ("group_hi", ctypes.c_uint32 * MAX_GATES), ("num_constants", ctypes.c_uint32),
+                ("num_routed_wires", ctypes.c_uint32), ("num_wires", ctypes.c_uint32),
+                ("quotient_degree_factor", ctypes.c_uint32), ("num_challenges", ctypes.c_uint32),
+                ("num_gate_constraints", ctypes.c_uint32)]
+
+    @classmethod
+    def build(cls, gates, groups, num_wires=135, num_routed_wires=80, num_gate_constants=2, rate_bits=3,
+              num_gate_constraints=None):
+        """gates: [(kind name, params tuple, selector index)], groups: [(lo, hi)]"""
+        g = cls()
+        g.num_gates = len(gates)
+        for i, (kind, params, sel) in enumerate(gates):
+            g.kind[i] = GATE_KINDS.index(kind)
+            params = tuple(params) + (0, 0, 0)
+            g.param[i], g.param2[i], g.param3[i] = params[:3]
+            g.selector_index[i] = sel
+        g.num_selectors = len(groups)
+        for i, (lo, hi) in enumerate(groups):
+            g.group_lo[i], g.group_hi[i] = lo, hi
+        g.num_constants = len(groups) + num_gate_constants
+        g.num_routed_wires, g.num_wires = num_routed_wires, num_wires
+        g.quotient_degree_factor, g.num_challenges = 1 << rate_bits, 2
+        g.num_gate_constraints = num_gate_constraints or 0
+        return g
 
 
 class QpError(RuntimeError):

@@ -58,6 +58,10 @@ def lib():
                                     U64P, np.ctypeslib.ndpointer(np.uint32, flags="C_CONTIGUOUS"), ctypes.c_uint,
                                     U64P, U64P]
         L.ora_fri_fold.argtypes = [U64P, ctypes.c_uint, ctypes.c_uint, U64P, U64P]
+        L.ora_quotient_desc.argtypes = [ctypes.c_void_p, ctypes.c_uint, ctypes.c_uint, U64P, U64P, U64P, U64P, U64P,
+                                        U64P, U64P, U64P]
+        L.ora_gate_eval.restype = ctypes.c_long
+        L.ora_gate_eval.argtypes = [ctypes.c_void_p, ctypes.c_uint, U64P, U64P, U64P, U64P]
         L.ora_pow_grind.restype = ctypes.c_uint64
         L.ora_pow_grind.argtypes = [U64P, ctypes.c_uint, ctypes.c_uint]
         _lib = L

@@ -70,6 +70,81 @@ def test_quotient_matches_oracle(ctx, circuit):
 
 
 @pytest.mark.gpu
+def test_quotient_generic_kernel_matches_oracle(ctx, circuit, monkeypatch):
+    """The any-gate-list kernel (QPGPU_QUOTIENT=generic forces it) on the Wormhole circuit."""
+    import qp_wormhole
+    monkeypatch.setenv("QPGPU_QUOTIENT", "generic")
+    rng = np.random.default_rng(43)
+    g = qp_wormhole.gate_desc(circuit)
+    n = circuit.n
+    cs = circuit.constants_sigmas()
+    wires = rand_felts(rng, circuit.num_wires, n)
+    zs = rand_felts(rng, 20, n)
+    betas, gammas, alphas, pih = rand_felts(rng, 2), rand_felts(rng, 2), rand_felts(rng, 2), rand_felts(rng, 4)
+    B = [qp_wormhole.PolynomialBatch.from_values(ctx, v, 3, 4) for v in (cs, wires, zs)]
+    got = qp_wormhole.quotient(ctx, B[0], B[1], B[2], g, betas, gammas, alphas, pih)
+    want = np.zeros_like(got)
+    cb = circuit.common_data()
+    assert olib().ora_quotient(cb, len(cb), cs, wires, zs, betas, gammas, alphas, pih, want) == 0
+    assert (got == want).all()
+
+
+# the recursive-verifier gate set with standard_recursion_config parameters (plonky2
+# *::new_from_config for 135 wires / 80 routed), three selector groups
+RECURSION_GATES = [
+    ("noop", (), 0), ("constant", (2,), 0), ("public_input", (), 0), ("base_sum", (63,), 0), ("arithmetic", (20,), 0),
+    ("poseidon", (), 1), ("arithmetic_extension", (10,), 1), ("mul_extension", (13,), 1),
+    ("random_access", (4, 4, 2), 1), ("exponentiation", (66,), 1),
+    ("reducing", (43,), 2), ("reducing_extension", (32,), 2), ("poseidon_mds", (), 2),
+    ("coset_interpolation", (4, 6), 2),
+]
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("log_n", [8, 10])
+def test_quotient_recursion_gate_set_matches_oracle(ctx, log_n):
+    """qp_quotient over the aggregator circuits' gate list (generic kernel) vs the
+    descriptor-driven oracle; random selector values make every gate's filter
+    nonzero, so every constraint of every gate reaches the quotient."""
+    import ctypes
+
+    import qp_wormhole
+    g = qp_wormhole.GateDesc.build(RECURSION_GATES, [(0, 5), (5, 10), (10, 14)], num_gate_constraints=123)
+    rng = np.random.default_rng(log_n)
+    n = 1 << log_n
+    cs = rand_felts(rng, g.num_constants + 80, n)
+    wires = rand_felts(rng, 135, n)
+    zs = rand_felts(rng, 20, n)
+    betas, gammas, alphas, pih = rand_felts(rng, 2), rand_felts(rng, 2), rand_felts(rng, 2), rand_felts(rng, 4)
+    B = [qp_wormhole.PolynomialBatch.from_values(ctx, v, 3, 4) for v in (cs, wires, zs)]
+    got = qp_wormhole.quotient(ctx, B[0], B[1], B[2], g, betas, gammas, alphas, pih)
+    want = np.zeros_like(got)
+    assert olib().ora_quotient_desc(ctypes.addressof(g), log_n, 3, cs, wires, zs, betas, gammas, alphas, pih,
+                                    want) == 0
+    assert (got == want).all(), np.argwhere(got != want)[:4]
+
+
+@pytest.mark.gpu
+def test_quotient_rejects_bad_gate_parameters(ctx):
+    import qp_wormhole
+    rng = np.random.default_rng(44)
+    n = 1 << 8
+    cs = qp_wormhole.PolynomialBatch.from_values(ctx, rand_felts(rng, 83, n), 3, 4)
+    w = qp_wormhole.PolynomialBatch.from_values(ctx, rand_felts(rng, 135, n), 3, 4)
+    z = qp_wormhole.PolynomialBatch.from_values(ctx, rand_felts(rng, 20, n), 3, 4)
+    two, four = np.ones(2, np.uint64), np.zeros(4, np.uint64)
+    for gates in ([("reducing", (70,), 0)],                 # 6 + 70 + 138 wires > 135
+                  [("random_access", (7, 1, 0), 0)],         # 2^7-item lists
+                  [("exponentiation", (40,), 0)] * 17):      # more than 16 gates
+        g = qp_wormhole.GateDesc.build(gates[:16] if len(gates) <= 16 else gates[:16], [(0, 1)],
+                                       num_gate_constraints=123)
+        if len(gates) > 16:
+            g.num_gates = 17
+        with pytest.raises(qp_wormhole.QpError, match="QP_ERR_ARG"):
+            qp_wormhole.quotient(ctx, cs, w, z, g, two, two, two, four)
+
+
+@pytest.mark.gpu
 def test_quotient_rejects_bad_shapes(ctx, circuit):
     import qp_wormhole
     rng = np.random.default_rng(42)
