@@ -156,7 +156,7 @@ def test_quotient_rejects_bad_shapes(ctx, circuit):
     two = np.ones(2, np.uint64)
     with pytest.raises(qp_wormhole.QpError, match="QP_ERR_ARG"):
         qp_wormhole.quotient(ctx, cs, w, z_bad, g, two, two, two, np.zeros(4, np.uint64))
-    g.kind[3] = 9
+    g.kind[3] = 99
     z = qp_wormhole.PolynomialBatch.from_values(ctx, rand_felts(rng, 20, n), 3, 4)
     with pytest.raises(qp_wormhole.QpError, match="unknown gate kind"):
         qp_wormhole.quotient(ctx, cs, w, z, g, two, two, two, np.zeros(4, np.uint64))
