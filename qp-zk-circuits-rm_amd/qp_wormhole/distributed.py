@@ -37,16 +37,24 @@ def unpack_proofs(arr: np.ndarray):
 
 
 def gather_proofs(proofs, slot: int, dist, device="cpu", dst: int = 0):
-    """Gather every rank's proofs to `dst` (rank order).  All ranks must pass the
-    same number of proofs (bench shards evenly); returns the list on dst, None elsewhere."""
+    """Gather every rank's proofs to `dst` in rank order; returns the list on dst,
+    None elsewhere.  Shards may differ in size (2048 over 3 ranks): counts are
+    exchanged first and short shards padded with empty entries, which dst drops
+    (a serialized proof is never empty)."""
     import torch
-    t = torch.from_numpy(pack_proofs(proofs, slot)).to(device)
     rank, world = dist.get_rank(), dist.get_world_size()
+    if any(len(p) == 0 for p in proofs):
+        raise ValueError("empty proof")
+    cnt = torch.tensor([len(proofs)], dtype=torch.int64, device=device)
+    counts = [torch.zeros_like(cnt) for _ in range(world)]
+    dist.all_gather(counts, cnt)
+    most = int(max(int(c.item()) for c in counts))
+    t = torch.from_numpy(pack_proofs(list(proofs) + [b""] * (most - len(proofs)), slot)).to(device)
     bufs = [torch.empty_like(t) for _ in range(world)] if rank == dst else None
     dist.gather(t, bufs, dst=dst)
     if rank != dst:
         return None
     out = []
     for b in bufs:
-        out.extend(unpack_proofs(b.cpu().numpy()))
+        out.extend(p for p in unpack_proofs(b.cpu().numpy()) if p)
     return out

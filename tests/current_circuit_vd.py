@@ -15,6 +15,8 @@ hash_no_pad(cap || hash_pad([]) || degree_bits) (plonk/circuit_builder.rs build)
 Test infrastructure: uses the oracle as the checker.
 """
 import functools
+import json
+import os
 import struct
 
 import numpy as np
@@ -79,10 +81,26 @@ def query_leaf_index(pf, q):
     return int(L.ora_merkle_find_index(leaf, 135, sibs, len(sibs) // 4, caps, 4))
 
 
+INDEX_FILE = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden", "dummy_query_indices.json")
+
+
+def brute_force_query_indices(name, count=None):
+    """Leaf indices of the fixture's queries by searching the wires Merkle paths (slow: ~25 s)."""
+    pf = golden(name)
+    return tuple(query_leaf_index(pf, q) for q in parse_queries(pf)[:count])
+
+
 @functools.lru_cache(maxsize=None)
 def query_indices(name):
-    pf = golden(name)
-    return tuple(query_leaf_index(pf, q) for q in parse_queries(pf))
+    """The query leaf indices, from tests/golden/dummy_query_indices.json (written by
+    `python tests/current_circuit_vd.py` with brute_force_query_indices; the fixture
+    tests re-derive them from the transcript and spot-check the search)."""
+    if os.path.exists(INDEX_FILE):
+        with open(INDEX_FILE) as f:
+            idx = json.load(f)
+        if name in idx:
+            return tuple(idx[name])
+    return brute_force_query_indices(name)
 
 
 @functools.lru_cache(maxsize=None)
@@ -107,3 +125,10 @@ def current_circuit_verifier_data(common_bytes):
     dig = np.zeros(4, np.uint64)
     lib().ora_circuit_digest(cap.reshape(-1).copy(), 16, 13, dig)
     return struct.pack("<Q", 4) + cap.tobytes() + dig.tobytes() + common_bytes, cap, dig
+
+
+if __name__ == "__main__":
+    data = {n: list(brute_force_query_indices(n)) for n in ("dummy_proof.bin", "dummy_proof_zk.bin")}
+    data["source"] = "leaf indices of the 28 queries of wormhole/aggregator/data/dummy_proof{,_zk}.bin (Merkle search)"
+    with open(INDEX_FILE, "w") as f:
+        json.dump(data, f, indent=1)

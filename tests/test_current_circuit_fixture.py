@@ -16,7 +16,8 @@ This pins, by a reference-held fixture rather than by synthesis:
 import numpy as np
 import pytest
 
-from current_circuit_vd import constants_sigmas_cap_entries, current_circuit_verifier_data, query_indices
+from current_circuit_vd import (brute_force_query_indices, constants_sigmas_cap_entries,
+                                current_circuit_verifier_data, query_indices)
 from oracle_lib import golden, lib
 from test_oracle_golden import current_common_bytes
 
@@ -76,3 +77,10 @@ def test_native_circuit_common_data_is_the_verified_one():
     from qp_wormhole import Circuit
     c = Circuit.wormhole()
     assert c.common_data() == current_common_bytes()
+
+
+@pytest.mark.parametrize("name", ["dummy_proof.bin", "dummy_proof_zk.bin"])
+def test_committed_query_indices_match_the_merkle_search(name):
+    """tests/golden/dummy_query_indices.json against a fresh Merkle-path search
+    (first 3 queries; the transcript test above covers all 28)."""
+    assert brute_force_query_indices(name, 3) == query_indices(name)[:3]

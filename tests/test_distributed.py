@@ -48,17 +48,54 @@ def _worker(rank, world, port, q):
     dist.destroy_process_group()
 
 
-def test_gather_world2_gloo():
+def _run(target, world, *args):
     import torch.multiprocessing as mp
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
-    procs = [ctx.Process(target=_worker, args=(r, 2, port, q)) for r in range(2)]
+    procs = [ctx.Process(target=target, args=(r, world, port, q) + args) for r in range(world)]
     for p in procs:
         p.start()
-    got = q.get(timeout=120)
+    got = q.get(timeout=180)
     for p in procs:
-        p.join(timeout=120)
+        p.join(timeout=180)
         assert p.exitcode == 0
+    return got
+
+
+def test_gather_world2_gloo():
+    got = _run(_worker, 2)
     expect = [bytes([r * 16 + i]) * (1000 + r) for r in range(2) for i in shard(8, r, 2)]
     assert got == expect
+
+
+def _worker_real(rank, world, port, q, total):
+    """Each rank ships its shard of the reference's own current-circuit proofs
+    (tests/golden/dummy_proof{,_zk}.bin, 132,712 B each, alternating); rank 0
+    verifies every gathered proof under the reconstructed verifier data."""
+    import torch.distributed as dist
+
+    from qp_wormhole.distributed import gather_proofs
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    from oracle_lib import golden
+    fixtures = [golden("dummy_proof.bin"), golden("dummy_proof_zk.bin")]
+    mine = [fixtures[i % 2] for i in shard(total, rank, world)]
+    got = gather_proofs(mine, 140000, dist)
+    if rank == 0:
+        from current_circuit_vd import current_circuit_verifier_data
+        from oracle_lib import lib as olib
+        from test_oracle_golden import current_common_bytes
+        vd = current_circuit_verifier_data(current_common_bytes())[0]
+        ok = [olib().ora_verify(vd, len(vd), p, len(p)) == 0 for p in got]
+        q.put((len(got), [p == fixtures[i % 2] for i, p in enumerate(got)], ok))
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("world,total", [(2, 2), (3, 4)])
+def test_gather_real_proofs_verify(world, total):
+    """Uneven shards (4 over 3 ranks) gather in order and every proof verifies on rank 0."""
+    n, same, ok = _run(_worker_real, world, total)
+    assert n == total and all(same) and all(ok)
