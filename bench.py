@@ -243,6 +243,25 @@ def main():
             prover.prove_inputs_array(one, 1)
             ts.append((time.perf_counter() - t1) * 1e3)
         lat = sorted(ts)[1]
+    # standard_recursion_zk_config (the reference's cargo-bench and aggregator config):
+    # under no_random it proves the same circuit without salts, one prover, one batch
+    zk = None
+    if rank == 0 and not voting and args.mode == "e2e":
+        zc = qp_wormhole.Circuit.wormhole(zero_knowledge=True)
+        zp = qp_wormhole.Prover(qp_wormhole.Context(local), zc, max_batch=per[0])
+        zin = zp.inputs_array(inputs[:per[0]])
+        zp.prove_inputs_array(zin, per[0])
+        t1 = time.perf_counter()
+        zproofs = zp.prove_inputs_array(zin, per[0])
+        zdt = time.perf_counter() - t1
+        zok = None
+        if args.warmup:
+            from oracle_lib import lib as olib
+            zvd = zp.verifier_data()
+            zok = olib().ora_verify(zvd, len(zvd), zproofs[0], len(zproofs[0])) == 0
+        zk = {"proofs_per_s_1prover": per[0] / zdt, "proofs_per_launch": per[0], "proof_verified": zok,
+              "note": "standard_recursion_zk_config, e2e, one prover (the headline runs two)"}
+        zp.free()
     if rank == 0:
         total = world * B * args.steps
         lde = ks["lde_wires"]
@@ -291,6 +310,7 @@ def main():
             "stage_ms_per_step": {k: v / args.steps for k, v in stages.items()},
             "proof_bytes": len(proofs[0]),
             "latency_1proof_ms": lat,
+            "zk_config": zk,
             "prove_only_1prover_proofs_per_s": prove_only,
             "warmup_proof_verified": verified,
         }
