@@ -90,10 +90,13 @@ __device__ __forceinline__ void permute_nc_v1(uint64_t s[12]) {
 }
 
 // permutation used by the kernels: poseidon_fast.h (2.24 vs 1.67 Gperm/s for
-// permute_nc_v1 on MI355X, tools/poseidon_ubench.hip).  Inputs in [0,2^64),
-// outputs in [0,2^64) (call canon on lanes read out)
+// permute_nc_v1 on MI355X, tools/poseidon_ubench.hip).  Mode 3 (each MDS row
+// one asm block: no compiler hazard s_nops between the mads): 2.35 Gperm/s in
+// isolation, leaf hash -0.8 %, Merkle levels -6 %, e2e 932 -> 942 proofs/s
+// (profiles/r02_ab_poseidon_mode3.log).  Inputs in [0,2^64), outputs in
+// [0,2^64) (call canon on lanes read out)
 #ifndef QP_POSEIDON_MODE
-#define QP_POSEIDON_MODE 0
+#define QP_POSEIDON_MODE 3
 #endif
 __device__ __forceinline__ void permute_nc(uint64_t s[12]) { pf::permute_nc<QP_POSEIDON_MODE>(s); }
 
