@@ -37,7 +37,7 @@ HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec peak (MI355X_MICROARCH.md)
 # HBM traffic of the roofline kernel from rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE
 # passes (tools/pmc_summary.py applies the gfx950 corrections); per proof, scaled
 # to the bench's per-launch proof count
-PMC_FILE = os.path.join(ROOT, "profiles", "r02_pmc_hbm_b128.json")
+PMC_FILE = os.path.join(ROOT, "profiles", "r02_v6_pmc_hbm_b128.json")
 
 
 def pmc_traffic(kernel, ncols, log_n, proofs, lanes_per_proof=None):
@@ -295,7 +295,7 @@ def main():
                                                 per[0]) if circuit.degree_bits == 13 else None,
                          "traffic_unit": "bytes per launch",
                          "algorithmic_bytes_per_launch": lde["units"] / max(lde["launches"], 1),
-                         "traffic_source": "profiles/r02_pmc_hbm_b128.json (rocprofv3 --pmc FETCH_SIZE, WRITE_SIZE "
+                         "traffic_source": "profiles/r02_v6_pmc_hbm_b128.json (rocprofv3 --pmc FETCH_SIZE, WRITE_SIZE "
                                            "passes of this bench at batch 128), per proof x proofs per launch",
                          "avg_launch_ms": lde["ms"] / max(lde["launches"], 1),
                          "note": "HIP events on the prover stream around each launch of the kernel"},
@@ -329,10 +329,11 @@ def main():
                                f"the timed region, where {NP} provers' kernels share the GPU"})
             lh, qk = iso["leaf_hash_wires"], iso["quotient"]
             if lh["ms"] and qk["ms"]:
-                rec["valu_kernels"] = {"leaf_hash_wires_perms_per_s": lh["units"] / (lh["ms"] * 1e-3),
-                                       "avg_launch_ms": lh["ms"] / max(lh["launches"], 1),
-                                       "quotient_avg_launch_ms": qk["ms"] / max(qk["launches"], 1),
-                                       "proofs_per_launch": per[0], "note": "isolated pass, as roofline.achieved"}
+                rec["valu_kernels"].update({"leaf_hash_wires_perms_per_s": lh["units"] / (lh["ms"] * 1e-3),
+                                            "avg_launch_ms": lh["ms"] / max(lh["launches"], 1),
+                                            "quotient_avg_launch_ms": qk["ms"] / max(qk["launches"], 1),
+                                            "proofs_per_launch": per[0],
+                                            "note": "isolated pass, as roofline.achieved; HBM bytes: PMC file"})
         rec["stage_ms_per_step"]["note"] = f"prover 0 ({per[0]} proofs), host + device"
         if world == 1 and args.cpu_sample > 0:
             rec["cpu_baseline"] = cpu_baseline(circuit, wires, pis, args.cpu_sample, args.cpu_seconds)

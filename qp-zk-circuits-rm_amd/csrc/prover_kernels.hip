@@ -153,7 +153,29 @@ __device__ __forceinline__ void rc_row(uint64_t k[12], int r) {
   for (int i = 0; i < 12; i++) k[i] = ps::RC_DEV[r * 12 + i];
 }
 
+// wire reader of the Poseidon gate: wires below `nstash` come from an LDS copy
+// made while they streamed by (k_quotient_1r), the rest from HBM
+struct WireRead {
+  const uint64_t *__restrict__ wl;
+  uint64_t N;
+  const uint64_t *stash;  // [nstash][blockDim.x], this lane's column at stash + threadIdx.x
+  uint32_t nstash;
+  __device__ __forceinline__ uint64_t operator()(uint32_t j) const {
+    return j < nstash ? stash[j * blockDim.x + threadIdx.x] : wl[(uint64_t)j * N];
+  }
+};
+
+template <class RD>
+__device__ __forceinline__ void poseidon_gate_rd(const RD &WR, TermAcc &A);
+
 __device__ __forceinline__ void poseidon_gate(const uint64_t *__restrict__ wl, uint64_t N, TermAcc &A) {
+  WireRead rd{wl, N, nullptr, 0};
+  poseidon_gate_rd(rd, A);
+}
+
+template <class RD>
+__device__ __forceinline__ void poseidon_gate_rd(const RD &WR, TermAcc &A) {
+#define WV(j) WR(j)
   const uint64_t swap = WV(24);
   A.emit(gfn::mul(swap, gfn::sub(swap, 1)));
   uint64_t s[12], k[12];
@@ -209,6 +231,8 @@ __device__ __forceinline__ void poseidon_gate(const uint64_t *__restrict__ wl, u
   }
 #pragma unroll
   for (int i = 0; i < 12; i++) A.emit(gfn::sub(s[i], WV(12 + i)));
+#undef WV
+#define WV(j) wl[(uint64_t)(j) * N]
 }
 
 // Recursive-verifier gates (the aggregator circuits, tree.rs:106-143), evaluated
@@ -510,6 +534,11 @@ __device__ __forceinline__ uint64_t mul_pow2_rt(uint64_t x, uint32_t e) {
   return e ? gfn::reduce(x << e, x >> (64 - e)) : x;
 }
 
+// wires kept in LDS for the Poseidon gate: 16 x 256 lanes x 8 B = 32 KB per
+// workgroup, 5 workgroups per CU (4 waves/SIMD need 4)
+#ifndef QP_QSTASH
+#define QP_QSTASH 16
+#endif
 __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(QP_QUOTIENT_WAVES)))
 k_quotient_1r(QuotientArgs a) {
   const uint32_t logN = a.log_n + a.rate_bits;
@@ -560,8 +589,13 @@ k_quotient_1r(QuotientArgs a) {
   // per-gate alpha sums (multiplied by the gate's filter at the end)
   uint64_t sc0 = 0, sc1 = 0, sp0 = 0, sp1 = 0, sb0 = 0, sb1 = 0, sa0 = 0, sa1 = 0;
   uint64_t bs_acc = 0, w0 = 0, wa0 = 0, wa1 = 0, wa2 = 0;
+  // the Poseidon gate reads wires 0..23 again after the sweep: the first
+  // QP_QSTASH of them are kept in LDS (per lane, conflict-free [j][lane])
+  __shared__ uint64_t stash[(QP_QSTASH ? QP_QSTASH : 1) * 256];
+  const uint32_t nst = g_pos >= 0 ? (R < QP_QSTASH ? R : QP_QSTASH) : 0;
   for (uint32_t jj = 0; jj < R; jj++) {
     const uint64_t w = WV(jj);
+    if (jj < nst) stash[jj * blockDim.x + threadIdx.x] = w;
     // permutation argument, both challenges (k_j = g^j folded into bkx)
     const uint64_t sg = cs[(uint64_t)(a.num_constants + jj) * N];
     num0 = gfn::mul(num0, gfn::add(gfn::add_c(w, gamma0), bkx0));
@@ -639,7 +673,8 @@ k_quotient_1r(QuotientArgs a) {
     A.p1 = p1;
     A.s0 = A.s1 = 0;
     A.i = pre;
-    poseidon_gate(wl, N, A);
+    WireRead rd{wl, N, stash, nst};
+    poseidon_gate_rd(rd, A);
     const uint64_t f = filter(g_pos);
     acc0 = gfn::add(acc0, gfn::mul(f, A.s0));
     acc1 = gfn::add(acc1, gfn::mul(f, A.s1));
