@@ -76,6 +76,50 @@ static void batch_inv(gl_t *v, size_t n) {
     free(pre);
 }
 
+/* wires_permutation_partial_products_and_zs (plonk/prover.rs): values of
+ * [Z_0..Z_nc-1, partial products of challenge 0, of challenge 1, ...] over H */
+static void zs_values(const or_common_t *cp, unsigned log_n, const gl_t *consts_sigmas, const gl_t *wires,
+                      const gl_t *betas, const gl_t *gammas, gl_t *zs_vals) {
+    const or_common_t c = *cp;
+    const size_t n = (size_t)1 << log_n;
+    const unsigned nc = (unsigned)c.num_challenges, R = (unsigned)c.num_routed_wires;
+    const unsigned NCONST = (unsigned)c.num_constants, npp = (unsigned)c.num_partial_products;
+    const unsigned qdf = (unsigned)c.quotient_degree_factor;
+    const gl_t w = gl_root_of_unity(log_n);
+    const gl_t *sig = consts_sigmas + (size_t)NCONST * n;
+    unsigned nchunks = (R + qdf - 1) / qdf;
+    gl_t *chunkprod = malloc((size_t)n * nchunks * sizeof(gl_t));
+    for (unsigned ch = 0; ch < nc; ch++) {
+        gl_t x = 1;
+        for (size_t i = 0; i < n; i++) {
+            gl_t den[256], num[256];
+            for (unsigned j = 0; j < R; j++) {
+                gl_t wv = wires[(size_t)j * n + i];
+                num[j] = gl_add(gl_add(wv, gl_mul(betas[ch], gl_mul(c.k_is[j], x))), gammas[ch]);
+                den[j] = gl_add(gl_add(wv, gl_mul(betas[ch], sig[(size_t)j * n + i])), gammas[ch]);
+            }
+            batch_inv(den, R);
+            for (unsigned k = 0; k < nchunks; k++) {
+                gl_t pr = 1;
+                for (unsigned j = k * qdf; j < (k + 1) * qdf && j < R; j++) pr = gl_mul(pr, gl_mul(num[j], den[j]));
+                chunkprod[i * nchunks + k] = pr;
+            }
+            x = gl_mul(x, w);
+        }
+        gl_t z = 1;
+        for (size_t i = 0; i < n; i++) {
+            zs_vals[(size_t)ch * n + i] = z;
+            gl_t acc = z;
+            for (unsigned k = 0; k < nchunks; k++) {
+                acc = gl_mul(acc, chunkprod[i * nchunks + k]);
+                if (k < npp) zs_vals[((size_t)nc + ch * npp + k) * n + i] = acc;
+            }
+            z = acc;
+        }
+    }
+    free(chunkprod);
+}
+
 /* compute_quotient_polys (plonk/prover.rs): the vanishing polynomial at every
  * point of the LDE coset from the leaf-order rows of the three committed
  * batches (constants||sigmas, wires, zs||partial products), alpha-reduced per
@@ -147,6 +191,37 @@ static void quotient_coeffs(const or_common_t *cp, unsigned log_n, const gl_t *c
     free(qvals);
 }
 
+/* PolynomialBatch::prove_openings (fri/oracle.rs): the initial FRI polynomial
+ * alpha^nc * (P_zeta(X) - P_zeta(zeta)) / (X - zeta) + (P_next(X) - P_next(g zeta)) / (X - g zeta),
+ * P_zeta = the alpha-reduced polys of the 4 oracles in order, P_next = the
+ * first nc polys of oracle 2 (the Z polys); fin gets n coefficients */
+static void fri_initial(const gl_t *const coeffs[4], const unsigned npolys[4], unsigned nc, size_t n, glx_t alpha,
+                        glx_t zeta, glx_t zeta_next, glx_t *fin) {
+    /* zeta batch: all polys of the 4 oracles in order; Horner over the reversed list */
+    glx_t *comp = calloc(n, sizeof(glx_t));
+    for (int o = 3; o >= 0; o--)
+        for (unsigned pi = npolys[o]; pi-- > 0;) {
+            const gl_t *cf = coeffs[o] + (size_t)pi * n;
+            for (size_t k = 0; k < n; k++) comp[k] = glx_add(glx_mul(comp[k], alpha), glx_from(cf[k]));
+        }
+    /* divide_by_linear(zeta) */
+    glx_t *q1 = calloc(n, sizeof(glx_t));
+    glx_t acc = glx(0, 0);
+    for (size_t k = n; k-- > 1;) { acc = glx_add(glx_mul(acc, zeta), comp[k]); q1[k - 1] = acc; }
+    /* next batch: Z polys */
+    glx_t *comp2 = calloc(n, sizeof(glx_t));
+    for (unsigned pi = nc; pi-- > 0;) {
+        const gl_t *cf = coeffs[2] + (size_t)pi * n;
+        for (size_t k = 0; k < n; k++) comp2[k] = glx_add(glx_mul(comp2[k], alpha), glx_from(cf[k]));
+    }
+    glx_t *q2 = calloc(n, sizeof(glx_t));
+    acc = glx(0, 0);
+    for (size_t k = n; k-- > 1;) { acc = glx_add(glx_mul(acc, zeta_next), comp2[k]); q2[k - 1] = acc; }
+    glx_t ap = glx_pow(alpha, nc);
+    for (size_t k = 0; k < n; k++) fin[k] = glx_add(glx_mul(q1[k], ap), q2[k]);
+    free(comp); free(comp2); free(q1); free(q2);
+}
+
 int or_prove(const uint8_t *common_bytes, size_t clen, const gl_t *consts_sigmas, const gl_t *wires,
              const gl_t *pis, size_t npis, uint8_t *proof_out, size_t out_cap, size_t *out_len,
              gl_t *cs_cap_out, gl_t *digest_out) {
@@ -201,41 +276,7 @@ int or_prove(const uint8_t *common_bytes, size_t clen, const gl_t *consts_sigmas
 
     /* 2. partial products and Z (plonk/prover.rs wires_permutation_partial_products_and_zs) */
     gl_t *zs_vals = calloc((size_t)nzs * n, sizeof(gl_t)); /* [Z_0..Z_nc-1, pp_0[0..npp], pp_1..] */
-    {
-        const gl_t w = gl_root_of_unity(log_n);
-        const gl_t *sig = consts_sigmas + (size_t)NCONST * n;
-        unsigned nchunks = (R + qdf - 1) / qdf;
-        gl_t *chunkprod = malloc((size_t)n * nchunks * sizeof(gl_t));
-        for (unsigned ch = 0; ch < nc; ch++) {
-            gl_t x = 1;
-            for (size_t i = 0; i < n; i++) {
-                gl_t den[256], num[256];
-                for (unsigned j = 0; j < R; j++) {
-                    gl_t wv = wires[(size_t)j * n + i];
-                    num[j] = gl_add(gl_add(wv, gl_mul(betas[ch], gl_mul(c.k_is[j], x))), gammas[ch]);
-                    den[j] = gl_add(gl_add(wv, gl_mul(betas[ch], sig[(size_t)j * n + i])), gammas[ch]);
-                }
-                batch_inv(den, R);
-                for (unsigned k = 0; k < nchunks; k++) {
-                    gl_t pr = 1;
-                    for (unsigned j = k * qdf; j < (k + 1) * qdf && j < R; j++) pr = gl_mul(pr, gl_mul(num[j], den[j]));
-                    chunkprod[i * nchunks + k] = pr;
-                }
-                x = gl_mul(x, w);
-            }
-            gl_t z = 1;
-            for (size_t i = 0; i < n; i++) {
-                zs_vals[(size_t)ch * n + i] = z;
-                gl_t acc = z;
-                for (unsigned k = 0; k < nchunks; k++) {
-                    acc = gl_mul(acc, chunkprod[i * nchunks + k]);
-                    if (k < npp) zs_vals[((size_t)nc + ch * npp + k) * n + i] = acc;
-                }
-                z = acc;
-            }
-        }
-        free(chunkprod);
-    }
+    zs_values(&c, log_n, consts_sigmas, wires, betas, gammas, zs_vals);
     batch_from_values(&bz, zs_vals, nzs, log_n, rb, cap_h);
     free(zs_vals);
     or_merkle_cap(bz.tree, p->zs_cap);
@@ -272,30 +313,9 @@ int or_prove(const uint8_t *common_bytes, size_t clen, const gl_t *consts_sigmas
     glx_t alpha = or_chal_get_ext(&t);
     glx_t *fin = calloc(N, sizeof(glx_t)); /* final poly coefficients, zero-padded to N */
     {
-        /* zeta batch: all polys of the 4 oracles in order; Horner over the reversed list */
-        glx_t *comp = calloc(n, sizeof(glx_t));
-        const batch_t *bs[4] = {&bcs, &bw, &bz, &bq};
-        for (int o = 3; o >= 0; o--)
-            for (unsigned pi = bs[o]->npolys; pi-- > 0;) {
-                const gl_t *cf = bs[o]->coeffs + (size_t)pi * n;
-                for (size_t k = 0; k < n; k++) comp[k] = glx_add(glx_mul(comp[k], alpha), glx_from(cf[k]));
-            }
-        /* divide_by_linear(zeta) */
-        glx_t *q1 = calloc(n, sizeof(glx_t));
-        glx_t acc = glx(0, 0);
-        for (size_t k = n; k-- > 1;) { acc = glx_add(glx_mul(acc, zeta), comp[k]); q1[k - 1] = acc; }
-        /* next batch: Z polys */
-        glx_t *comp2 = calloc(n, sizeof(glx_t));
-        for (unsigned pi = nc; pi-- > 0;) {
-            const gl_t *cf = bz.coeffs + (size_t)pi * n;
-            for (size_t k = 0; k < n; k++) comp2[k] = glx_add(glx_mul(comp2[k], alpha), glx_from(cf[k]));
-        }
-        glx_t *q2 = calloc(n, sizeof(glx_t));
-        acc = glx(0, 0);
-        for (size_t k = n; k-- > 1;) { acc = glx_add(glx_mul(acc, zeta_next), comp2[k]); q2[k - 1] = acc; }
-        glx_t ap = glx_pow(alpha, nc);
-        for (size_t k = 0; k < n; k++) fin[k] = glx_add(glx_mul(q1[k], ap), q2[k]);
-        free(comp); free(comp2); free(q1); free(q2);
+        const gl_t *coeffs[4] = {bcs.coeffs, bw.coeffs, bz.coeffs, bq.coeffs};
+        const unsigned npolys[4] = {bcs.npolys, bw.npolys, bz.npolys, bq.npolys};
+        fri_initial(coeffs, npolys, nc, n, alpha, zeta, zeta_next, fin);
     }
     glx_t *vals = malloc(N * sizeof(glx_t));
     memcpy(vals, fin, N * sizeof(glx_t));
@@ -536,4 +556,38 @@ int ora_quotient_desc(const ora_gate_desc_t *g, unsigned log_n, unsigned rate_bi
     batch_free(&bcs); batch_free(&bw); batch_free(&bz);
     free(c);
     return 0;
+}
+
+/* checker hooks for a seam-composed prove (tests/seam_prover.py): the host
+ * steps plonky2 keeps when the GPU seams take the rest */
+int ora_zs_values(const uint8_t *common_bytes, size_t clen, const gl_t *consts_sigmas, const gl_t *wires,
+                  const gl_t *betas, const gl_t *gammas, gl_t *zs_out) {
+    or_common_t c;
+    size_t used;
+    if (or_parse_common(common_bytes, clen, &used, &c) || used != clen) return -1;
+    zs_values(&c, (unsigned)c.degree_bits, consts_sigmas, wires, betas, gammas, zs_out);
+    return 0;
+}
+
+/* out[p] = coeffs[p](x) in the extension (ext x as [2]) */
+void ora_eval_ext(const gl_t *coeffs, unsigned npolys, unsigned log_n, const gl_t *x, gl_t *out) {
+    const size_t n = (size_t)1 << log_n;
+    for (unsigned p = 0; p < npolys; p++) {
+        glx_t v = eval_coeffs_ext(coeffs + (size_t)p * n, n, glx(x[0], x[1]));
+        out[2 * p] = v.c0; out[2 * p + 1] = v.c1;
+    }
+}
+
+/* initial FRI polynomial from the 4 oracles' coefficient matrices: fin_out [n][2] */
+void ora_fri_initial(const gl_t *cs, unsigned ncs, const gl_t *w, unsigned nw, const gl_t *z, unsigned nz,
+                     const gl_t *q, unsigned nq, unsigned nc, unsigned log_n, const gl_t *alpha, const gl_t *zeta,
+                     const gl_t *zeta_next, gl_t *fin_out) {
+    const size_t n = (size_t)1 << log_n;
+    const gl_t *coeffs[4] = {cs, w, z, q};
+    const unsigned np[4] = {ncs, nw, nz, nq};
+    glx_t *fin = calloc(n, sizeof(glx_t));
+    fri_initial(coeffs, np, nc, n, glx(alpha[0], alpha[1]), glx(zeta[0], zeta[1]), glx(zeta_next[0], zeta_next[1]),
+                fin);
+    for (size_t k = 0; k < n; k++) { fin_out[2 * k] = fin[k].c0; fin_out[2 * k + 1] = fin[k].c1; }
+    free(fin);
 }
