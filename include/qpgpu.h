@@ -292,7 +292,8 @@ int qp_fri_fold(qp_ctx *ctx, const uint64_t *coeffs, uint32_t log_coeffs, uint32
  * duplex intermediate states (sponge_state with the pending input_buffer
  * written into lanes 0..pos-1), pos[b] = input_buffer.len() < 8.  Returns the
  * MINIMAL witness w with leading_zeros(permute(state with lane pos = w)[7])
- * >= pow_bits (the reference's rayon find_any returns any such w).         */
+ * >= pow_bits, 1 <= pow_bits <= 32 (the reference's rayon find_any returns any
+ * such w).                                                                 */
 int qp_pow_grind(qp_ctx *ctx, const uint64_t *states, const uint32_t *pos, uint32_t n, uint32_t pow_bits,
                  uint64_t *witness_out);
 

@@ -28,6 +28,11 @@
 #include "witness_kernels.h"
 
 // PoW search window per launch (candidates per still-searching proof), log2
+// QP_POW_SCAN 1: one k_pow_scan launch per PoW stage; 0: the windowed k_pow
+// loop with a host check per window (A/B)
+#ifndef QP_POW_SCAN
+#define QP_POW_SCAN 1
+#endif
 #ifndef QP_POW_WINDOW_LOG
 #define QP_POW_WINDOW_LOG 13
 #endif
@@ -97,7 +102,8 @@ struct qp_prover {
   Tree cs;
   DevBuf sigmas, kis;
   Tree wires, zs, quot;
-  DevBuf chal, apow, prods, qvals, cbuf, openings, comp, fin, pow_state, pow_found, pow_pos, pow_active, qidx, qout, qtab;
+  DevBuf chal, apow, prods, qvals, cbuf, openings, comp, fin, pow_state, pow_found, pow_pos, pow_active, pow_next, qidx,
+      qout, qtab;
   std::vector<DevBuf> fvals, fdig, fcoef;
   size_t qout_words = 0;
   std::unique_ptr<qh::ThreadPool> pool;
@@ -323,6 +329,7 @@ int setup(qp_prover *P) {
   TRY(P->pow_found.alloc(B));
   TRY(P->pow_pos.alloc((B + 1) / 2));
   TRY(P->pow_active.alloc((B + 1) / 2));
+  TRY(P->pow_next.alloc(B));
   {
     std::vector<uint64_t> tab = qpk::quotient_point_tables(P->log_n, P->rate_bits);
     TRY(P->qtab.alloc(tab.size()));
@@ -713,6 +720,23 @@ int prove_batch(qp_prover *P, const uint64_t *d_wires, const uint64_t *const *wi
   TRY(hipMemcpyAsync(P->pow_pos.p, P->h_pos.data(), (size_t)nb * 4, hipMemcpyHostToDevice, s));
   TRY(hipMemsetAsync(P->pow_found.p, 0xFF, (size_t)nb * 8, s));
   {
+#if QP_POW_SCAN
+    // Minimal witness per proof in one launch (k_pow_scan): 2048 workgroups
+    // claim 256-candidate blocks from per-proof counters, moving on to the
+    // next proof once theirs has a hit below the claimed block
+    const uint64_t limit = 1ull << std::min<uint32_t>(P->pow_bits + 20, 62);
+    TRY(hipMemsetAsync(P->pow_next.p, 0, (size_t)nb * 8, s));
+    qpk::k_pow_scan<<<2048, 256, 0, s>>>(P->pow_state.p, (const uint32_t *)P->pow_pos.p, P->pow_found.p,
+                                         P->pow_next.p, nb, P->pow_bits, limit);
+    TRY(hipGetLastError());
+    TRY(hipMemcpyAsync(P->h_found.data(), P->pow_found.p, (size_t)nb * 8, hipMemcpyDeviceToHost, s));
+    TRY(hipStreamSynchronize(s));
+    for (uint32_t b = 0; b < nb; b++)
+      if (P->h_found[b] == ~0ull) {
+        c->err = "proof of work not found";
+        return QP_ERR_STATE;
+      }
+#else
     // Minimal witness per proof: every proof still searching scans the same
     // candidate window [base, base + W) per launch; only those proofs are
     // launched (compacted list), so a proof stops costing work as soon as its
@@ -743,6 +767,7 @@ int prove_batch(qp_prover *P, const uint64_t *d_wires, const uint64_t *const *wi
         return QP_ERR_STATE;
       }
     }
+#endif
   }
   P->pool->parallel_for(nb, [&](size_t b) {
     ProofState &S = st[b];

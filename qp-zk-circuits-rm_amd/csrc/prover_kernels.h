@@ -80,6 +80,8 @@ __global__ void k_fri_leaf(const uint64_t *vals, uint64_t *dig, uint32_t log_len
                            uint64_t d_bstride);
 __global__ void k_fold(const uint64_t *cin, uint64_t *cout, uint32_t log_len, uint32_t ab, uint32_t layer,
                        const uint64_t *chal, uint64_t i_bstride, uint64_t o_bstride, uint32_t log_nz);
+__global__ void k_pow_scan(const uint64_t *states, const uint32_t *pos, uint64_t *found, uint64_t *next, uint32_t nb,
+                           uint32_t bits, uint64_t limit);
 __global__ void k_pow(const uint64_t *states, const uint32_t *pos, const uint32_t *active, uint64_t *found, uint64_t base,
                       uint32_t bits);
 __global__ void k_gather_rows_b(const uint64_t *cols, uint64_t stride, uint64_t bstride, uint32_t ncols,

@@ -175,6 +175,7 @@ __device__ __forceinline__ void poseidon_gate(const uint64_t *__restrict__ wl, u
 
 template <class RD>
 __device__ __forceinline__ void poseidon_gate_rd(const RD &WR, TermAcc &A) {
+#undef WV
 #define WV(j) WR(j)
   const uint64_t swap = WV(24);
   A.emit(gfn::mul(swap, gfn::sub(swap, 1)));
@@ -944,6 +945,52 @@ __global__ void __launch_bounds__(256) k_fold(const uint64_t *__restrict__ cin, 
 }
 
 // ---------------------------------------------------------------- a12
+
+// Minimal witness, one launch for all proofs.  Candidates of proof b are
+// claimed in blocks of 256 from a per-proof counter (next[b], increasing), so
+// every block below the best hit is claimed while that hit is still unknown
+// and gets tested: the final found[b] is the minimal witness.  A workgroup
+// keeps claiming blocks of one proof until the claimed block starts at or
+// above found[b] (or at limit), then moves to the next proof, so the stragglers
+// of the geometric search get every workgroup of the grid.  limit bounds every
+// loop (16 PoW bits: no hit below 2^36 has probability exp(-2^20)).
+__device__ __forceinline__ bool pow_hit(const uint64_t *__restrict__ pre, uint32_t pos, uint64_t cand, uint32_t bits) {
+  const uint64_t y = pf::sbox(pf::add_c(cand, ps::RC_DEV[pos]));
+  const uint32_t y0 = pf::lo32(y), y1 = pf::hi32(y);
+  uint64_t s[12];
+#pragma unroll
+  for (int r = 0; r < 12; r++) {
+    const uint32_t c = (uint32_t)pre[12 + r];
+    s[r] = pf::reduce_row((uint64_t)y0 * c + (pre[r] & pf::EPS), (uint64_t)y1 * c + (pre[r] >> 32));
+  }
+  pf::rounds<QP_POSEIDON_MODE, 1>(s);
+  return (psd::canon(s[7]) >> (64 - bits)) == 0;
+}
+
+__global__ void __launch_bounds__(256) k_pow_scan(const uint64_t *__restrict__ states, const uint32_t *__restrict__ pos,
+                                                  uint64_t *__restrict__ found, uint64_t *__restrict__ next, uint32_t nb,
+                                                  uint32_t bits, uint64_t limit) {
+  __shared__ uint64_t blk;
+  __shared__ uint32_t done;
+  for (uint32_t i = 0; i < nb; i++) {
+    const uint32_t b = (blockIdx.x + i) % nb;
+    const uint64_t *pre = states + b * 24;
+    for (;;) {
+      if (threadIdx.x == 0) {
+        const uint64_t k = atomicAdd((unsigned long long *)(next + b), 1ull);
+        blk = k;
+        done = k * 256 >= limit || k * 256 >= *(const volatile uint64_t *)(found + b);
+      }
+      __syncthreads();
+      const uint64_t k = blk;
+      const uint32_t d = done;
+      __syncthreads();  // every lane has read blk / done before lane 0 rewrites them
+      if (d) break;
+      const uint64_t cand = k * 256 + threadIdx.x;
+      if (pow_hit(pre, pos[b], cand, bits)) atomicMin((unsigned long long *)(found + b), (unsigned long long)cand);
+    }
+  }
+}
 
 __global__ void __launch_bounds__(256) k_pow(const uint64_t *__restrict__ states, const uint32_t *__restrict__ pos,
                                              const uint32_t *__restrict__ active, uint64_t *__restrict__ found,

@@ -365,7 +365,7 @@ int qp_fri_fold(qp_ctx *ctx, const uint64_t *coeffs, uint32_t log_coeffs, uint32
 
 int qp_pow_grind(qp_ctx *ctx, const uint64_t *states, const uint32_t *pos, uint32_t n, uint32_t pow_bits,
                  uint64_t *witness_out) {
-  if (!ctx || !states || !pos || !witness_out || !n || pow_bits == 0 || pow_bits > 40) return QP_ERR_ARG;
+  if (!ctx || !states || !pos || !witness_out || !n || pow_bits == 0 || pow_bits > 32) return QP_ERR_ARG;
   for (uint32_t b = 0; b < n; b++)
     if (pos[b] >= 8) {  // Challenger invariant: input_buffer.len() < RATE when the witness is observed
       ctx->err = "qp_pow_grind: witness position must be < 8";
@@ -380,42 +380,26 @@ int qp_pow_grind(qp_ctx *ctx, const uint64_t *states, const uint32_t *pos, uint3
       for (int i = 0; i < 12; i++) st[i] = gl::canon(states[(size_t)b * 12 + i]);
       qpk::pow_prestate(st, pos[b], pre.data() + (size_t)b * 24);
     }
-    DMem d_pre, d_pos, d_act, d_found;
+    DMem d_pre, d_pos, d_next, d_found;
     QP_HIP_TRY(ctx, d_pre.alloc(pre.size()));
     QP_HIP_TRY(ctx, d_pos.alloc((n + 1) / 2));
-    QP_HIP_TRY(ctx, d_act.alloc((n + 1) / 2));
+    QP_HIP_TRY(ctx, d_next.alloc(n));
     QP_HIP_TRY(ctx, d_found.alloc(n));
     QP_HIP_TRY(ctx, hipMemcpyAsync(d_pre.p, pre.data(), pre.size() * 8, hipMemcpyHostToDevice, s));
     QP_HIP_TRY(ctx, hipMemcpyAsync(d_pos.p, pos, n * 4ull, hipMemcpyHostToDevice, s));
     QP_HIP_TRY(ctx, hipMemsetAsync(d_found.p, 0xFF, n * 8ull, s));
-    // every state still searching scans the same candidate window per launch
-    // (the prover's PoW loop, prover.cpp stage 6): the minimal witness is the
-    // first hit of the first window that holds one
-    std::vector<uint32_t> active(n);
-    for (uint32_t b = 0; b < n; b++) active[b] = b;
-    uint64_t base = 0;
-    const uint64_t limit = 1ull << std::min<uint32_t>(pow_bits + 24, 62);
-    while (!active.empty()) {
-      const uint32_t na = (uint32_t)active.size();
-      uint64_t window = 1ull << 13;
-      while ((uint64_t)na * window < (1ull << 21)) window <<= 1;
-      QP_HIP_TRY(ctx, hipMemcpyAsync(d_act.p, active.data(), na * 4ull, hipMemcpyHostToDevice, s));
-      qpk::k_pow<<<dim3((uint32_t)(window / 256), na), 256, 0, s>>>(d_pre.p, (const uint32_t *)d_pos.p,
-                                                                     (const uint32_t *)d_act.p, d_found.p, base,
-                                                                     pow_bits);
-      QP_HIP_TRY(ctx, hipGetLastError());
-      QP_HIP_TRY(ctx, hipMemcpyAsync(found.data(), d_found.p, n * 8ull, hipMemcpyDeviceToHost, s));
-      QP_HIP_TRY(ctx, hipStreamSynchronize(s));
-      std::vector<uint32_t> still;
-      for (uint32_t b : active)
-        if (found[b] == ~0ull) still.push_back(b);
-      active.swap(still);
-      base += window;
-      if (base > limit && !active.empty()) {
+    QP_HIP_TRY(ctx, hipMemsetAsync(d_next.p, 0, n * 8ull, s));
+    // the prover's single-launch minimal-witness search (prover.cpp stage 6)
+    const uint64_t limit = 1ull << std::min<uint32_t>(pow_bits + 20, 62);
+    qpk::k_pow_scan<<<2048, 256, 0, s>>>(d_pre.p, (const uint32_t *)d_pos.p, d_found.p, d_next.p, n, pow_bits, limit);
+    QP_HIP_TRY(ctx, hipGetLastError());
+    QP_HIP_TRY(ctx, hipMemcpyAsync(found.data(), d_found.p, n * 8ull, hipMemcpyDeviceToHost, s));
+    QP_HIP_TRY(ctx, hipStreamSynchronize(s));
+    for (uint32_t b = 0; b < n; b++)
+      if (found[b] == ~0ull) {
         ctx->err = "qp_pow_grind: no witness below the search limit";
         return QP_ERR_STATE;
       }
-    }
     memcpy(witness_out, found.data(), n * 8ull);
   } catch (const std::bad_alloc &) {
     return QP_ERR_OOM;
