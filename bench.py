@@ -34,6 +34,13 @@ sys.path.insert(0, os.path.join(ROOT, "qp-zk-circuits-rm_amd"))
 sys.path.insert(0, os.path.join(ROOT, "tests"))
 
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec peak (MI355X_MICROARCH.md)
+# VALU issue ceiling of the dominant (Poseidon) kernels: 1024 SIMDs x 2.4 GHz /
+# 2.56 cycles per VOP3 wave-instruction at 8 waves/SIMD (profiles/r02_isa_rates.log,
+# tools/gen_isa_rates.py); one permutation = 18,708 VALU instructions (static ISA
+# count of poseidon_fast.h mode 3, equal to the PMC SQ_INSTS_VALU per wave of the
+# one-permutation-per-lane Merkle kernel)
+VALU_PEAK_WAVE_INSTR_S = 1024 * 2.4e9 / 2.56
+PERM_VALU_INSTR = 18708
 # HBM traffic of the roofline kernel from rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE
 # passes (tools/pmc_summary.py applies the gfx950 corrections); per proof, scaled
 # to the bench's per-launch proof count
@@ -334,6 +341,14 @@ def main():
                                             "quotient_avg_launch_ms": qk["ms"] / max(qk["launches"], 1),
                                             "proofs_per_launch": per[0],
                                             "note": "isolated pass, as roofline.achieved; HBM bytes: PMC file"})
+        vk = rec["valu_kernels"]
+        if vk.get("leaf_hash_wires_perms_per_s"):
+            ach = vk["leaf_hash_wires_perms_per_s"] / 64 * PERM_VALU_INSTR
+            rec["dominant_kernel"] = {
+                "kernel": "k_leaf_hash (Poseidon Merkle leaves, ~59 % of GPU time)", "bound": "valu",
+                "achieved": ach, "peak": VALU_PEAK_WAVE_INSTR_S, "unit": "wave-instructions/s",
+                "frac": ach / VALU_PEAK_WAVE_INSTR_S, "instr_per_perm": PERM_VALU_INSTR,
+                "note": "issue-bound 64-bit integer work (no MFMA path); peak from the measured VOP3 issue cost"}
         rec["stage_ms_per_step"]["note"] = f"prover 0 ({per[0]} proofs), host + device"
         if world == 1 and args.cpu_sample > 0:
             rec["cpu_baseline"] = cpu_baseline(circuit, wires, pis, args.cpu_sample, args.cpu_seconds)
