@@ -44,7 +44,7 @@ PERM_VALU_INSTR = 18708
 # HBM traffic of the roofline kernel from rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE
 # passes (tools/pmc_summary.py applies the gfx950 corrections); per proof, scaled
 # to the bench's per-launch proof count
-PMC_FILE = os.path.join(ROOT, "profiles", "r02_v6_pmc_hbm_b128.json")
+PMC_FILE = os.path.join(ROOT, "profiles", "r02_final_pmc_hbm_b128.json")
 
 
 def pmc_traffic(kernel, ncols, log_n, proofs, lanes_per_proof=None):
@@ -302,7 +302,7 @@ def main():
                                                 per[0]) if circuit.degree_bits == 13 else None,
                          "traffic_unit": "bytes per launch",
                          "algorithmic_bytes_per_launch": lde["units"] / max(lde["launches"], 1),
-                         "traffic_source": "profiles/r02_v6_pmc_hbm_b128.json (rocprofv3 --pmc FETCH_SIZE, WRITE_SIZE "
+                         "traffic_source": "profiles/r02_final_pmc_hbm_b128.json (rocprofv3 --pmc FETCH_SIZE, WRITE_SIZE "
                                            "passes of this bench at batch 128), per proof x proofs per launch",
                          "avg_launch_ms": lde["ms"] / max(lde["launches"], 1),
                          "note": "HIP events on the prover stream around each launch of the kernel"},
