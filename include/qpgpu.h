@@ -274,7 +274,8 @@ int qp_quotient(qp_ctx *ctx, const qp_batch *cs, const qp_batch *wires, const qp
  * them full length with a zero tail, so log_coeffs may equal log_values: only
  * the nonzero prefix (at most 2^13 coefficients) is transformed.  The caller
  * observes the cap, draws beta and calls qp_fri_fold; out (optional) keeps the
- * layer for qp_fri_layer_open in the query rounds.                          */
+ * layer for qp_fri_layer_open in the query rounds.  A layer uses its context's
+ * stream: free it (qp_fri_layer_free) before qp_ctx_destroy.                */
 typedef struct qp_fri_layer qp_fri_layer;
 int qp_fri_layer_commit(qp_ctx *ctx, const uint64_t *coeffs, uint32_t log_coeffs, uint32_t log_values, uint64_t shift,
                         uint32_t arity_bits, uint32_t cap_height, uint64_t *cap_out, qp_fri_layer **out);
