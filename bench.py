@@ -71,7 +71,7 @@ def parse():
     ap.add_argument("--warmup", type=int, default=1)
     ap.add_argument("--batch", type=int, default=0,
                     help="proofs per GPU per step (default: 256 Wormhole, 1024 voting)")
-    ap.add_argument("--provers", type=int, default=2,
+    ap.add_argument("--provers", type=int, default=3,
                     help="concurrent provers per GPU (own HIP stream + host thread each, B/provers proofs each): "
                          "one prover's host transcript phases overlap the other's kernels")
     ap.add_argument("--circuit", choices=["wormhole", "voting"], default="wormhole",
