@@ -101,20 +101,28 @@ int qp_quotient(qp_ctx *ctx, const qp_batch *cs, const qp_batch *wires, const qp
       nterms > qpk::APOW_STRIDE || wires->log_n != log_n || zs_pp->log_n != log_n || wires->rate_bits != rb ||
       zs_pp->rate_bits != rb || cs->nbat != 1 || wires->nbat != 1 || zs_pp->nbat != 1 ||
       cs->npolys != g->num_constants + R || wires->npolys != g->num_wires || zs_pp->npolys != nc * nchunks ||
-      wires->nsalt || zs_pp->nsalt || cs->nsalt || R > g->num_wires) {
-    ctx->err = "qp_quotient: unsupported shape (2 challenges, qdf = 2^rate_bits, unsalted batches of one)";
+      wires->nsalt || zs_pp->nsalt || cs->nsalt || R > g->num_wires || rb > 4 ||
+      g->num_constants < g->num_selectors) {
+    ctx->err = "qp_quotient: unsupported shape (2 challenges, qdf = 2^rate_bits <= 16, unsalted batches of one)";
     return QP_ERR_ARG;
   }
   // per-gate checks: known kind, selector in range, parameters inside the
   // kernels' bounds, every wire a gate reads < num_wires, every gate constant
   // < num_constants - num_selectors, constraint count <= num_gate_constraints
   const uint32_t W = g->num_wires, n_gc = g->num_constants - g->num_selectors;
+  for (uint32_t s = 0; s < g->num_selectors; s++)
+    if (g->group_lo[s] > g->group_hi[s] || g->group_hi[s] > g->num_gates) {
+      ctx->err = "qp_quotient: selector group " + std::to_string(s) + " out of range";
+      return QP_ERR_ARG;
+    }
   bool fast = g->num_gates <= 8 && !getenv_flag_eq("QPGPU_QUOTIENT", "generic");
   uint32_t seen = 0;
   for (uint32_t i = 0; i < g->num_gates; i++) {
     const uint32_t k = g->kind[i], p = g->param[i], p2 = g->param2[i], p3 = g->param3[i];
     uint64_t wires_used = 0, consts_used = 0, ncons = 0;
-    bool ok = g->selector_index[i] < g->num_selectors;
+    // plonky2 places each gate in the selector group it belongs to
+    bool ok = g->selector_index[i] < g->num_selectors && g->group_lo[g->selector_index[i]] <= i &&
+              i < g->group_hi[g->selector_index[i]];
     switch (k) {
       case QP_GATE_NOOP: break;
       case QP_GATE_CONSTANT: wires_used = p; consts_used = p; ncons = p; break;
@@ -151,8 +159,9 @@ int qp_quotient(qp_ctx *ctx, const qp_batch *cs, const qp_batch *wires, const qp
       ctx->err = "qp_quotient: gate " + std::to_string(i) + ": unknown gate kind, selector or parameters";
       return QP_ERR_ARG;
     }
-    // the single-read kernel: the six leaf-circuit kinds, each at most once
-    if (k > QP_GATE_POSEIDON || (seen >> k) & 1) fast = false;
+    // the single-read kernel: the six leaf-circuit kinds, each at most once, the
+    // non-Poseidon ones inside the routed wires it sweeps
+    if (k > QP_GATE_POSEIDON || (seen >> k) & 1 || (k != QP_GATE_POSEIDON && wires_used > R)) fast = false;
     seen |= 1u << k;
   }
   const uint64_t n = 1ull << log_n, N = 1ull << logN;
