@@ -102,9 +102,8 @@ static void batch_build(qp_batch *b) {
   const uint32_t logN = b->log_n + b->rate_bits;
   qpk::lde(c->tw, b->d_coeffs, n, b->d_lde, N, b->npolys, b->log_n, b->rate_bits, gl::GEN, b->nbat,
            (uint64_t)b->npolys * n, (uint64_t)b->npolys * N, c->stream);
-  qpk::leaf_hash(b->d_lde, N, b->npolys, b->d_salt, b->nsalt, b->d_dig, (uint32_t)N, b->nbat,
-                 (uint64_t)b->npolys * N, N * b->nsalt, b->ndig() * 4, c->stream);
-  qpk::merkle_tree(b->d_dig, logN, b->cap_h, b->nbat, b->ndig() * 4, c->stream);
+  qpk::leaf_hash_tree(b->d_lde, N, b->npolys, b->d_salt, b->nsalt, b->d_dig, logN, b->cap_h, b->nbat,
+                      (uint64_t)b->npolys * N, N * b->nsalt, b->ndig() * 4, c->stream);
 }
 
 static uint64_t *cap_ptr(qp_batch *b, uint32_t bi) {

@@ -52,6 +52,17 @@ void leaf_hash(const uint64_t *cols, uint64_t stride, uint32_t ncols, const uint
 // parent levels down to the cap (two_to_one), appended after the N leaf digests
 void merkle_tree(uint64_t *digests, uint32_t log_N, uint32_t cap_h, uint32_t nbat, uint64_t d_bstride,
                  hipStream_t s);
+// leaf digests and, when the tree has a level below the cap, its first level
+// in the same kernel; returns the first level merkle_tree_from still builds
+uint32_t leaf_hash_first(const uint64_t *cols, uint64_t stride, uint32_t ncols, const uint64_t *salt, uint32_t nsalt,
+                         uint64_t *digests, uint32_t log_N, uint32_t cap_h, uint32_t nbat, uint64_t c_bstride,
+                         uint64_t s_bstride, uint64_t d_bstride, hipStream_t s);
+void merkle_tree_from(uint64_t *digests, uint32_t log_N, uint32_t cap_h, uint32_t nbat, uint64_t d_bstride,
+                      uint32_t first_level, hipStream_t s);
+// leaf digests + the whole tree (first level fused into the leaf kernel)
+void leaf_hash_tree(const uint64_t *cols, uint64_t stride, uint32_t ncols, const uint64_t *salt, uint32_t nsalt,
+                    uint64_t *digests, uint32_t log_N, uint32_t cap_h, uint32_t nbat, uint64_t c_bstride,
+                    uint64_t s_bstride, uint64_t d_bstride, hipStream_t s);
 
 inline uint64_t tree_digest_count(uint32_t log_N, uint32_t cap_h) {
   uint64_t n = 0;

@@ -11,23 +11,27 @@
 
 // trees narrower than 2^QP_MERKLE_FUSE_LOG nodes per level finish in one
 // launch (one wave per block at 6, so no wave idles at the level barriers)
+// QP_LEAF_PAIRS 1: leaf digests and the first tree level in one kernel
+// (k_leaf_hash2); 0 (default): leaf kernel + a level launch.  Measured
+// (python bench.py --steps 10, two runs each, one box): fused 919.8 / 924.9 vs
+// 930.0 / 933.0 proofs/s — three inlined permutations in one kernel cost more
+// than the level launch they save (profiles/r02_ab_leaf_pairs.log)
+#ifndef QP_LEAF_PAIRS
+#define QP_LEAF_PAIRS 0
+#endif
 #ifndef QP_MERKLE_FUSE_LOG
 #define QP_MERKLE_FUSE_LOG 6
 #endif
 
 namespace qpk {
 
-__global__ void __launch_bounds__(256) k_leaf_hash(const uint64_t *__restrict__ cols, uint64_t stride, uint32_t ncols,
-                                                   const uint64_t *__restrict__ salt, uint32_t nsalt,
-                                                   uint64_t *__restrict__ dig, uint32_t N, uint64_t c_bstride,
-                                                   uint64_t s_bstride, uint64_t d_bstride) {
-  const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
-  if (i >= N) return;
-  cols += blockIdx.y * c_bstride;
-  if (salt) salt += blockIdx.y * s_bstride;
-  dig += blockIdx.y * d_bstride;
+// leaf digest of row i: hash_or_noop over the ncols column values (+ salt)
+__device__ __forceinline__ void leaf_digest(const uint64_t *__restrict__ cols, uint64_t stride, uint32_t ncols,
+                                            const uint64_t *__restrict__ salt, uint32_t nsalt, uint32_t i,
+                                            uint64_t s[12]) {
   const uint32_t W = ncols + nsalt;
-  uint64_t s[12] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0};
+#pragma unroll
+  for (int k = 0; k < 12; k++) s[k] = 0;
   if (W <= 4) {
     for (uint32_t c = 0; c < W; c++) s[c] = c < ncols ? cols[(uint64_t)c * stride + i] : salt[(uint64_t)i * nsalt + c - ncols];
   } else {
@@ -41,8 +45,60 @@ __global__ void __launch_bounds__(256) k_leaf_hash(const uint64_t *__restrict__ 
       psd::permute_nc(s);
     }
   }
+#pragma unroll
+  for (int k = 0; k < 4; k++) s[k] = psd::canon(s[k]);
+}
+
+__global__ void __launch_bounds__(256) k_leaf_hash(const uint64_t *__restrict__ cols, uint64_t stride, uint32_t ncols,
+                                                   const uint64_t *__restrict__ salt, uint32_t nsalt,
+                                                   uint64_t *__restrict__ dig, uint32_t N, uint64_t c_bstride,
+                                                   uint64_t s_bstride, uint64_t d_bstride) {
+  const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= N) return;
+  cols += blockIdx.y * c_bstride;
+  if (salt) salt += blockIdx.y * s_bstride;
+  dig += blockIdx.y * d_bstride;
+  uint64_t s[12];
+  leaf_digest(cols, stride, ncols, salt, nsalt, i, s);
   uint64_t *o = dig + (uint64_t)i * 4;
-  o[0] = psd::canon(s[0]); o[1] = psd::canon(s[1]); o[2] = psd::canon(s[2]); o[3] = psd::canon(s[3]);
+  o[0] = s[0]; o[1] = s[1]; o[2] = s[2]; o[3] = s[3];
+}
+
+// leaves 2j and 2j+1 and their parent in one lane: the first tree level runs
+// at the leaf kernel's occupancy instead of as its own launch (level 1 of a
+// tree sits at node offset N)
+__global__ void __launch_bounds__(256) k_leaf_hash2(const uint64_t *__restrict__ cols, uint64_t stride, uint32_t ncols,
+                                                    const uint64_t *__restrict__ salt, uint32_t nsalt,
+                                                    uint64_t *__restrict__ dig, uint32_t N, uint64_t c_bstride,
+                                                    uint64_t s_bstride, uint64_t d_bstride) {
+  const uint32_t j = blockIdx.x * blockDim.x + threadIdx.x;
+  if (2 * j >= N) return;
+  cols += blockIdx.y * c_bstride;
+  if (salt) salt += blockIdx.y * s_bstride;
+  dig += blockIdx.y * d_bstride;
+  uint64_t s[12], d0[4];
+  leaf_digest(cols, stride, ncols, salt, nsalt, 2 * j, s);
+#pragma unroll
+  for (int k = 0; k < 4; k++) d0[k] = s[k];
+  leaf_digest(cols, stride, ncols, salt, nsalt, 2 * j + 1, s);
+  uint64_t *o = dig + (uint64_t)j * 8;
+#pragma unroll
+  for (int k = 0; k < 4; k++) {
+    o[k] = d0[k];
+    o[4 + k] = s[k];
+  }
+  // two_to_one(left, right) = permute([left, right, 0, 0, 0, 0])[0..4]
+#pragma unroll
+  for (int k = 3; k >= 0; k--) {
+    s[4 + k] = s[k];
+    s[k] = d0[k];
+  }
+#pragma unroll
+  for (int k = 8; k < 12; k++) s[k] = 0;
+  psd::permute_nc(s);
+  uint64_t *p = dig + ((uint64_t)N + j) * 4;
+#pragma unroll
+  for (int k = 0; k < 4; k++) p[k] = psd::canon(s[k]);
 }
 
 // 1..9 tree levels per launch: a block takes B = min(256, count) nodes of
@@ -97,10 +153,10 @@ void leaf_hash(const uint64_t *cols, uint64_t stride, uint32_t ncols, const uint
   k_leaf_hash<<<grid, 256, 0, s>>>(cols, stride, ncols, salt, nsalt, digests, N, c_bstride, s_bstride, d_bstride);
 }
 
-void merkle_tree(uint64_t *digests, uint32_t log_N, uint32_t cap_h, uint32_t nbat, uint64_t d_bstride,
-                 hipStream_t s) {
+void merkle_tree_from(uint64_t *digests, uint32_t log_N, uint32_t cap_h, uint32_t nbat, uint64_t d_bstride,
+                      uint32_t first_level, hipStream_t s) {
   const uint32_t K = log_N - cap_h;  // levels above the leaves
-  for (uint32_t k0 = 1; k0 <= K;) {
+  for (uint32_t k0 = first_level; k0 <= K;) {
     const uint32_t lc = log_N - k0;  // log2(nodes at level k0)
     const uint32_t lb = lc < 8 ? lc : 8;
     // wide levels one launch each (a fused block would idle all but one
@@ -111,6 +167,32 @@ void merkle_tree(uint64_t *digests, uint32_t log_N, uint32_t cap_h, uint32_t nba
     k_merkle_levels<<<grid, 1u << lb, 0, s>>>(digests, log_N, k0, nl, d_bstride);
     k0 += nl;
   }
+}
+
+void merkle_tree(uint64_t *digests, uint32_t log_N, uint32_t cap_h, uint32_t nbat, uint64_t d_bstride,
+                 hipStream_t s) {
+  merkle_tree_from(digests, log_N, cap_h, nbat, d_bstride, 1, s);
+}
+
+uint32_t leaf_hash_first(const uint64_t *cols, uint64_t stride, uint32_t ncols, const uint64_t *salt, uint32_t nsalt,
+                         uint64_t *digests, uint32_t log_N, uint32_t cap_h, uint32_t nbat, uint64_t c_bstride,
+                         uint64_t s_bstride, uint64_t d_bstride, hipStream_t s) {
+  const uint32_t N = 1u << log_N;
+  if (!QP_LEAF_PAIRS || log_N <= cap_h) {
+    leaf_hash(cols, stride, ncols, salt, nsalt, digests, N, nbat, c_bstride, s_bstride, d_bstride, s);
+    return 1;
+  }
+  dim3 grid((N / 2 + 255) / 256, nbat);
+  k_leaf_hash2<<<grid, 256, 0, s>>>(cols, stride, ncols, salt, nsalt, digests, N, c_bstride, s_bstride, d_bstride);
+  return 2;
+}
+
+void leaf_hash_tree(const uint64_t *cols, uint64_t stride, uint32_t ncols, const uint64_t *salt, uint32_t nsalt,
+                    uint64_t *digests, uint32_t log_N, uint32_t cap_h, uint32_t nbat, uint64_t c_bstride,
+                    uint64_t s_bstride, uint64_t d_bstride, hipStream_t s) {
+  const uint32_t first = leaf_hash_first(cols, stride, ncols, salt, nsalt, digests, log_N, cap_h, nbat, c_bstride,
+                                         s_bstride, d_bstride, s);
+  merkle_tree_from(digests, log_N, cap_h, nbat, d_bstride, first, s);
 }
 
 __global__ void k_gather_rows(const uint64_t *__restrict__ cols, uint64_t stride, uint32_t ncols,

@@ -73,8 +73,8 @@ struct Tree {  // one Merkle-committed matrix per proof
   // coefficients in `coeffs`: LDE + leaves + tree
   void build(qp_ctx *c, uint32_t nbat) {
     qpk::lde(c->tw, coeffs.p, n(), lde.p, N(), npolys, log_n, rate_bits, gl::GEN, nbat, cbs(), lbs(), c->stream);
-    qpk::leaf_hash(lde.p, N(), npolys, nullptr, 0, dig.p, (uint32_t)N(), nbat, lbs(), 0, dbs(), c->stream);
-    qpk::merkle_tree(dig.p, log_n + rate_bits, cap_h, nbat, dbs(), c->stream);
+    qpk::leaf_hash_tree(lde.p, N(), npolys, nullptr, 0, dig.p, log_n + rate_bits, cap_h, nbat, lbs(), 0, dbs(),
+                        c->stream);
   }
   // values in `vals` ([nb][npolys][n]): ifft then build
   void build_from_values(qp_ctx *c, uint32_t nbat) {
@@ -491,11 +491,14 @@ int prove_batch(qp_prover *P, const uint64_t *d_wires, const uint64_t *const *wi
     qpk::lde(c->tw, t.coeffs.p, t.n(), t.lde.p, t.N(), t.npolys, t.log_n, t.rate_bits, gl::GEN, nb, t.cbs(), t.lbs(), s);
     kt_end(P, 0, (double)nb * t.npolys * 8.0 * (double)(t.n() + t.N()));
     kt_begin(P, 1);
-    qpk::leaf_hash(t.lde.p, t.N(), t.npolys, nullptr, 0, t.dig.p, (uint32_t)t.N(), nb, t.lbs(), 0, t.dbs(), s);
-    kt_end(P, 1, (double)nb * t.N() * ((t.npolys + 7) / 8));
+    const uint32_t first = qpk::leaf_hash_first(t.lde.p, t.N(), t.npolys, nullptr, 0, t.dig.p, t.log_n + t.rate_bits,
+                                                t.cap_h, nb, t.lbs(), 0, t.dbs(), s);
+    // permutations: the leaves' (+ the first level's when fused)
+    const double lvl1 = first == 2 ? (double)(t.N() / 2) : 0.0;
+    kt_end(P, 1, (double)nb * ((double)t.N() * ((t.npolys + 7) / 8) + lvl1));
     kt_begin(P, 2);
-    qpk::merkle_tree(t.dig.p, t.log_n + t.rate_bits, t.cap_h, nb, t.dbs(), s);
-    kt_end(P, 2, (double)nb * (t.N() - (1u << t.cap_h)));
+    qpk::merkle_tree_from(t.dig.p, t.log_n + t.rate_bits, t.cap_h, nb, t.dbs(), first, s);
+    kt_end(P, 2, (double)nb * ((double)t.N() - (1u << t.cap_h) - lvl1));
   }
   TRY(hipGetLastError());
   if ((rc = fetch_caps(P, P->wires.dig.p, P->wires.dbs(), logN, nb))) return rc;
