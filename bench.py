@@ -267,7 +267,7 @@ def main():
             zvd = zp.verifier_data()
             zok = olib().ora_verify(zvd, len(zvd), zproofs[0], len(zproofs[0])) == 0
         zk = {"proofs_per_s_1prover": per[0] / zdt, "proofs_per_launch": per[0], "proof_verified": zok,
-              "note": "standard_recursion_zk_config, e2e, one prover (the headline runs two)"}
+              "note": "standard_recursion_zk_config, e2e, one prover (the headline runs --provers, default 3)"}
         zp.free()
     if rank == 0:
         total = world * B * args.steps

@@ -5,6 +5,22 @@
 // its VALU instruction count and v_mad_u64_u32 — a 32x32+64 product-sum in one
 // issue — is the densest instruction there is.
 //
+// Hazard rule (gfx950): a VALU instruction reading a carry/mask SGPR written
+// by the previous VALU instruction needs 2 wait states (hipcc puts s_nop 1
+// between its own v_add_co/v_addc pairs).  Around inline asm hipcc adds only a
+// fixed 1-state pad, so every asm statement below that reads a carry written
+// by the preceding one opens with its own s_nop 0.
+//
+// (QP_CARRY_WAIT=0 drops it: A/B only, profiles/r02_ab_carry_wait.log.)
+#ifndef QP_CARRY_WAIT
+#define QP_CARRY_WAIT 1
+#endif
+#if QP_CARRY_WAIT
+#define QP_CWAIT "s_nop 0\n\t"
+#else
+#define QP_CWAIT ""
+#endif
+//
 // Same function as ps::permute (poseidon.h); arithmetic discipline:
 //   * state NON-canonical in [0, 2^64) (plonky2's GoldilocksField form);
 //   * MDS row r = sum_i CIRC[i] * s[(i+r)%12] (+ DIAG) computed on 32-bit
@@ -67,7 +83,7 @@ __device__ __forceinline__ uint64_t reduce_row(uint64_t al, uint64_t ah) {
   // t.hi += lo32(ah), carry c2 (worth 2^64 = eps)
   uint32_t t0 = lo32(t), t1 = hi32(t);
   asm("v_add_co_u32_e64 %0, %1, %2, %3" : "=v"(t1), "=s"(c2) : "v"(t1), "v"(lo32(ah)));
-  asm("v_cndmask_b32_e64 %0, 0, -1, %1" : "=v"(e) : "s"(c2));
+  asm(QP_CWAIT "v_cndmask_b32_e64 %0, 0, -1, %1" : "=v"(e) : "s"(c2));
   // t + e: when c2, t < 2^42 so no overflow
   const uint64_t tt = ((uint64_t)t1 << 32) | t0;
   uint64_t r;
@@ -88,17 +104,17 @@ __device__ __forceinline__ uint64_t mul(uint64_t a, uint64_t b) {
   uint64_t t, c1, c2, c3;
   uint32_t e;
   asm("v_mad_u64_u32 %0, %1, %2, -1, %3" : "=v"(t), "=s"(c1) : "v"(lo32(W)), "v"(X));
-  asm("v_cndmask_b32_e64 %0, 0, -1, %1" : "=v"(e) : "s"(c1));
+  asm(QP_CWAIT "v_cndmask_b32_e64 %0, 0, -1, %1" : "=v"(e) : "s"(c1));
   // carry: true value t + 2^64 ≡ t + eps; t < 2^64 - 2^33 then, no overflow
   asm("v_mad_u64_u32 %0, %1, %2, 1, %3" : "=v"(t), "=s"(c2) : "v"(e), "v"(t));
   // t - w3, borrow b (worth -2^64 ≡ -eps)
   uint32_t r0 = lo32(t), r1 = hi32(t);
   asm("v_sub_co_u32_e64 %0, %1, %2, %3" : "=v"(r0), "=s"(c3) : "v"(r0), "v"(hi32(W)));
-  asm("v_subb_co_u32_e64 %0, %1, %2, 0, %3" : "=v"(r1), "=s"(c3) : "v"(r1), "s"(c3));
-  asm("v_cndmask_b32_e64 %0, 0, -1, %1" : "=v"(e) : "s"(c3));
+  asm(QP_CWAIT "v_subb_co_u32_e64 %0, %1, %2, 0, %3" : "=v"(r1), "=s"(c3) : "v"(r1), "s"(c3));
+  asm(QP_CWAIT "v_cndmask_b32_e64 %0, 0, -1, %1" : "=v"(e) : "s"(c3));
   // borrow: t - w3 + 2^64 >= 2^64 - 2^32, minus eps stays >= 0
   asm("v_sub_co_u32_e64 %0, %1, %2, %3" : "=v"(r0), "=s"(c3) : "v"(r0), "v"(e));
-  asm("v_subb_co_u32_e64 %0, %1, %2, 0, %3" : "=v"(r1), "=s"(c3) : "v"(r1), "s"(c3));
+  asm(QP_CWAIT "v_subb_co_u32_e64 %0, %1, %2, 0, %3" : "=v"(r1), "=s"(c3) : "v"(r1), "s"(c3));
   return ((uint64_t)r1 << 32) | r0;
 }
 

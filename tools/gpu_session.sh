@@ -44,6 +44,10 @@ for s in "$@"; do
     test_commit) step pytest_commit 600 python -u -m pytest tests/test_gpu_commit.py -x -v --timeout 300 --timeout-method thread ;;
     lde_ab) step prof_lde_new 300 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/prof_lde_new -o run -- python3 tools/kbench.py 16 3 &&
             export QPGPU_LDE_PERCOSET=1 && step prof_lde_old 300 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/prof_lde_old -o run -- python3 tools/kbench.py 16 3 && unset QPGPU_LDE_PERCOSET ;;
+    ab_cw) for r in 1 2; do
+             step ab_cw1_$r 300 python bench.py --cpu-sample 0 --steps 10 &&
+             step ab_cw0_$r 300 env QPGPU_LIB=gpurun_ab/libqpgpu_cw0.so python bench.py --cpu-sample 0 --steps 10
+           done ;;
     isa) step isa_rates 300 tools/isa_rates ;;
     *) echo "unknown step $s" ;;
   esac
