@@ -41,6 +41,7 @@
 #include <hip/hip_runtime.h>
 #include "poseidon.h"
 #include "poseidon_mds_asm.h"
+#include "poseidon_partial_consts.h"
 
 namespace pf {
 
@@ -366,9 +367,124 @@ __device__ __forceinline__ void full_round_dyn(uint64_t s[12], const uint64_t *_
   mds_rows_block_dyn<0>(s, lo, hi, knext);
 }
 
+// ---- sparse partial rounds (tools/gen_poseidon_partial.py): round 3's MDS
+// merged with D_4 (rows 1..11 dense), then per partial round one S-box, one
+// dot product for lane 0 and 11 scalar multiply-adds.  Dense constants act on
+// 22-bit limbs (x = l0 + 2^22 l1 + 2^44 l2) through precomputed c 2^(22k) mod
+// p halves, so every accumulator stays < 2^60 and reduces in 4 instructions.
+// Same permutation as the plain rounds (QP_POSEIDON_SPARSE=0 keeps those).
+#ifndef QP_POSEIDON_SPARSE
+#define QP_POSEIDON_SPARSE 1
+#endif
+
+__device__ __forceinline__ void limbs22(uint64_t x, uint32_t l[3]) {
+  const uint32_t lo = lo32(x), hi = hi32(x);
+  l[0] = lo & 0x3FFFFFu;
+  l[1] = __builtin_amdgcn_alignbit(hi, lo, 22) & 0x3FFFFFu;
+  l[2] = hi >> 12;
+}
+
+// the generated tables as compile-time values (every product below has a
+// literal constant operand; zero halves emit nothing)
+enum { PT_INIT, PT_AHAT, PT_BV, PT_S0C };
+template <int TB, int OFF>
+__device__ __forceinline__ constexpr uint32_t ptab() {
+  return TB == PT_INIT ? pfp::INIT[OFF] : TB == PT_AHAT ? pfp::AHAT[OFF] : TB == PT_BV ? pfp::BV[OFF] : pfp::S0C[OFF];
+}
+
+// al/ah += sum_k l[k] * (halves of the constant at table TB, words OFF..OFF+5)
+template <int TB, int OFF, int K = 0>
+__device__ __forceinline__ void mac_limbs(uint64_t &al, uint64_t &ah, const uint32_t l[3]) {
+  if constexpr (K < 3) {
+    constexpr uint32_t cl = ptab<TB, OFF + 2 * K>(), ch = ptab<TB, OFF + 2 * K + 1>();
+    if constexpr (cl != 0) al += (uint64_t)l[K] * cl;
+    if constexpr (ch != 0) ah += (uint64_t)l[K] * ch;
+    mac_limbs<TB, OFF, K + 1>(al, ah, l);
+  }
+}
+
+// row I (1..11) of D_4 M over the limbs of all 12 lanes
+template <int I, int J = 0>
+__device__ __forceinline__ void init_row(uint64_t &al, uint64_t &ah, const uint32_t L[12][3]) {
+  if constexpr (J < 12) {
+    mac_limbs<PT_INIT, ((I - 1) * 12 + J) * 6>(al, ah, L[J]);
+    init_row<I, J + 1>(al, ah, L);
+  }
+}
+template <int I = 1>
+__device__ __forceinline__ void init_rows(uint64_t out[12], const uint32_t L[12][3]) {
+  if constexpr (I < 12) {
+    uint64_t al = pfp::INIT_K[2 * I], ah = pfp::INIT_K[2 * I + 1];
+    init_row<I>(al, ah, L);
+    out[I] = reduce_row(al, ah);
+    init_rows<I + 1>(out, L);
+  }
+}
+
+// s <- D_4 M s + D_4 c_4  (s = the S-box outputs of round 3)
+__device__ __forceinline__ void mds_init_sparse(uint64_t s[12]) {
+  uint32_t lo[12], hi[12], L[12][3];
+#pragma unroll
+  for (int j = 0; j < 12; j++) {
+    lo[j] = lo32(s[j]);
+    hi[j] = hi32(s[j]);
+    limbs22(s[j], L[j]);
+  }
+  uint64_t out[12];
+  {
+    uint64_t al, ah;
+    mds_row_block<0>(al, ah, lo, hi, pfp::INIT_K[0], pfp::INIT_K[1]);
+    out[0] = reduce_row(al, ah);
+  }
+  init_rows(out, L);
+#pragma unroll
+  for (int i = 0; i < 12; i++) s[i] = out[i];
+}
+
+template <int T, int J = 1>
+__device__ __forceinline__ void sparse_row0(uint64_t &al, uint64_t &ah, const uint64_t s[12]) {
+  if constexpr (J < 12) {
+    uint32_t L[3];
+    limbs22(s[J], L);
+    mac_limbs<PT_AHAT, (T * 11 + J - 1) * 6>(al, ah, L);
+    sparse_row0<T, J + 1>(al, ah, s);
+  }
+}
+template <int T, int I = 1>
+__device__ __forceinline__ void sparse_col0(uint64_t s[12], const uint32_t l0[3]) {
+  if constexpr (I < 12) {
+    uint64_t bl = (uint64_t)lo32(s[I]) + (T == 21 ? pfp::KLAST[2 * I] : 0u);
+    uint64_t bh = (uint64_t)hi32(s[I]) + (T == 21 ? pfp::KLAST[2 * I + 1] : 0u);
+    mac_limbs<PT_BV, (T * 11 + I - 1) * 6>(bl, bh, l0);
+    s[I] = reduce_row(bl, bh);
+    sparse_col0<T, I + 1>(s, l0);
+  }
+}
+
+// partial round 4 + T in sparse form (the next round's constants folded in)
+template <int T>
+__device__ __forceinline__ void partial_sparse(uint64_t s[12]) {
+  const uint64_t x0 = sbox(s[0]);
+  uint32_t l0[3];
+  limbs22(x0, l0);
+  uint64_t al = pfp::K0[2 * T], ah = pfp::K0[2 * T + 1];
+  mac_limbs<PT_S0C, 0>(al, ah, l0);
+  sparse_row0<T>(al, ah, s);
+  sparse_col0<T>(s, l0);
+  s[0] = reduce_row(al, ah);
+}
+
 template <int M, int R>
 __device__ __forceinline__ void rounds(uint64_t s[12]) {
-  if constexpr (M == 5 && R == 0) {
+  if constexpr (QP_POSEIDON_SPARSE && M == 3 && R == 3) {
+#pragma unroll
+    for (int i = 0; i < 12; i++) s[i] = sbox(s[i]);
+    mds_init_sparse(s);
+    rounds<M, 4>(s);
+  } else if constexpr (QP_POSEIDON_SPARSE && M == 3 && R >= 4 && R < 26) {
+    partial_sparse<R - 4>(s);
+    rounds<M, R + 1>(s);
+  } else if constexpr (M == 5 && R == 0) {
     // every round rolled: a ~4k-instruction permutation
 #pragma unroll 1
     for (int r = 0; r < 4; r++) full_round_dyn(s, ps::RC_DEV + (r + 1) * 12);

@@ -125,6 +125,7 @@ struct qp_prover {
   DevBuf wg_gens, wg_lvl, wg_wslot, wg_wslot_cm, wg_in_slots, wg_pi_slots, wg_vals, wg_in, wg_err, wg_pis;
   uint32_t wg_nslots = 0, wg_nin = 0, wg_nlev = 0;
   bool quotient_rereads = false;
+  bool pp_generic = false;  // QPGPU_PP_GENERIC=1: the runtime-shape k_pp_rows (A/B)
   uint64_t *h_in = nullptr;  // pinned [max_batch][wg_nin] commit() values
   std::vector<uint32_t> h_werr;
   std::vector<uint64_t> h_wpis;
@@ -390,6 +391,8 @@ int setup(qp_prover *P) {
   {
     const char *qv = getenv("QPGPU_QUOTIENT");
     P->quotient_rereads = qv && !strcmp(qv, "rereads");
+    const char *pv = getenv("QPGPU_PP_GENERIC");
+    P->pp_generic = pv && pv[0] && pv[0] != '0';
   }
   unsigned hw = std::thread::hardware_concurrency();
   unsigned nthreads = std::min<unsigned>(hw ? hw : 4, 16);
@@ -519,8 +522,12 @@ int prove_batch(qp_prover *P, const uint64_t *d_wires, const uint64_t *const *wi
 
   // ---- 2. partial products + Z (a9), commitment
   const uint64_t pbs = (uint64_t)nc * P->nchunks * n;
-  qpk::k_pp_rows<<<dim3(cdiv(n, 256), nb), 256, 0, s>>>(wv, P->sigmas.p, P->kis.p, P->chal.p, P->prods.p,
-                                                         P->log_n, P->R, P->qdf, nc, P->wires.cbs(), pbs, c->tw.fwd);
+  if (P->R == 80 && P->qdf == 8 && nc == 2 && !P->pp_generic)
+    qpk::k_pp_rows_t<80, 8><<<dim3(cdiv(n, 256), nb), 256, 0, s>>>(wv, P->sigmas.p, P->kis.p, P->chal.p, P->prods.p,
+                                                                    P->log_n, P->wires.cbs(), pbs, c->tw.fwd);
+  else
+    qpk::k_pp_rows<<<dim3(cdiv(n, 256), nb), 256, 0, s>>>(wv, P->sigmas.p, P->kis.p, P->chal.p, P->prods.p,
+                                                           P->log_n, P->R, P->qdf, nc, P->wires.cbs(), pbs, c->tw.fwd);
   qpk::k_z_scan<<<dim3(nc, nb), 1024, 8u * (qpk::ntt_lds_words(n) + 1024), s>>>(P->prods.p, P->zs.vals.p, P->log_n, nc, P->nchunks, pbs, P->zs.cbs());
   P->zs.build_from_values(c, nb);
   TRY(hipGetLastError());

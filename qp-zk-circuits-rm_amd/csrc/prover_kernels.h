@@ -60,6 +60,10 @@ struct FriComposeArgs {
 __global__ void k_pp_rows(const uint64_t *wires, const uint64_t *sigmas, const uint64_t *k_is, const uint64_t *chal,
                           uint64_t *prods, uint32_t log_n, uint32_t R, uint32_t qdf, uint32_t nc, uint64_t w_bstride,
                           uint64_t p_bstride, const uint64_t *tw);
+template <int R, int QDF>
+__global__ void k_pp_rows_t(const uint64_t *wires, const uint64_t *sigmas, const uint64_t *k_is, const uint64_t *chal,
+                            uint64_t *prods, uint32_t log_n, uint64_t w_bstride, uint64_t p_bstride,
+                            const uint64_t *tw);
 __global__ void k_z_scan(const uint64_t *prods, uint64_t *zs, uint32_t log_n, uint32_t nc, uint32_t nchunks,
                          uint64_t p_bstride, uint64_t z_bstride);
 template <int PH>

@@ -79,6 +79,87 @@ __global__ void __launch_bounds__(256) k_pp_rows(const uint64_t *__restrict__ wi
   }
 }
 
+// a^(p-2) by the addition chain of p - 2 = (2^32 - 2) 2^32 + (2^32 - 1):
+// 63 squarings + 8 products (the generic gl::inv runs a 64-step
+// square-and-multiply loop with a product per set bit: 125 products)
+__device__ __forceinline__ uint64_t inv_chain(uint64_t x) {
+  auto sq = [](uint64_t v, int k) {
+#pragma unroll
+    for (int i = 0; i < k; i++) v = gfn::mul(v, v);
+    return v;
+  };
+  const uint64_t t1 = x;
+  const uint64_t t2 = gfn::mul(sq(t1, 1), t1);   // x^(2^2-1)
+  const uint64_t t3 = gfn::mul(sq(t2, 1), t1);   // x^(2^3-1)
+  const uint64_t t6 = gfn::mul(sq(t3, 3), t3);   // x^(2^6-1)
+  const uint64_t t12 = gfn::mul(sq(t6, 6), t6);  // x^(2^12-1)
+  const uint64_t t24 = gfn::mul(sq(t12, 12), t12);
+  const uint64_t t30 = gfn::mul(sq(t24, 6), t6);
+  const uint64_t t31 = gfn::mul(sq(t30, 1), t1);  // x^(2^31-1)
+  const uint64_t t32 = gfn::mul(sq(t31, 1), t1);  // x^(2^32-1)
+  // x^(2^32-2) = (x^(2^31-1))^2; then shift up 32 and add 2^32-1
+  return gfn::mul(sq(sq(t31, 1), 32), t32);
+}
+
+// k_pp_rows for the leaf circuits' shape (R routed wires in chunks of QDF,
+// 2 challenges), compile-time so the per-row chunk values stay in registers:
+// the numerator term is w + gamma + k_j (beta x) (beta x once per row), and
+// the running quotient is kept as a fraction N_k / D_k (prefix products of
+// the chunk numerators and denominators), so one inversion of D_last per
+// challenge gives every D_k^-1 walking back (D_(k-1)^-1 = D_k^-1 den_k).
+// Non-canonical arithmetic inside (field_nc.h), canonical products out.  Same
+// values as k_pp_rows (plonky2 wires_permutation_partial_products_and_zs).
+template <int R, int QDF>
+__global__ void __launch_bounds__(256) k_pp_rows_t(const uint64_t *__restrict__ wires,
+                                                   const uint64_t *__restrict__ sigmas,
+                                                   const uint64_t *__restrict__ k_is,
+                                                   const uint64_t *__restrict__ chal, uint64_t *__restrict__ prods,
+                                                   uint32_t log_n, uint64_t w_bstride, uint64_t p_bstride,
+                                                   const uint64_t *__restrict__ tw) {
+  constexpr int NCH = (R + QDF - 1) / QDF;
+  const uint32_t n = 1u << log_n;
+  const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  const uint32_t b = blockIdx.y;
+  wires += b * w_bstride;
+  prods += b * p_bstride;
+  const uint64_t *ch = chal + b * CHAL_STRIDE;
+  const uint64_t x = wpow_N(tw, i, log_n);
+#pragma unroll 1
+  for (int c = 0; c < 2; c++) {
+    const uint64_t beta = ch[CH_BETA + c], gamma = ch[CH_GAMMA + c];
+    const uint64_t bx = gfn::mul(beta, x);
+    uint64_t N[NCH], den[NCH], D = 1;
+#pragma unroll
+    for (int k = 0; k < NCH; k++) {
+      uint64_t nn = 1, dd = 1;
+#pragma unroll
+      for (int jj = 0; jj < QDF; jj++) {
+        const int j = k * QDF + jj;
+        if (j < R) {
+          const uint64_t wg = gfn::add(wires[(uint64_t)j * n + i], gamma);
+          const uint64_t nj = gfn::add(wg, gfn::mul(k_is[j], bx));
+          const uint64_t dj = gfn::add(wg, gfn::mul(beta, sigmas[(uint64_t)j * n + i]));
+          nn = jj ? gfn::mul(nn, nj) : nj;
+          dd = jj ? gfn::mul(dd, dj) : dj;
+        }
+      }
+      N[k] = k ? gfn::mul(N[k - 1], nn) : nn;
+      den[k] = dd;
+      D = k ? gfn::mul(D, dd) : dd;
+    }
+    uint64_t dinv = inv_chain(D);
+    uint64_t *out = prods + (uint64_t)c * NCH * n + i;
+#pragma unroll
+    for (int k = NCH - 1; k >= 0; k--) {
+      out[(uint64_t)k * n] = gfn::canon(gfn::mul(N[k], dinv));
+      if (k) dinv = gfn::mul(dinv, den[k]);
+    }
+  }
+}
+template __global__ void k_pp_rows_t<80, 8>(const uint64_t *, const uint64_t *, const uint64_t *, const uint64_t *,
+                                            uint64_t *, uint32_t, uint64_t, uint64_t, const uint64_t *);
+
 // exclusive prefix product of the full-row products -> Z; pp_j = Z * P_j.
 // The row products go through LDS (coalesced in, each thread's contiguous
 // chunk scanned from LDS, Z written back over them), so every HBM access is a
