@@ -93,15 +93,34 @@ __device__ __forceinline__ uint64_t reduce_row(uint64_t al, uint64_t ah) {
 }
 
 // a * b mod p, a, b in [0, 2^64), result in [0, 2^64)
+#ifndef QP_MUL_FORM
+#define QP_MUL_FORM 1
+#endif
 __device__ __forceinline__ uint64_t mul(uint64_t a, uint64_t b) {
   const uint32_t a0 = lo32(a), a1 = hi32(a), b0 = lo32(b), b1 = hi32(b);
-  const uint64_t L = (uint64_t)a0 * b0;
-  const uint64_t T = (uint64_t)a0 * b1 + hi32(L);
-  const uint64_t U = (uint64_t)a1 * b0 + lo32(T);
-  const uint64_t V = (uint64_t)a1 * b1 + hi32(T);
-  const uint64_t W = V + hi32(U);  // < 2^64: a1 b1 + 2 (2^32 - 1) < 2^64
+  uint64_t W, X;
+  if constexpr (QP_MUL_FORM == 1) {
+    // middle column as one 65-bit sum: T = a0 b1 + L.hi, U = a1 b0 + T with
+    // its carry-out c (worth 2^96), W = a1 b1 + (U.hi | c << 32): one
+    // zero-extension and no separate 64-bit add (the form below needs three
+    // and a v_lshl_add_u64)
+    const uint64_t L = (uint64_t)a0 * b0;
+    const uint64_t T = (uint64_t)a0 * b1 + hi32(L);
+    uint64_t U, cu;
+    uint32_t ce;
+    asm("v_mad_u64_u32 %0, %1, %2, %3, %4" : "=v"(U), "=s"(cu) : "v"(a1), "v"(b0), "v"(T));
+    asm(QP_CWAIT "v_cndmask_b32_e64 %0, 0, 1, %1" : "=v"(ce) : "s"(cu));
+    W = (uint64_t)a1 * b1 + (((uint64_t)ce << 32) | hi32(U));  // < 2^64 (high half of a 128-bit product)
+    X = ((uint64_t)lo32(U) << 32) | lo32(L);
+  } else {
+    const uint64_t L = (uint64_t)a0 * b0;
+    const uint64_t T = (uint64_t)a0 * b1 + hi32(L);
+    const uint64_t U = (uint64_t)a1 * b0 + lo32(T);
+    const uint64_t V = (uint64_t)a1 * b1 + hi32(T);
+    W = V + hi32(U);  // < 2^64: a1 b1 + 2 (2^32 - 1) < 2^64
+    X = ((uint64_t)lo32(U) << 32) | lo32(L);
+  }
   // 128-bit product = X + 2^64 W, X = (L0, U0);  ≡ X + eps*w2 - w3
-  const uint64_t X = ((uint64_t)lo32(U) << 32) | lo32(L);
   uint64_t t, c1, c2, c3;
   uint32_t e;
   asm("v_mad_u64_u32 %0, %1, %2, -1, %3" : "=v"(t), "=s"(c1) : "v"(lo32(W)), "v"(X));
@@ -397,8 +416,11 @@ template <int TB, int OFF, int K = 0>
 __device__ __forceinline__ void mac_limbs(uint64_t &al, uint64_t &ah, const uint32_t l[3]) {
   if constexpr (K < 3) {
     constexpr uint32_t cl = ptab<TB, OFF + 2 * K>(), ch = ptab<TB, OFF + 2 * K + 1>();
-    if constexpr (cl != 0) al += (uint64_t)l[K] * cl;
-    if constexpr (ch != 0) ah += (uint64_t)l[K] * ch;
+    // explicit mads with the (dead) carry-out sunk into VCC: as C the compiler
+    // hands the carry the SGPR pair holding the constant, and the next
+    // constant's s_mov into it then costs a hazard s_nop per product
+    if constexpr (cl != 0) asm("v_mad_u64_u32 %0, vcc, %1, %2, %0" : "+v"(al) : "v"(l[K]), "s"(cl) : "vcc");
+    if constexpr (ch != 0) asm("v_mad_u64_u32 %0, vcc, %1, %2, %0" : "+v"(ah) : "v"(l[K]), "s"(ch) : "vcc");
     mac_limbs<TB, OFF, K + 1>(al, ah, l);
   }
 }
@@ -461,17 +483,66 @@ __device__ __forceinline__ void sparse_col0(uint64_t s[12], const uint32_t l0[3]
   }
 }
 
+// lane-0 dot product on the 32-bit halves of lanes 1..11 (AH2 pieces of
+// weights 1, 2^22, 2^44; each accumulator < 2^59)
+template <int T, int J = 1, int H = 0, int K = 0>
+__device__ __forceinline__ void sparse_row0_h(uint64_t S[3], const uint64_t s[12]) {
+  if constexpr (J < 12) {
+    constexpr uint32_t c = pfp::AH2[((T * 11 + J - 1) * 2 + H) * 3 + K];
+    const uint32_t v = H ? hi32(s[J]) : lo32(s[J]);
+    if constexpr (c != 0) asm("v_mad_u64_u32 %0, vcc, %1, %2, %0" : "+v"(S[K]) : "v"(v), "s"(c) : "vcc");
+    if constexpr (K < 2) sparse_row0_h<T, J, H, K + 1>(S, s);
+    else if constexpr (H == 0) sparse_row0_h<T, J, 1, 0>(S, s);
+    else sparse_row0_h<T, J + 1, 0, 0>(S, s);
+  }
+}
+
+// r - y for y < 2^40: a borrow means r - y + 2^64 (>= 2^64 - 2^40) was kept,
+// so subtracting eps = 2^64 mod p cannot borrow again
+__device__ __forceinline__ uint64_t sub_small(uint64_t r, uint32_t y0, uint32_t y1) {
+  uint32_t r0 = lo32(r), r1 = hi32(r), e;
+  uint64_t c;
+  asm("v_sub_co_u32_e64 %0, %1, %2, %3" : "=v"(r0), "=s"(c) : "v"(r0), "v"(y0));
+  asm(QP_CWAIT "v_subb_co_u32_e64 %0, %1, %2, %3, %4" : "=v"(r1), "=s"(c) : "v"(r1), "v"(y1), "s"(c));
+  asm(QP_CWAIT "v_cndmask_b32_e64 %0, 0, -1, %1" : "=v"(e) : "s"(c));
+  asm("v_sub_co_u32_e64 %0, %1, %2, %3" : "=v"(r0), "=s"(c) : "v"(r0), "v"(e));
+  asm(QP_CWAIT "v_subb_co_u32_e64 %0, %1, %2, 0, %3" : "=v"(r1), "=s"(c) : "v"(r1), "s"(c));
+  return ((uint64_t)r1 << 32) | r0;
+}
+
+#ifndef QP_PF_DOT_HALVES
+#define QP_PF_DOT_HALVES 1
+#endif
+
 // partial round 4 + T in sparse form (the next round's constants folded in)
 template <int T>
 __device__ __forceinline__ void partial_sparse(uint64_t s[12]) {
   const uint64_t x0 = sbox(s[0]);
   uint32_t l0[3];
   limbs22(x0, l0);
-  uint64_t al = pfp::K0[2 * T], ah = pfp::K0[2 * T + 1];
-  mac_limbs<PT_S0C, 0>(al, ah, l0);
-  sparse_row0<T>(al, ah, s);
-  sparse_col0<T>(s, l0);
-  s[0] = reduce_row(al, ah);
+  if constexpr (QP_PF_DOT_HALVES) {
+    // V = S0 + 2^22 S1 + 2^44 S2 + k,  25 x0 = 25 lo + (25 2^10) 2^22 hi
+    constexpr uint32_t kl = pfp::K0[2 * T], kh = pfp::K0[2 * T + 1];
+    uint64_t S[3];
+    asm("v_mad_u64_u32 %0, vcc, %1, 25, %2" : "=v"(S[0]) : "v"(lo32(x0)), "s"((uint64_t)kl) : "vcc");
+    S[1] = (uint64_t)hi32(x0) * 25600u;
+    S[2] = 0;
+    sparse_row0_h<T>(S, s);
+    sparse_col0<T>(s, l0);
+    // al + 2^32 ah - y:  2^22 S1 = 2^22 S1.lo + 2^32 (2^22 S1.hi);
+    // 2^44 S2 = 2^32 (2^12 S2.lo) + 2^76 S2.hi, 2^76 = 2^32 2^12 - 2^12 (mod p)
+    const uint64_t al = S[0] + (uint64_t)lo32(S[1]) * (1u << 22);
+    uint64_t ah = (uint64_t)kh + (uint64_t)hi32(S[1]) * (1u << 22);
+    ah += (uint64_t)lo32(S[2]) * (1u << 12);
+    ah += (uint64_t)hi32(S[2]) * (1u << 12);
+    s[0] = sub_small(reduce_row(al, ah), hi32(S[2]) << 12, hi32(S[2]) >> 20);
+  } else {
+    uint64_t al = pfp::K0[2 * T], ah = pfp::K0[2 * T + 1];
+    mac_limbs<PT_S0C, 0>(al, ah, l0);
+    sparse_row0<T>(al, ah, s);
+    sparse_col0<T>(s, l0);
+    s[0] = reduce_row(al, ah);
+  }
 }
 
 template <int M, int R>

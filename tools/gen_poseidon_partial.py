@@ -21,7 +21,10 @@ Device arithmetic: a state value x is split into 22-bit limbs
 x = l0 + 2^22 l1 + 2^44 l2, and every constant c of the sparse rows is stored
 as the three field elements c 2^(22k) mod p split into 32-bit halves, so a
 product-accumulate is 2 v_mad_u64_u32 per limb with all partial sums < 2^60
-(one 4-instruction reduction per output).
+(one 4-instruction reduction per output).  The lane-0 dot product instead
+multiplies the 32-bit halves of the state by 22/22/20-bit pieces of the
+constants (AH2: no limb extraction of the 11 inputs), three accumulators at
+weights 1, 2^22, 2^44 recombined once per round.
 
     python tools/gen_poseidon_partial.py   # writes the header, self-checks
 """
@@ -183,6 +186,11 @@ def emit(A, init_rows, init_k, kscalar, c26):
     arr("AHAT", [lc(A[r][0][j]) for r in range(4, 26) for j in range(W - 1)])
     arr("BV", [lc(A[r][1][i]) for r in range(4, 26) for i in range(W - 1)])
     arr("S0C", [lc(25)])
+    # AH2[t][j][h]: a_hat_j (h = 0, times the low half) and a_hat_j 2^32 mod p
+    # (h = 1, times the high half) as 22/22/20-bit pieces (weights 1, 2^22, 2^44)
+    def pieces(c):
+        return [c & 0x3FFFFF, (c >> 22) & 0x3FFFFF, c >> 44]
+    arr("AH2", [pieces(A[r][0][j] * (1 << (32 * h)) % P) for r in range(4, 26) for j in range(W - 1) for h in range(2)])
     k0 = [kscalar[r + 1] if r < 25 else c26[0] for r in range(4, 26)]
     arr("K0", [[k & 0xFFFFFFFF, k >> 32] for k in k0])
     arr("KLAST", [[c26[i] & 0xFFFFFFFF, c26[i] >> 32] for i in range(W)])
