@@ -146,6 +146,30 @@ __global__ void __launch_bounds__(256) k_merkle_levels(uint64_t *__restrict__ di
   }
 }
 
+// one wide tree level: lane t hashes children 2t, 2t+1 of level k-1 into node t
+// of level k (no LDS, no level loop: 69 VGPRs = 7 waves/SIMD against the
+// folding kernel's 103 = 4)
+__global__ void __launch_bounds__(256) k_merkle_level(uint64_t *__restrict__ digests, uint32_t log_N, uint32_t k,
+                                                      uint64_t d_bstride) {
+  const uint32_t t = blockIdx.x * blockDim.x + threadIdx.x;
+  if (t >= (1u << (log_N - k))) return;
+  digests += blockIdx.y * d_bstride;
+  const uint64_t top = (uint64_t)1 << (log_N + 1);
+  const uint64_t *c = digests + (top - ((uint64_t)1 << (log_N - k + 2))) * 4 + (uint64_t)t * 8;
+  uint64_t s[12];
+#pragma unroll
+  for (int j = 0; j < 8; j++) s[j] = c[j];
+  s[8] = s[9] = s[10] = s[11] = 0;
+  psd::permute_nc(s);
+  uint64_t *o = digests + (top - ((uint64_t)1 << (log_N - k + 1))) * 4 + (uint64_t)t * 4;
+#pragma unroll
+  for (int j = 0; j < 4; j++) o[j] = psd::canon(s[j]);
+}
+
+#ifndef QP_MERKLE_SINGLE
+#define QP_MERKLE_SINGLE 1
+#endif
+
 void leaf_hash(const uint64_t *cols, uint64_t stride, uint32_t ncols, const uint64_t *salt, uint32_t nsalt,
                uint64_t *digests, uint32_t N, uint32_t nbat, uint64_t c_bstride, uint64_t s_bstride,
                uint64_t d_bstride, hipStream_t s) {
@@ -164,7 +188,10 @@ void merkle_tree_from(uint64_t *digests, uint32_t log_N, uint32_t cap_h, uint32_
     // from 2^QP_MERKLE_FUSE_LOG nodes per tree down, the rest of the tree in one launch
     const uint32_t nl = lc > QP_MERKLE_FUSE_LOG ? 1 : ((lb + 1) < (K - k0 + 1) ? (lb + 1) : (K - k0 + 1));
     dim3 grid(1u << (lc - lb), nbat);
-    k_merkle_levels<<<grid, 1u << lb, 0, s>>>(digests, log_N, k0, nl, d_bstride);
+    if (QP_MERKLE_SINGLE && nl == 1)
+      k_merkle_level<<<grid, 1u << lb, 0, s>>>(digests, log_N, k0, d_bstride);
+    else
+      k_merkle_levels<<<grid, 1u << lb, 0, s>>>(digests, log_N, k0, nl, d_bstride);
     k0 += nl;
   }
 }

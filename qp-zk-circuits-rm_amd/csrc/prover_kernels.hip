@@ -249,6 +249,20 @@ struct WireRead {
 template <class RD>
 __device__ __forceinline__ void poseidon_gate_rd(const RD &WR, TermAcc &A);
 
+#ifndef QP_QPOS_SPARSE
+#define QP_QPOS_SPARSE 1
+#endif
+template <int T, class RD>
+__device__ __forceinline__ void qpos_partial(const RD &WR, TermAcc &A, uint64_t s[12]) {
+  if constexpr (T < 22) {
+    const uint64_t sb = WR(65 + T);
+    A.emit(gfn::sub(s[0], sb));
+    s[0] = sb;
+    pf::partial_sparse<T>(s);
+    qpos_partial<T + 1>(WR, A, s);
+  }
+}
+
 __device__ __forceinline__ void poseidon_gate(const uint64_t *__restrict__ wl, uint64_t N, TermAcc &A) {
   WireRead rd{wl, N, nullptr, 0};
   poseidon_gate_rd(rd, A);
@@ -284,15 +298,25 @@ __device__ __forceinline__ void poseidon_gate_rd(const RD &WR, TermAcc &A) {
     }
 #pragma unroll
     for (int i = 0; i < 12; i++) s[i] = gfn::sbox(s[i]);
-    rc_row(k, r + 1);
-    pf::mds_k(s, k);
+    if (QP_QPOS_SPARSE && r == 3) {
+      pf::mds_init_sparse(s);
+    } else {
+      rc_row(k, r + 1);
+      pf::mds_k(s, k);
+    }
   }
-  for (int r = 0; r < 22; r++) {
-    const uint64_t sb = WV(65 + r);
-    A.emit(gfn::sub(s[0], sb));
-    s[0] = gfn::sbox(sb);
-    rc_row(k, 5 + r);
-    pf::mds_k(s, k);
+  if constexpr (QP_QPOS_SPARSE) {
+    // sparse partial rounds (poseidon_fast.h): lane 0 before each S-box is the
+    // plain form's S-box input, so the wire checks are unchanged
+    qpos_partial<0>(WR, A, s);
+  } else {
+    for (int r = 0; r < 22; r++) {
+      const uint64_t sb = WV(65 + r);
+      A.emit(gfn::sub(s[0], sb));
+      s[0] = gfn::sbox(sb);
+      rc_row(k, 5 + r);
+      pf::mds_k(s, k);
+    }
   }
 #pragma unroll
   for (int r = 0; r < 4; r++) {
