@@ -19,6 +19,15 @@
 #ifndef QP_LEAF_PAIRS
 #define QP_LEAF_PAIRS 0
 #endif
+// occupancy cap of the hashing kernels (0: compiler's choice, 72 VGPRs = 7 waves/SIMD)
+#ifndef QP_HASH_WAVES
+#define QP_HASH_WAVES 0
+#endif
+#if QP_HASH_WAVES
+#define QP_HASH_OCC __attribute__((amdgpu_waves_per_eu(QP_HASH_WAVES)))
+#else
+#define QP_HASH_OCC
+#endif
 #ifndef QP_MERKLE_FUSE_LOG
 #define QP_MERKLE_FUSE_LOG 6
 #endif
@@ -49,7 +58,7 @@ __device__ __forceinline__ void leaf_digest(const uint64_t *__restrict__ cols, u
   for (int k = 0; k < 4; k++) s[k] = psd::canon(s[k]);
 }
 
-__global__ void __launch_bounds__(256) k_leaf_hash(const uint64_t *__restrict__ cols, uint64_t stride, uint32_t ncols,
+__global__ void __launch_bounds__(256) QP_HASH_OCC k_leaf_hash(const uint64_t *__restrict__ cols, uint64_t stride, uint32_t ncols,
                                                    const uint64_t *__restrict__ salt, uint32_t nsalt,
                                                    uint64_t *__restrict__ dig, uint32_t N, uint64_t c_bstride,
                                                    uint64_t s_bstride, uint64_t d_bstride) {
@@ -149,7 +158,7 @@ __global__ void __launch_bounds__(256) k_merkle_levels(uint64_t *__restrict__ di
 // one wide tree level: lane t hashes children 2t, 2t+1 of level k-1 into node t
 // of level k (no LDS, no level loop: 69 VGPRs = 7 waves/SIMD against the
 // folding kernel's 103 = 4)
-__global__ void __launch_bounds__(256) k_merkle_level(uint64_t *__restrict__ digests, uint32_t log_N, uint32_t k,
+__global__ void __launch_bounds__(256) QP_HASH_OCC k_merkle_level(uint64_t *__restrict__ digests, uint32_t log_N, uint32_t k,
                                                       uint64_t d_bstride) {
   const uint32_t t = blockIdx.x * blockDim.x + threadIdx.x;
   if (t >= (1u << (log_N - k))) return;
