@@ -166,11 +166,166 @@ __device__ __forceinline__ uint64_t sbox_c(uint64_t x) {
   return mul_c(x3, x4);
 }
 
+// ---- K independent products with their carry steps interleaved (K = 2, 3):
+// each asm statement below issues one step of every product, so a carry SGPR
+// written by product i's instruction is read K - 1 instructions (plus the
+// compiler's one-state pad after an asm statement) later — the gfx950 carry
+// hazard's two wait states are met by the other products' work instead of
+// s_nop (one product alone needs ~14 pad states).  Same arithmetic as mul():
+// U = a1 b0 + T with carry, W = a1 b1 + (U.hi | c << 32), X = (U.lo, L.lo),
+// then the 8-step reduction.  Measured slower (QP_MULK=1: leaf hash +4 %,
+// e2e -2 %, profiles/r02_ab_mulk.log): at 7 waves/SIMD the pads it removes
+// (8.0k -> 2.9k s_nop per permutation) were nearly free and it adds ~500
+// register-pair moves, so the default keeps one product at a time.
+#ifndef QP_MULK
+#define QP_MULK 0
+#endif
+#define QP_W2 QP_CWAIT  // K = 2: one explicit wait state before each carry read
+template <int K>
+__device__ __forceinline__ void mulk(const uint64_t *a, const uint64_t *b, uint64_t *r) {
+  static_assert(K == 2 || K == 3, "K");
+  uint64_t T[K], U[K], W[K], X[K], t[K], cs[K];
+  uint32_t ce[K], e[K], r0[K], r1[K];
+#pragma unroll
+  for (int i = 0; i < K; i++) {
+    const uint64_t L = (uint64_t)lo32(a[i]) * lo32(b[i]);
+    T[i] = (uint64_t)lo32(a[i]) * hi32(b[i]) + hi32(L);
+    X[i] = lo32(L);
+  }
+  if constexpr (K == 3) {
+    asm("v_mad_u64_u32 %0, %3, %6, %9, %12\n\t"
+        "v_mad_u64_u32 %1, %4, %7, %10, %13\n\t"
+        "v_mad_u64_u32 %2, %5, %8, %11, %14"
+        : "=&v"(U[0]), "=&v"(U[1]), "=&v"(U[2]), "=&s"(cs[0]), "=&s"(cs[1]), "=&s"(cs[2])
+        : "v"(hi32(a[0])), "v"(hi32(a[1])), "v"(hi32(a[2])), "v"(lo32(b[0])), "v"(lo32(b[1])), "v"(lo32(b[2])),
+          "v"(T[0]), "v"(T[1]), "v"(T[2]));
+    asm("v_cndmask_b32_e64 %0, 0, 1, %3\n\t"
+        "v_cndmask_b32_e64 %1, 0, 1, %4\n\t"
+        "v_cndmask_b32_e64 %2, 0, 1, %5"
+        : "=v"(ce[0]), "=v"(ce[1]), "=v"(ce[2]) : "s"(cs[0]), "s"(cs[1]), "s"(cs[2]));
+  } else {
+    asm("v_mad_u64_u32 %0, %2, %4, %6, %8\n\t"
+        "v_mad_u64_u32 %1, %3, %5, %7, %9"
+        : "=&v"(U[0]), "=&v"(U[1]), "=&s"(cs[0]), "=&s"(cs[1])
+        : "v"(hi32(a[0])), "v"(hi32(a[1])), "v"(lo32(b[0])), "v"(lo32(b[1])), "v"(T[0]), "v"(T[1]));
+    asm(QP_W2 "v_cndmask_b32_e64 %0, 0, 1, %2\n\t"
+        "v_cndmask_b32_e64 %1, 0, 1, %3"
+        : "=v"(ce[0]), "=v"(ce[1]) : "s"(cs[0]), "s"(cs[1]));
+  }
+#pragma unroll
+  for (int i = 0; i < K; i++) {
+    W[i] = (uint64_t)hi32(a[i]) * hi32(b[i]) + (((uint64_t)ce[i] << 32) | hi32(U[i]));
+    X[i] |= (uint64_t)lo32(U[i]) << 32;
+  }
+  if constexpr (K == 3) {
+    // t = X + eps w2 (carry c1); e = c1 ? eps : 0; t += e
+    asm("v_mad_u64_u32 %0, %3, %6, -1, %9\n\t"
+        "v_mad_u64_u32 %1, %4, %7, -1, %10\n\t"
+        "v_mad_u64_u32 %2, %5, %8, -1, %11"
+        : "=&v"(t[0]), "=&v"(t[1]), "=&v"(t[2]), "=&s"(cs[0]), "=&s"(cs[1]), "=&s"(cs[2])
+        : "v"(lo32(W[0])), "v"(lo32(W[1])), "v"(lo32(W[2])), "v"(X[0]), "v"(X[1]), "v"(X[2]));
+    asm("v_cndmask_b32_e64 %0, 0, -1, %3\n\t"
+        "v_cndmask_b32_e64 %1, 0, -1, %4\n\t"
+        "v_cndmask_b32_e64 %2, 0, -1, %5"
+        : "=v"(e[0]), "=v"(e[1]), "=v"(e[2]) : "s"(cs[0]), "s"(cs[1]), "s"(cs[2]));
+    asm("v_mad_u64_u32 %0, vcc, %3, 1, %0\n\t"
+        "v_mad_u64_u32 %1, vcc, %4, 1, %1\n\t"
+        "v_mad_u64_u32 %2, vcc, %5, 1, %2"
+        : "+v"(t[0]), "+v"(t[1]), "+v"(t[2]) : "v"(e[0]), "v"(e[1]), "v"(e[2]) : "vcc");
+    // r = t - w3 (borrow b); e = b ? eps : 0; r -= e
+    asm("v_sub_co_u32_e64 %0, %3, %6, %9\n\t"
+        "v_sub_co_u32_e64 %1, %4, %7, %10\n\t"
+        "v_sub_co_u32_e64 %2, %5, %8, %11"
+        : "=&v"(r0[0]), "=&v"(r0[1]), "=&v"(r0[2]), "=&s"(cs[0]), "=&s"(cs[1]), "=&s"(cs[2])
+        : "v"(lo32(t[0])), "v"(lo32(t[1])), "v"(lo32(t[2])), "v"(hi32(W[0])), "v"(hi32(W[1])), "v"(hi32(W[2])));
+    asm("v_subb_co_u32_e64 %0, %3, %6, 0, %3\n\t"
+        "v_subb_co_u32_e64 %1, %4, %7, 0, %4\n\t"
+        "v_subb_co_u32_e64 %2, %5, %8, 0, %5"
+        : "=&v"(r1[0]), "=&v"(r1[1]), "=&v"(r1[2]), "+s"(cs[0]), "+s"(cs[1]), "+s"(cs[2])
+        : "v"(hi32(t[0])), "v"(hi32(t[1])), "v"(hi32(t[2])));
+    asm("v_cndmask_b32_e64 %0, 0, -1, %3\n\t"
+        "v_cndmask_b32_e64 %1, 0, -1, %4\n\t"
+        "v_cndmask_b32_e64 %2, 0, -1, %5"
+        : "=v"(e[0]), "=v"(e[1]), "=v"(e[2]) : "s"(cs[0]), "s"(cs[1]), "s"(cs[2]));
+    asm("v_sub_co_u32_e64 %0, %3, %0, %6\n\t"
+        "v_sub_co_u32_e64 %1, %4, %1, %7\n\t"
+        "v_sub_co_u32_e64 %2, %5, %2, %8"
+        : "+v"(r0[0]), "+v"(r0[1]), "+v"(r0[2]), "=&s"(cs[0]), "=&s"(cs[1]), "=&s"(cs[2])
+        : "v"(e[0]), "v"(e[1]), "v"(e[2]));
+    asm("v_subb_co_u32_e64 %0, vcc, %0, 0, %3\n\t"
+        "v_subb_co_u32_e64 %1, vcc, %1, 0, %4\n\t"
+        "v_subb_co_u32_e64 %2, vcc, %2, 0, %5"
+        : "+v"(r1[0]), "+v"(r1[1]), "+v"(r1[2]) : "s"(cs[0]), "s"(cs[1]), "s"(cs[2]) : "vcc");
+  } else {
+    asm("v_mad_u64_u32 %0, %2, %4, -1, %6\n\t"
+        "v_mad_u64_u32 %1, %3, %5, -1, %7"
+        : "=&v"(t[0]), "=&v"(t[1]), "=&s"(cs[0]), "=&s"(cs[1])
+        : "v"(lo32(W[0])), "v"(lo32(W[1])), "v"(X[0]), "v"(X[1]));
+    asm(QP_W2 "v_cndmask_b32_e64 %0, 0, -1, %2\n\t"
+        "v_cndmask_b32_e64 %1, 0, -1, %3"
+        : "=v"(e[0]), "=v"(e[1]) : "s"(cs[0]), "s"(cs[1]));
+    asm("v_mad_u64_u32 %0, vcc, %2, 1, %0\n\t"
+        "v_mad_u64_u32 %1, vcc, %3, 1, %1"
+        : "+v"(t[0]), "+v"(t[1]) : "v"(e[0]), "v"(e[1]) : "vcc");
+    asm("v_sub_co_u32_e64 %0, %2, %4, %6\n\t"
+        "v_sub_co_u32_e64 %1, %3, %5, %7"
+        : "=&v"(r0[0]), "=&v"(r0[1]), "=&s"(cs[0]), "=&s"(cs[1])
+        : "v"(lo32(t[0])), "v"(lo32(t[1])), "v"(hi32(W[0])), "v"(hi32(W[1])));
+    asm(QP_W2 "v_subb_co_u32_e64 %0, %2, %4, 0, %2\n\t"
+        "v_subb_co_u32_e64 %1, %3, %5, 0, %3"
+        : "=&v"(r1[0]), "=&v"(r1[1]), "+s"(cs[0]), "+s"(cs[1])
+        : "v"(hi32(t[0])), "v"(hi32(t[1])));
+    asm(QP_W2 "v_cndmask_b32_e64 %0, 0, -1, %2\n\t"
+        "v_cndmask_b32_e64 %1, 0, -1, %3"
+        : "=v"(e[0]), "=v"(e[1]) : "s"(cs[0]), "s"(cs[1]));
+    asm("v_sub_co_u32_e64 %0, %2, %0, %4\n\t"
+        "v_sub_co_u32_e64 %1, %3, %1, %5"
+        : "+v"(r0[0]), "+v"(r0[1]), "=&s"(cs[0]), "=&s"(cs[1])
+        : "v"(e[0]), "v"(e[1]));
+    asm(QP_W2 "v_subb_co_u32_e64 %0, vcc, %0, 0, %2\n\t"
+        "v_subb_co_u32_e64 %1, vcc, %1, 0, %3"
+        : "+v"(r1[0]), "+v"(r1[1]) : "s"(cs[0]), "s"(cs[1]) : "vcc");
+  }
+#pragma unroll
+  for (int i = 0; i < K; i++) r[i] = ((uint64_t)r1[i] << 32) | r0[i];
+}
+
 __device__ __forceinline__ uint64_t sbox(uint64_t x) {
   const uint64_t x2 = mul(x, x);
-  const uint64_t x3 = mul(x2, x);
-  const uint64_t x4 = mul(x2, x2);
-  return mul(x3, x4);
+  if constexpr (QP_MULK) {
+    // x^3 and x^4 are independent: one interleaved pair
+    const uint64_t a[2] = {x2, x2}, b[2] = {x, x2};
+    uint64_t r[2];
+    mulk<2>(a, b, r);
+    return mul(r[0], r[1]);
+  } else {
+    const uint64_t x3 = mul(x2, x);
+    const uint64_t x4 = mul(x2, x2);
+    return mul(x3, x4);
+  }
+}
+
+// three S-boxes with every product interleaved three ways
+__device__ __forceinline__ void sbox3(uint64_t &x, uint64_t &y, uint64_t &z) {
+  uint64_t v[3] = {x, y, z}, v2[3], v3[3], v4[3], v7[3];
+  mulk<3>(v, v, v2);
+  mulk<3>(v2, v, v3);
+  mulk<3>(v2, v2, v4);
+  mulk<3>(v3, v4, v7);
+  x = v7[0];
+  y = v7[1];
+  z = v7[2];
+}
+
+// the 12 S-boxes of a full round
+__device__ __forceinline__ void sbox12(uint64_t s[12]) {
+  if constexpr (QP_MULK) {
+#pragma unroll
+    for (int i = 0; i < 12; i += 3) sbox3(s[i], s[i + 1], s[i + 2]);
+  } else {
+#pragma unroll
+    for (int i = 0; i < 12; i++) s[i] = sbox(s[i]);
+  }
 }
 
 // a + c, a in [0, 2^64), c < p
@@ -548,8 +703,7 @@ __device__ __forceinline__ void partial_sparse(uint64_t s[12]) {
 template <int M, int R>
 __device__ __forceinline__ void rounds(uint64_t s[12]) {
   if constexpr (QP_POSEIDON_SPARSE && M == 3 && R == 3) {
-#pragma unroll
-    for (int i = 0; i < 12; i++) s[i] = sbox(s[i]);
+    sbox12(s);
     mds_init_sparse(s);
     rounds<M, 4>(s);
   } else if constexpr (QP_POSEIDON_SPARSE && M == 3 && R >= 4 && R < 26) {
@@ -581,7 +735,9 @@ __device__ __forceinline__ void rounds(uint64_t s[12]) {
     rounds<M, 26>(s);
   } else if constexpr (R < 30) {
     constexpr bool full = R < 4 || R >= 26;
-    if constexpr (full) {
+    if constexpr (full && M == 3) {
+      sbox12(s);
+    } else if constexpr (full) {
 #pragma unroll
       for (int i = 0; i < 12; i++) s[i] = M == 2 ? sbox_c(s[i]) : sbox(s[i]);
     } else {

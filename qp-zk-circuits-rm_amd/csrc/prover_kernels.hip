@@ -296,8 +296,7 @@ __device__ __forceinline__ void poseidon_gate_rd(const RD &WR, TermAcc &A) {
         s[i] = sb;
       }
     }
-#pragma unroll
-    for (int i = 0; i < 12; i++) s[i] = gfn::sbox(s[i]);
+    pf::sbox12(s);
     if (QP_QPOS_SPARSE && r == 3) {
       pf::mds_init_sparse(s);
     } else {
@@ -326,8 +325,7 @@ __device__ __forceinline__ void poseidon_gate_rd(const RD &WR, TermAcc &A) {
       A.emit(gfn::sub(s[i], sb));
       s[i] = sb;
     }
-#pragma unroll
-    for (int i = 0; i < 12; i++) s[i] = gfn::sbox(s[i]);
+    pf::sbox12(s);
     if (r < 3) {
       rc_row(k, 27 + r);
       pf::mds_k(s, k);
