@@ -560,10 +560,11 @@ __device__ __forceinline__ void limbs22(uint64_t x, uint32_t l[3]) {
 
 // the generated tables as compile-time values (every product below has a
 // literal constant operand; zero halves emit nothing)
-enum { PT_INIT, PT_AHAT, PT_BV, PT_S0C };
+enum { PT_INIT, PT_AHAT, PT_BV, PT_S0C, PT_GAM };
 template <int TB, int OFF>
 __device__ __forceinline__ constexpr uint32_t ptab() {
-  return TB == PT_INIT ? pfp::INIT[OFF] : TB == PT_AHAT ? pfp::AHAT[OFF] : TB == PT_BV ? pfp::BV[OFF] : pfp::S0C[OFF];
+  return TB == PT_INIT ? pfp::INIT[OFF] : TB == PT_AHAT ? pfp::AHAT[OFF] : TB == PT_BV ? pfp::BV[OFF]
+       : TB == PT_GAM ? pfp::GAM[OFF] : pfp::S0C[OFF];
 }
 
 // al/ah += sum_k l[k] * (halves of the constant at table TB, words OFF..OFF+5)
@@ -700,6 +701,77 @@ __device__ __forceinline__ void partial_sparse(uint64_t s[12]) {
   }
 }
 
+// ---- groups of G partial rounds (tools/gen_poseidon_partial.py
+// permute_fast_grouped): lanes 1..11 only change by b_i x0 per round, so their
+// updates are deferred to the end of the group (one reduction per lane per
+// group instead of per round); round t's lane-0 dot then reads the group-start
+// lanes and adds gamma[t][l] x_l for the group's earlier S-box outputs x_l.
+#ifndef QP_PF_GROUP
+#define QP_PF_GROUP 4
+#endif
+struct NoHook {
+  __device__ __forceinline__ uint64_t operator()(int, uint64_t v) const { return v; }
+};
+
+template <int T0, int M, int L = 0>
+__device__ __forceinline__ void group_gammas(uint64_t &al, uint64_t &ah, const uint32_t (*l)[3]) {
+  if constexpr (L < M) {
+    mac_limbs<PT_GAM, ((T0 + M) * 22 + T0 + L) * 6>(al, ah, l[L]);
+    group_gammas<T0, M, L + 1>(al, ah, l);
+  }
+}
+
+template <int T0, int G, int M = 0, class HK>
+__device__ __forceinline__ void group_lane0(const uint64_t s[12], uint64_t &s0, uint32_t (*l)[3], const HK &hook) {
+  if constexpr (M < G) {
+    constexpr int T = T0 + M;
+    const uint64_t x = sbox(hook(T, s0));
+    limbs22(x, l[M]);
+    constexpr uint32_t kl = pfp::K0[2 * T], kh = pfp::K0[2 * T + 1];
+    uint64_t S[3];
+    asm("v_mad_u64_u32 %0, vcc, %1, 25, %2" : "=v"(S[0]) : "v"(lo32(x)), "s"((uint64_t)kl) : "vcc");
+    S[1] = (uint64_t)hi32(x) * 25600u;
+    S[2] = 0;
+    sparse_row0_h<T>(S, s);
+    uint64_t al = S[0] + (uint64_t)lo32(S[1]) * (1u << 22);
+    uint64_t ah = (uint64_t)kh + (uint64_t)hi32(S[1]) * (1u << 22);
+    ah += (uint64_t)lo32(S[2]) * (1u << 12);
+    ah += (uint64_t)hi32(S[2]) * (1u << 12);
+    group_gammas<T0, M>(al, ah, l);
+    s0 = sub_small(reduce_row(al, ah), hi32(S[2]) << 12, hi32(S[2]) >> 20);
+    group_lane0<T0, G, M + 1>(s, s0, l, hook);
+  }
+}
+
+template <int T0, int G, int I, int M>
+__device__ __forceinline__ void group_col_macs(uint64_t &bl, uint64_t &bh, const uint32_t (*l)[3]) {
+  if constexpr (M < G) {
+    mac_limbs<PT_BV, ((T0 + M) * 11 + I - 1) * 6>(bl, bh, l[M]);
+    group_col_macs<T0, G, I, M + 1>(bl, bh, l);
+  }
+}
+
+template <int T0, int G, int I = 1>
+__device__ __forceinline__ void group_cols(uint64_t s[12], const uint32_t (*l)[3]) {
+  if constexpr (I < 12) {
+    constexpr bool last = T0 + G == 22;
+    uint64_t bl = (uint64_t)lo32(s[I]) + (last ? pfp::KLAST[2 * I] : 0u);
+    uint64_t bh = (uint64_t)hi32(s[I]) + (last ? pfp::KLAST[2 * I + 1] : 0u);
+    group_col_macs<T0, G, I, 0>(bl, bh, l);
+    s[I] = reduce_row(bl, bh);
+    group_cols<T0, G, I + 1>(s, l);
+  }
+}
+
+template <int T0, int G, class HK = NoHook>
+__device__ __forceinline__ void partial_group(uint64_t s[12], const HK &hook = HK{}) {
+  uint32_t l[G][3];
+  uint64_t s0 = s[0];
+  group_lane0<T0, G>(s, s0, l, hook);
+  group_cols<T0, G>(s, l);
+  s[0] = s0;
+}
+
 template <int M, int R>
 __device__ __forceinline__ void rounds(uint64_t s[12]) {
   if constexpr (QP_POSEIDON_SPARSE && M == 3 && R == 3) {
@@ -707,8 +779,10 @@ __device__ __forceinline__ void rounds(uint64_t s[12]) {
     mds_init_sparse(s);
     rounds<M, 4>(s);
   } else if constexpr (QP_POSEIDON_SPARSE && M == 3 && R >= 4 && R < 26) {
-    partial_sparse<R - 4>(s);
-    rounds<M, R + 1>(s);
+    constexpr int T0 = R - 4, G = (22 - T0) < QP_PF_GROUP ? (22 - T0) : QP_PF_GROUP;
+    if constexpr (G > 1) partial_group<T0, G>(s);
+    else partial_sparse<T0>(s);
+    rounds<M, R + G>(s);
   } else if constexpr (M == 5 && R == 0) {
     // every round rolled: a ~4k-instruction permutation
 #pragma unroll 1

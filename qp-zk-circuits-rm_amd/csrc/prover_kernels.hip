@@ -252,14 +252,32 @@ __device__ __forceinline__ void poseidon_gate_rd(const RD &WR, TermAcc &A);
 #ifndef QP_QPOS_SPARSE
 #define QP_QPOS_SPARSE 1
 #endif
+// the partial-round wire check as the grouped rounds' pre-S-box hook: lane 0
+// is checked against the gate's S-box input wire and replaced by it
+template <class RD>
+struct QposHook {
+  const RD &WR;
+  TermAcc &A;
+  __device__ __forceinline__ uint64_t operator()(int T, uint64_t s0) const {
+    const uint64_t sb = WR(65 + T);
+    A.emit(gfn::sub(s0, sb));
+    return sb;
+  }
+};
+
 template <int T, class RD>
 __device__ __forceinline__ void qpos_partial(const RD &WR, TermAcc &A, uint64_t s[12]) {
   if constexpr (T < 22) {
-    const uint64_t sb = WR(65 + T);
-    A.emit(gfn::sub(s[0], sb));
-    s[0] = sb;
-    pf::partial_sparse<T>(s);
-    qpos_partial<T + 1>(WR, A, s);
+    constexpr int G = (22 - T) < QP_PF_GROUP ? (22 - T) : QP_PF_GROUP;
+    if constexpr (G > 1) {
+      pf::partial_group<T, G>(s, QposHook<RD>{WR, A});
+    } else {
+      const uint64_t sb = WR(65 + T);
+      A.emit(gfn::sub(s[0], sb));
+      s[0] = sb;
+      pf::partial_sparse<T>(s);
+    }
+    qpos_partial<T + G>(WR, A, s);
   }
 }
 

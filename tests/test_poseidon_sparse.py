@@ -30,6 +30,9 @@ def test_sparse_rounds_equal_plain_and_oracle():
         fast = g.permute_fast(s, A, init_rows, init_k, kscalar, c26)
         assert fast == g.permute_plain(s)
         assert fast == [int(x) for x in ora_permute(np.array(s, np.uint64))]
+        # grouped form (lane 1..11 updates deferred over G rounds, gamma terms)
+        for G in (2, 3, 4, 5):
+            assert g.permute_fast_grouped(s, A, init_rows, init_k, kscalar, c26, G) == fast
 
 
 def test_committed_header_is_generated(tmp_path, monkeypatch):

@@ -148,6 +148,55 @@ def permute_fast(s, A, init_rows, init_k, kscalar, c26):
     return s
 
 
+def gammas(A):
+    """gamma[t][l] = a_hat^(t) . b^(l) (t, l = partial round - 4, l < t): the
+    effect of round l's S-box output on round t's lane-0 dot when the lane
+    1..11 updates of rounds l..t-1 are deferred"""
+    g = [[0] * 22 for _ in range(22)]
+    for t in range(22):
+        for l in range(t):
+            g[t][l] = sum(a * b for a, b in zip(A[t + 4][0], A[l + 4][1])) % P
+    return g
+
+
+def permute_fast_grouped(s, A, init_rows, init_k, kscalar, c26, G):
+    """permute_fast with the lane 1..11 updates of G consecutive partial rounds
+    applied once per group (lane-0 dots use the group-start lanes + gamma terms)"""
+    gam = gammas(A)
+    s = list(s)
+    for r in range(4):
+        s = [(x + c) % P for x, c in zip(s, RC[r])]
+        s = [sbox(x) for x in s]
+        if r < 3:
+            s = matvec(M, s)
+    s = [(x + k) % P for x, k in zip(matvec(init_rows, s), init_k)]
+    for t0 in range(0, 22, G):
+        ts = list(range(t0, min(t0 + G, 22)))
+        xs = []
+        s0 = s[0]
+        for t in ts:
+            r = t + 4
+            x = sbox(s0)
+            k0 = kscalar[r + 1] if r < 25 else c26[0]
+            d = 25 * x + sum(a * v for a, v in zip(A[r][0], s[1:])) + k0
+            d += sum(gam[t][l] * xl for l, xl in zip(ts, xs))
+            xs.append(x)
+            s0 = d % P
+        rest = []
+        for i in range(1, W):
+            v = s[i] + sum(A[t + 4][1][i - 1] * x for t, x in zip(ts, xs))
+            if ts[-1] == 21:
+                v += c26[i]
+            rest.append(v % P)
+        s = [s0] + rest
+    for r in range(26, 30):
+        if r > 26:
+            s = [(x + c) % P for x, c in zip(s, RC[r])]
+        s = [sbox(x) for x in s]
+        s = matvec(M, s)
+    return s
+
+
 def limbs_consts(c):
     """c 2^(22k) mod p for k = 0, 1, 2 -> [(lo32, hi32)] * 3"""
     out = []
@@ -193,6 +242,9 @@ def emit(A, init_rows, init_k, kscalar, c26):
     arr("AH2", [pieces(A[r][0][j] * (1 << (32 * h)) % P) for r in range(4, 26) for j in range(W - 1) for h in range(2)])
     k0 = [kscalar[r + 1] if r < 25 else c26[0] for r in range(4, 26)]
     arr("K0", [[k & 0xFFFFFFFF, k >> 32] for k in k0])
+    # GAM[t][l] (l < t, zero elsewhere): a_hat^(t) . b^(l), as limb halves
+    gam = gammas(A)
+    arr("GAM", [lc(gam[t][l]) for t in range(22) for l in range(22)])
     arr("KLAST", [[c26[i] & 0xFFFFFFFF, c26[i] >> 32] for i in range(W)])
     L.append("}  // namespace pfp")
     open(HDR, "w").write("\n".join(L) + "\n")
@@ -204,6 +256,8 @@ def main():
     for _ in range(20):
         s = [rnd.randrange(P) for _ in range(W)]
         assert permute_fast(s, A, init_rows, init_k, kscalar, c26) == permute_plain(s)
+        for G in (1, 2, 3, 4, 6):
+            assert permute_fast_grouped(s, A, init_rows, init_k, kscalar, c26, G) == permute_plain(s)
     try:
         sys.path.insert(0, os.path.join(ROOT, "tests"))
         from oracle_lib import permute as ora_permute
