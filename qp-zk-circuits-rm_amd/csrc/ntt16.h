@@ -80,6 +80,23 @@ __device__ __forceinline__ uint64_t neg(uint64_t x) {
   return x ? gl::P - x : 0;
 }
 
+// r - (b ? eps : 0) for a borrow b of a subtraction whose wrapped result is
+// >= 2^64 - 2^63 (so subtracting eps cannot borrow again); r = (r0, r1)
+__device__ __forceinline__ uint64_t sub_borrow_eps(uint32_t r0, uint32_t r1, uint64_t b) {
+  uint32_t e;
+  uint64_t c;
+  asm(QP_CWAIT "v_cndmask_b32_e64 %0, 0, -1, %1" : "=v"(e) : "s"(b));
+  asm("v_sub_co_u32_e64 %0, %1, %2, %3" : "=v"(r0), "=s"(c) : "v"(r0), "v"(e));
+  asm(QP_CWAIT "v_subb_co_u32_e64 %0, %1, %2, 0, %3" : "=v"(r1), "=s"(c) : "v"(r1), "s"(c));
+  return ((uint64_t)r1 << 32) | r0;
+}
+
+// QP_POW2_FORM (default 1): mad-based reductions for shifts E in [32, 96)
+// (10 and 9 instructions against 14 and 23 for the reduce()-based forms)
+#ifndef QP_POW2_FORM
+#define QP_POW2_FORM 1
+#endif
+
 // x * 2^E for a compile-time E in [0, 192) (2^96 = -1, 2^192 = 1)
 template <int E>
 __device__ __forceinline__ uint64_t mul_pow2(uint64_t x) {
@@ -87,6 +104,32 @@ __device__ __forceinline__ uint64_t mul_pow2(uint64_t x) {
     return neg(mul_pow2<E - 96>(x));
   } else if constexpr (E == 0) {
     return x;
+  } else if constexpr (QP_POW2_FORM && E >= 32 && E < 64) {
+    // x 2^E = lo + 2^64 (h0 + 2^32 h1) = lo + h0 eps - h1  (h1 < 2^31)
+    const uint64_t lo = x << E, hi = x >> (64 - E);
+    uint64_t t, c;
+    uint32_t e;
+    asm("v_mad_u64_u32 %0, %1, %2, -1, %3" : "=v"(t), "=s"(c) : "v"((uint32_t)hi), "v"(lo));
+    asm(QP_CWAIT "v_cndmask_b32_e64 %0, 0, -1, %1" : "=v"(e) : "s"(c));
+    // carry: the wrapped t < 2^64 - 2^33 + 1, so + eps stays below 2^64
+    asm("v_mad_u64_u32 %0, %1, %2, 1, %3" : "=v"(t), "=s"(c) : "v"(e), "v"(t));
+    uint32_t r0, r1;
+    asm("v_sub_co_u32_e64 %0, %1, %2, %3" : "=v"(r0), "=s"(c) : "v"((uint32_t)t), "v"((uint32_t)(hi >> 32)));
+    asm(QP_CWAIT "v_subb_co_u32_e64 %0, %1, %2, 0, %3" : "=v"(r1), "=s"(c) : "v"((uint32_t)(t >> 32)), "s"(c));
+    return sub_borrow_eps(r0, r1, c);
+  } else if constexpr (QP_POW2_FORM && E >= 64) {
+    // E = 64 + F: x 2^E = x0 2^F 2^64 + x1 2^F 2^96 = u eps - v with
+    // u = x0 2^F, v = x1 2^F (< 2^63); u eps = u0 2^32 - u0 - u1, so
+    // x 2^E = (u0 << 32) - S, S = u0 + u1 + v < 2^64
+    constexpr int F = E - 64;
+    const uint64_t u = (uint64_t)(uint32_t)x << F, v = (x >> 32) << F;
+    const uint64_t S = v + (uint32_t)u + (uint32_t)(u >> 32);
+    uint32_t r0, r1;
+    uint64_t c;
+    asm("v_sub_co_u32_e64 %0, %1, 0, %2" : "=v"(r0), "=s"(c) : "v"((uint32_t)S));
+    asm(QP_CWAIT "v_subb_co_u32_e64 %0, %1, %2, %3, %1" : "=v"(r1), "+s"(c) : "v"((uint32_t)u), "v"((uint32_t)(S >> 32)));
+    // borrow: the wrapped A - S + 2^64 >= 2^64 - S > 2^63
+    return sub_borrow_eps(r0, r1, c);
   } else if constexpr (E < 64) {
     return reduce(x << E, x >> (64 - E));
   } else {
