@@ -139,7 +139,7 @@ __global__ void __launch_bounds__(256) k_merkle_levels(uint64_t *__restrict__ di
         for (int j = 0; j < 8; j++) s[j] = sh[t * 8 + j];
       }
       s[8] = s[9] = s[10] = s[11] = 0;
-      psd::permute_nc(s);
+      psd::permute_nc_node(s);
 #pragma unroll
       for (int j = 0; j < 4; j++) s[j] = psd::canon(s[j]);
       uint64_t *o = digests + (top - ((uint64_t)1 << (log_N - k + 1))) * 4 + (uint64_t)((base >> l) + t) * 4;
@@ -169,7 +169,7 @@ __global__ void __launch_bounds__(256) QP_HASH_OCC k_merkle_level(uint64_t *__re
 #pragma unroll
   for (int j = 0; j < 8; j++) s[j] = c[j];
   s[8] = s[9] = s[10] = s[11] = 0;
-  psd::permute_nc(s);
+  psd::permute_nc_node(s);
   uint64_t *o = digests + (top - ((uint64_t)1 << (log_N - k + 1))) * 4 + (uint64_t)t * 4;
 #pragma unroll
   for (int j = 0; j < 4; j++) o[j] = psd::canon(s[j]);

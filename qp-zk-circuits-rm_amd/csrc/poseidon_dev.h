@@ -99,6 +99,11 @@ __device__ __forceinline__ void permute_nc_v1(uint64_t s[12]) {
 #define QP_POSEIDON_MODE 3
 #endif
 __device__ __forceinline__ void permute_nc(uint64_t s[12]) { pf::permute_nc<QP_POSEIDON_MODE>(s); }
+// two_to_one form: s[8..11] == 0 on entry, only lanes 0..3 read
+__device__ __forceinline__ void permute_nc_node(uint64_t s[12]) {
+  if constexpr (QP_POSEIDON_MODE == 3) pf::permute_nc_capz<0xFu>(s);
+  else pf::permute_nc<QP_POSEIDON_MODE>(s);
+}
 
 __device__ __forceinline__ void permute(uint64_t s[12]) {
   permute_nc(s);

@@ -456,14 +456,16 @@ __device__ __forceinline__ void mds_row_block(uint64_t &al, uint64_t &ah, const 
   (void)cd;
 }
 
-template <int R, int RC>
+template <int R, int RC, uint32_t OUT = 0xFFFu>
 __device__ __forceinline__ void mds_rows_block(uint64_t s[12], const uint32_t lo[12], const uint32_t hi[12]) {
   if constexpr (R < 12) {
-    constexpr uint64_t k = RC >= 0 ? ps::rc_cx(RC * 12 + R) : 0;
-    uint64_t al, ah;
-    mds_row_block<R>(al, ah, lo, hi, k & EPS, k >> 32);
-    s[R] = reduce_row(al, ah);
-    mds_rows_block<R + 1, RC>(s, lo, hi);
+    if constexpr ((OUT >> R) & 1) {  // rows nobody reads (OUT) are skipped
+      constexpr uint64_t k = RC >= 0 ? ps::rc_cx(RC * 12 + R) : 0;
+      uint64_t al, ah;
+      mds_row_block<R>(al, ah, lo, hi, k & EPS, k >> 32);
+      s[R] = reduce_row(al, ah);
+    }
+    mds_rows_block<R + 1, RC, OUT>(s, lo, hi);
   }
 }
 
@@ -499,8 +501,8 @@ __device__ __forceinline__ void mds_rows_multi(uint64_t s[12], const uint32_t lo
   }
 }
 
-// s <- MDS(s) + RC[next] (next < 0: no constant)
-template <int M, int NEXT>
+// s <- MDS(s) + RC[next] (next < 0: no constant); OUT: the output rows needed
+template <int M, int NEXT, uint32_t OUT = 0xFFFu>
 __device__ __forceinline__ void mds(uint64_t s[12]) {
   uint32_t lo[12], hi[12];
 #pragma unroll
@@ -509,7 +511,7 @@ __device__ __forceinline__ void mds(uint64_t s[12]) {
     hi[i] = hi32(s[i]);
   }
   if constexpr (M >= 6) mds_rows_multi<mds_block_rows<M>(), 0, NEXT>(s, lo, hi);
-  else if constexpr (M >= 3) mds_rows_block<0, NEXT>(s, lo, hi);
+  else if constexpr (M >= 3) mds_rows_block<0, NEXT, OUT>(s, lo, hi);
   else mds_rows<M, 0, NEXT>(s, lo, hi);
 }
 
@@ -772,17 +774,19 @@ __device__ __forceinline__ void partial_group(uint64_t s[12], const HK &hook = H
   s[0] = s0;
 }
 
-template <int M, int R>
+// OUT: bit mask of the output lanes the caller reads (the last MDS computes
+// only those rows; digests need lanes 0..3, the PoW lane 7)
+template <int M, int R, uint32_t OUT = 0xFFFu>
 __device__ __forceinline__ void rounds(uint64_t s[12]) {
   if constexpr (QP_POSEIDON_SPARSE && M == 3 && R == 3) {
     sbox12(s);
     mds_init_sparse(s);
-    rounds<M, 4>(s);
+    rounds<M, 4, OUT>(s);
   } else if constexpr (QP_POSEIDON_SPARSE && M == 3 && R >= 4 && R < 26) {
     constexpr int T0 = R - 4, G = (22 - T0) < QP_PF_GROUP ? (22 - T0) : QP_PF_GROUP;
     if constexpr (G > 1) partial_group<T0, G>(s);
     else partial_sparse<T0>(s);
-    rounds<M, R + G>(s);
+    rounds<M, R + G, OUT>(s);
   } else if constexpr (M == 5 && R == 0) {
     // every round rolled: a ~4k-instruction permutation
 #pragma unroll 1
@@ -817,8 +821,58 @@ __device__ __forceinline__ void rounds(uint64_t s[12]) {
     } else {
       s[0] = M == 2 ? sbox_c(s[0]) : sbox(s[0]);
     }
-    mds<M, R + 1 < 30 ? R + 1 : -1>(s);
-    rounds<M, R + 1>(s);
+    if constexpr (R == 29) mds<M, -1, OUT>(s);
+    else mds<M, R + 1>(s);
+    rounds<M, R + 1, OUT>(s);
+  }
+}
+
+// round 0 of a state whose lanes 8..11 enter as zero (two_to_one, the first
+// absorption of a sponge): their S-box outputs are constants, so only lanes
+// 0..7 are S-boxed and each MDS row takes 16 mads on them, starting from the
+// folded constant CAPZ_K[r] = RC[1][r] + sum_(j>=8) M[r][j] sbox(RC[0][j])
+template <int R, int I = 0>
+__device__ __forceinline__ void capz_row_terms(uint64_t &al, uint64_t &ah, const uint32_t lo[12], const uint32_t hi[12]) {
+  if constexpr (I < 12) {
+    constexpr int J = (I + R) % 12;
+    if constexpr (J < 8) {
+      constexpr int C = (int)ps::mds_circ(I) + ((R == 0 && I == 0) ? 8 : 0);
+      al = mad_c<C>(lo[J], al);
+      ah = mad_c<C>(hi[J], ah);
+    }
+    capz_row_terms<R, I + 1>(al, ah, lo, hi);
+  }
+}
+template <int R = 0>
+__device__ __forceinline__ void capz_mds(uint64_t s[12], const uint32_t lo[12], const uint32_t hi[12]) {
+  if constexpr (R < 12) {
+    uint64_t al = pfp::CAPZ_K[2 * R], ah = pfp::CAPZ_K[2 * R + 1];
+    capz_row_terms<R>(al, ah, lo, hi);
+    s[R] = reduce_row(al, ah);
+    capz_mds<R + 1>(s, lo, hi);
+  }
+}
+
+#ifndef QP_POSEIDON_CAPZ
+#define QP_POSEIDON_CAPZ 1
+#endif
+// permute_nc for s[8..11] == 0 on entry (mode 3), reading only lanes OUT
+template <uint32_t OUT = 0xFFFu>
+__device__ __forceinline__ void permute_nc_capz(uint64_t s[12]) {
+  if constexpr (!QP_POSEIDON_CAPZ) {
+#pragma unroll
+    for (int i = 0; i < 12; i++) s[i] = add_c(s[i], ps::rc_cx(i));
+    rounds<3, 0, OUT>(s);
+  } else {
+    uint32_t lo[12], hi[12];
+#pragma unroll
+    for (int i = 0; i < 8; i++) {
+      s[i] = sbox(add_c(s[i], ps::rc_cx(i)));
+      lo[i] = lo32(s[i]);
+      hi[i] = hi32(s[i]);
+    }
+    capz_mds(s, lo, hi);
+    rounds<3, 1, OUT>(s);
   }
 }
 

@@ -1084,7 +1084,7 @@ __device__ __forceinline__ bool pow_hit(const uint64_t *__restrict__ pre, uint32
     const uint32_t c = (uint32_t)pre[12 + r];
     s[r] = pf::reduce_row((uint64_t)y0 * c + (pre[r] & pf::EPS), (uint64_t)y1 * c + (pre[r] >> 32));
   }
-  pf::rounds<QP_POSEIDON_MODE, 1>(s);
+  pf::rounds<QP_POSEIDON_MODE, 1, 0x80u>(s);  // only lane 7 is read
   return (psd::canon(s[7]) >> (64 - bits)) == 0;
 }
 
@@ -1128,7 +1128,7 @@ __global__ void __launch_bounds__(256) k_pow(const uint64_t *__restrict__ states
     const uint32_t c = (uint32_t)pre[12 + r];
     s[r] = pf::reduce_row((uint64_t)y0 * c + (pre[r] & pf::EPS), (uint64_t)y1 * c + (pre[r] >> 32));
   }
-  pf::rounds<QP_POSEIDON_MODE, 1>(s);
+  pf::rounds<QP_POSEIDON_MODE, 1, 0x80u>(s);  // only lane 7 is read
   if ((psd::canon(s[7]) >> (64 - bits)) == 0) atomicMin((unsigned long long *)&found[b], (unsigned long long)cand);
 }
 

@@ -242,6 +242,12 @@ def emit(A, init_rows, init_k, kscalar, c26):
     arr("AH2", [pieces(A[r][0][j] * (1 << (32 * h)) % P) for r in range(4, 26) for j in range(W - 1) for h in range(2)])
     k0 = [kscalar[r + 1] if r < 25 else c26[0] for r in range(4, 26)]
     arr("K0", [[k & 0xFFFFFFFF, k >> 32] for k in k0])
+    # CAPZ_K[r]: round 1's constant plus row r of the round-0 MDS applied to
+    # the S-box outputs of lanes 8..11 when they enter the permutation as zero
+    # (two_to_one / first absorption: sbox(0 + RC[0][j]) is a constant)
+    cz = [sbox(RC[0][j]) if j >= 8 else 0 for j in range(W)]
+    capz = [(RC[1][r] + sum(M[r][j] * cz[j] for j in range(8, W))) % P for r in range(W)]
+    arr("CAPZ_K", [[k & 0xFFFFFFFF, k >> 32] for k in capz])
     # GAM[t][l] (l < t, zero elsewhere): a_hat^(t) . b^(l), as limb halves
     gam = gammas(A)
     arr("GAM", [lc(gam[t][l]) for t in range(22) for l in range(22)])
