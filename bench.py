@@ -79,6 +79,9 @@ def parse():
                     help="wormhole = BASELINE configs[2] (the headline); voting = configs[4]")
     ap.add_argument("--mode", choices=["e2e", "wires-dev"], default="e2e",
                     help="e2e: CircuitInputs -> proofs (headline); wires-dev: prove() from HBM-resident wires")
+    ap.add_argument("--no-pipeline", dest="pipeline", action="store_false",
+                    help="join the prover threads after every step (default: each prover runs its share of all "
+                         "steps back to back)")
     ap.add_argument("--cpu-sample", type=int, default=2, help="min proofs in the CPU baseline sample (0 = skip)")
     ap.add_argument("--cpu-seconds", type=float, default=10.0, help="min seconds of CPU baseline proving")
     return ap.parse_args()
@@ -194,6 +197,32 @@ def main():
             gather_proofs(proofs, prover.proof_size, dist, device=f"cuda:{local}")
         return proofs
 
+    def steps_pipelined(k):
+        """k steps with each prover thread running its share of every step
+        back to back (no join between steps, so no prover idles the GPU while
+        the slowest finishes a step); the steps' leaf proofs are then gathered
+        step by step.  Same work as k calls of step()."""
+        outs = [[None] * k for _ in range(NP)]
+
+        def run(i):
+            for s in range(k):
+                if args.mode == "e2e":
+                    outs[i][s] = provers[i].prove_inputs_array(cin[i], per[i])
+                else:
+                    outs[i][s] = provers[i].prove_wires_dev(d_wires.data_ptr() + first[i] * wstride,
+                                                            pis[first[i]:first[i] + per[i]], per[i])
+        th = [threading.Thread(target=run, args=(i,)) for i in range(NP)]
+        for t in th:
+            t.start()
+        for t in th:
+            t.join()
+        if any(o is None for row in outs for o in row):
+            raise RuntimeError("a prover thread failed")
+        for s in range(k):
+            proofs = [p for i in range(NP) for p in outs[i][s]]
+            if dist is not None:
+                gather_proofs(proofs, prover.proof_size, dist, device=f"cuda:{local}")
+
     for _ in range(args.warmup):
         proofs = step()
     # proofs of the warmup verify (rank 0 checks the first and last with the oracle verifier)
@@ -210,8 +239,11 @@ def main():
         dist.barrier()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
-    for _ in range(args.steps):
-        step()
+    if args.pipeline and NP > 1:
+        steps_pipelined(args.steps)
+    else:
+        for _ in range(args.steps):
+            step()
     torch.cuda.synchronize()
     if dist is not None:
         dist.barrier()
@@ -294,6 +326,7 @@ def main():
             "config": {"workload": f"batch{B}_{circuit.kind}_proofs_per_gpu",
                        "circuit": f"{circuit.kind} deg{circuit.degree_bits} (135 wires)",
                        "batch_per_gpu": B, "provers_per_gpu": NP,
+                       "step_schedule": "pipelined" if (args.pipeline and NP > 1) else "joined per step",
                        "parallelism": f"proofs sharded x{world}, RCCL gather of leaf proofs"},
             "roofline": {"kernel": f"k_lde (wires LDE, 135 cols x 2^{circuit.degree_bits} -> "
                                    f"2^{circuit.degree_bits + 3})", "bound": "hbm",
