@@ -36,16 +36,17 @@ sys.path.insert(0, os.path.join(ROOT, "tests"))
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec peak (MI355X_MICROARCH.md)
 # VALU issue ceiling of the dominant (Poseidon) kernels: 1024 SIMDs x 2.4 GHz /
 # 2.56 cycles per VOP3 wave-instruction at 8 waves/SIMD (profiles/r02_isa_rates.log,
-# tools/gen_isa_rates.py); one permutation = 15,356 VALU instructions (PMC
-# SQ_INSTS_VALU per wave of the one-permutation-per-lane Merkle level kernel,
-# profiles/r02_v9_pmc_valu_b128.txt: sparse partial rounds in groups of 4;
-# 18,617 at the start of round 2)
+# tools/gen_isa_rates.py); one (general) permutation = 15,356 VALU
+# instructions (PMC SQ_INSTS_VALU per wave of the one-permutation-per-lane
+# Merkle level kernel, profiles/r02_v9_pmc_valu_b128.txt: sparse partial rounds
+# in groups of 4; 18,617 at the start of round 2; the Merkle kernel itself now
+# runs the zero-capacity form, 15,020 in profiles/r02_v10_pmc_valu_b128.txt)
 VALU_PEAK_WAVE_INSTR_S = 1024 * 2.4e9 / 2.56
 PERM_VALU_INSTR = 15356
 # HBM traffic of the roofline kernel from rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE
 # passes (tools/pmc_summary.py applies the gfx950 corrections); per proof, scaled
 # to the bench's per-launch proof count
-PMC_FILE = os.path.join(ROOT, "profiles", "r02_v9_pmc_hbm_b128.json")
+PMC_FILE = os.path.join(ROOT, "profiles", "r02_v10_pmc_hbm_b128.json")
 
 
 def pmc_traffic(kernel, ncols, log_n, proofs, lanes_per_proof=None):
@@ -336,7 +337,7 @@ def main():
                                                 per[0]) if circuit.degree_bits == 13 else None,
                          "traffic_unit": "bytes per launch",
                          "algorithmic_bytes_per_launch": lde["units"] / max(lde["launches"], 1),
-                         "traffic_source": "profiles/r02_v9_pmc_hbm_b128.json (rocprofv3 --pmc FETCH_SIZE, WRITE_SIZE "
+                         "traffic_source": "profiles/r02_v10_pmc_hbm_b128.json (rocprofv3 --pmc FETCH_SIZE, WRITE_SIZE "
                                            "passes of this bench at batch 128), per proof x proofs per launch",
                          "avg_launch_ms": lde["ms"] / max(lde["launches"], 1),
                          "note": "HIP events on the prover stream around each launch of the kernel"},
@@ -379,7 +380,7 @@ def main():
         if vk.get("leaf_hash_wires_perms_per_s"):
             ach = vk["leaf_hash_wires_perms_per_s"] / 64 * PERM_VALU_INSTR
             rec["dominant_kernel"] = {
-                "kernel": "k_leaf_hash (Poseidon Merkle leaves, ~57 % of GPU time, profiles/r02_v9_rocprof_bench_b256_1prover_kernel_stats.csv)", "bound": "valu",
+                "kernel": "k_leaf_hash (Poseidon Merkle leaves, ~58 % of GPU time, profiles/r02_v10_rocprof_bench_b256_1prover_kernel_stats.csv)", "bound": "valu",
                 "achieved": ach, "peak": VALU_PEAK_WAVE_INSTR_S, "unit": "wave-instructions/s",
                 "frac": ach / VALU_PEAK_WAVE_INSTR_S, "instr_per_perm": PERM_VALU_INSTR,
                 "note": "issue-bound 64-bit integer work (no MFMA path); peak from the measured VOP3 issue cost"}
