@@ -195,7 +195,7 @@ def main():
     def step():
         proofs = prove_all()
         if dist is not None:  # leaf proofs -> aggregator rank over RCCL
-            gather_proofs(proofs, prover.proof_size, dist, device=f"cuda:{local}")
+            gather_proofs(proofs, prover.proof_size, dist, device=f"cuda:{local}", raw=True)
         return proofs
 
     def steps_pipelined(k):
@@ -222,7 +222,7 @@ def main():
         for s in range(k):
             proofs = [p for i in range(NP) for p in outs[i][s]]
             if dist is not None:
-                gather_proofs(proofs, prover.proof_size, dist, device=f"cuda:{local}")
+                gather_proofs(proofs, prover.proof_size, dist, device=f"cuda:{local}", raw=True)
 
     for _ in range(args.warmup):
         proofs = step()

@@ -19,6 +19,12 @@ def shard(total: int, rank: int, world: int) -> range:
 
 def pack_proofs(proofs, slot: int) -> np.ndarray:
     """[n][8 + slot] uint8: little-endian length prefix + proof bytes (zero padded)."""
+    if proofs and all(len(p) == slot for p in proofs):
+        # fixed-size proofs (the prover's case): one join + one strided copy
+        out = np.empty((len(proofs), 8 + slot), np.uint8)
+        out[:, :8] = np.frombuffer(slot.to_bytes(8, "little"), np.uint8)
+        out[:, 8:] = np.frombuffer(b"".join(proofs), np.uint8).reshape(len(proofs), slot)
+        return out
     out = np.zeros((len(proofs), 8 + slot), np.uint8)
     for i, p in enumerate(proofs):
         if len(p) > slot:
@@ -36,11 +42,14 @@ def unpack_proofs(arr: np.ndarray):
     return res
 
 
-def gather_proofs(proofs, slot: int, dist, device="cpu", dst: int = 0):
+def gather_proofs(proofs, slot: int, dist, device="cpu", dst: int = 0, raw: bool = False):
     """Gather every rank's proofs to `dst` in rank order; returns the list on dst,
     None elsewhere.  Shards may differ in size (2048 over 3 ranks): counts are
     exchanged first and short shards padded with empty entries, which dst drops
-    (a serialized proof is never empty)."""
+    (a serialized proof is never empty).  raw=True returns, on dst, the
+    gathered [rank] tensors of packed rows ([n][8 + slot] uint8, on `device`)
+    and the per-rank counts instead of Python bytes objects (what a consumer
+    reading the packed buffer needs; no per-proof host copies)."""
     import torch
     rank, world = dist.get_rank(), dist.get_world_size()
     if any(len(p) == 0 for p in proofs):
@@ -54,6 +63,8 @@ def gather_proofs(proofs, slot: int, dist, device="cpu", dst: int = 0):
     dist.gather(t, bufs, dst=dst)
     if rank != dst:
         return None
+    if raw:
+        return bufs, [int(c.item()) for c in counts]
     out = []
     for b in bufs:
         out.extend(p for p in unpack_proofs(b.cpu().numpy()) if p)

@@ -26,6 +26,15 @@ def test_pack_roundtrip():
         pack_proofs([b"x" * 300], 200)
 
 
+def test_pack_fixed_size_fast_path():
+    """Fixed-size proofs (the prover's case) take the one-copy path; same rows."""
+    proofs = [bytes([i]) * 64 for i in range(7)]
+    fast = pack_proofs(proofs, 64)
+    slow = pack_proofs(proofs + [b"z"], 64)[:7]
+    assert (fast == slow).all()
+    assert unpack_proofs(fast) == proofs
+
+
 def _free_port():
     s = socket.socket()
     s.bind(("127.0.0.1", 0))
@@ -67,6 +76,31 @@ def test_gather_world2_gloo():
     got = _run(_worker, 2)
     expect = [bytes([r * 16 + i]) * (1000 + r) for r in range(2) for i in shard(8, r, 2)]
     assert got == expect
+
+
+def _worker_raw(rank, world, port, q):
+    import torch.distributed as dist
+    from qp_wormhole.distributed import gather_proofs
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    mine = [bytes([rank * 16 + i]) * 512 for i in shard(7, rank, world)]  # uneven shards, fixed size
+    got = gather_proofs(mine, 512, dist, raw=True)
+    if rank == 0:
+        bufs, counts = got
+        q.put((counts, [unpack_proofs(b.numpy()) for b in bufs]))
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+def test_gather_raw_world3_gloo():
+    """raw=True (the bench's mode): the dst rank gets the packed per-rank
+    buffers and counts; rows past a rank's count are padding."""
+    counts, rows = _run(_worker_raw, 3)
+    assert counts == [len(shard(7, r, 3)) for r in range(3)]
+    for r in range(3):
+        want = [bytes([r * 16 + i]) * 512 for i in shard(7, r, 3)]
+        assert [p for p in rows[r] if p] == want
 
 
 def _worker_real(rank, world, port, q, total):
