@@ -120,11 +120,20 @@ typedef struct {
     const uint8_t *const *nodes;       /* node byte strings */
     const uint32_t *node_lens;
     const uint64_t *indices;           /* hex-character child-hash indices */
+    /* zk config only (NULL otherwise): values of the PublicInputGate row's
+     * unused wires 4..num_wires-1 (num_wires - 4 canonical felts), which the
+     * reference fills from RandomValueGenerator (plonky2 CircuitBuilder::build,
+     * randomize_unused_pi_wires).  NULL under zk = derived deterministically
+     * from the private inputs (a Poseidon nonce; see DESIGN.md "zk").        */
+    const uint64_t *zk_randomness;
 } qp_wormhole_inputs;
 
 /* WormholeCircuit::new(config) + build_prover (wormhole/circuit/src/circuit.rs:76-108,
  * wormhole/prover/src/lib.rs:190-202) — host part.  zero_knowledge selects
- * standard_recursion_zk_config (salted commitments) vs standard_recursion_config. */
+ * standard_recursion_zk_config vs standard_recursion_config.  Under the
+ * workspace's `no_random` feature the two share the preprocessing and proof
+ * shape (no salt columns; tests/test_current_circuit_fixture.py); zk adds the
+ * PublicInputGate row's random cells (qp_wormhole_inputs.zk_randomness).   */
 int qp_wormhole_circuit_new(int zero_knowledge, qp_circuit **out);
 void qp_circuit_free(qp_circuit *c);
 /* info[0..6] = degree_bits, num_wires, num_routed_wires, num_constants,
@@ -150,6 +159,7 @@ typedef struct {
     uint32_t num_path_indices;         /* path_indices.len() */
     const uint8_t *path_indices;       /* [num_path_indices], 0 = left, 1 = right */
     uint64_t actual_merkle_depth;
+    const uint64_t *zk_randomness;     /* as in qp_wormhole_inputs */
 } qp_voting_inputs;
 
 /* VoteTargets::new + VoteCircuitData::circuit + builder.build()

@@ -284,6 +284,12 @@ CircuitData CircuitBuilder::build() {
   auto pih = hash_n_to_hash_no_pad(public_inputs_);
   uint32_t pi_row = add_gate(G_PUBLIC_INPUT);
   for (uint32_t i = 0; i < 4; i++) connect(pih[i], Target::wire(pi_row, i));
+  // randomize_unused_pi_wires: under the zk config the remaining wires of the
+  // PublicInputGate row carry random values; they are inputs of commit() here
+  std::vector<Target> zk_cells;
+  if (cfg_.zero_knowledge)
+    for (uint32_t j = 4; j < cfg_.num_wires; j++) zk_cells.push_back(Target::wire(pi_row, j));
+  mark_inputs(zk_cells);
   // constant gates: cfg.num_constants constants per ConstantGate row, in
   // ascending canonical value (plonky2 build(): constants_to_targets
   // .sorted_by_key(|(c, _)| c.to_canonical_u64()) zipped with the generators)
@@ -311,6 +317,7 @@ CircuitData CircuitBuilder::build() {
   cd.degree_bits = 0;
   while ((1u << cd.degree_bits) < n) cd.degree_bits++;
   cd.rows = rows_;
+  cd.pi_row = pi_row;
   cd.quotient_degree_factor = cfg_.max_quotient_degree_factor;
   cd.num_public_inputs = (uint32_t)public_inputs_.size();
   // gate set in common-data order (degree, id string)
@@ -538,6 +545,7 @@ CircuitData CircuitBuilder::build() {
       }
     }
     for (Target t : public_inputs_) cd.pi_slots.push_back(sid[pt(t)]);
+    for (Target t : zk_cells) cd.zk_slots.push_back(sid[pt(t)]);
     // device schedule: a generator runs at the first level where all its
     // inputs exist; its outputs exist from the next level on
     {

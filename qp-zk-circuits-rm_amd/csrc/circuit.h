@@ -124,6 +124,12 @@ struct CircuitData {
   std::vector<uint32_t> virt_slot;      // virtual target index -> slot
   uint32_t zero_const_slot = 0;         // slot of builder.zero() (0 if the circuit has none)
   std::vector<uint32_t> input_slots;    // distinct slots of the targets commit() sets
+  // zk config: the PublicInputGate row's unused wires 4..num_wires-1, which
+  // plonky2's build() hands to RandomValueGenerators (randomize_unused_pi_wires,
+  // plonk/circuit_builder.rs).  Here they are commit() inputs (zk randomness is an
+  // ABI input, so a proof is a pure function of its inputs); empty if not zk
+  std::vector<uint32_t> zk_slots;
+  uint32_t pi_row = 0;
   std::vector<DevGen> dev_gens;         // generators ordered by dependency level
   std::vector<uint32_t> level_off;      // [levels + 1] offsets into dev_gens
   // commitments (filled by the prover backend at setup)

@@ -9,6 +9,51 @@
 #include "circuit_obj.h"
 #include "host_util.h"
 
+// zk config: the PublicInputGate row's unused wires (plonky2 randomize_unused_pi_wires
+// -> RandomValueGenerator).  `given` holds num_wires - 4 canonical values; when it is
+// null they are derived as hash_n_to_m_no_pad(domain tag || private felts): a
+// deterministic nonce that hides like fresh randomness while the private inputs
+// stay secret, so the proof remains a pure function of the inputs.
+static std::string zk_fill(const qc::CircuitData &cd, const uint64_t *given, const std::vector<uint64_t> &priv,
+                           qc::Witness &w, int *code) {
+  *code = QP_ERR_ARG;
+  const size_t m = cd.zk_slots.size();
+  if (!m) return given ? "zk randomness given for a circuit built without zero_knowledge" : "";
+  std::vector<uint64_t> v(m);
+  if (given) {
+    for (size_t i = 0; i < m; i++) {
+      if (given[i] >= gl::P) return "zk randomness value " + std::to_string(i) + " is not a canonical field element";
+      v[i] = given[i];
+    }
+  } else {
+    std::vector<uint64_t> in = {0x6b7a2d626c696e64ull % gl::P /* "zk-blind" */, (uint64_t)m};
+    in.insert(in.end(), priv.begin(), priv.end());
+    uint64_t st[12] = {0};
+    for (size_t off = 0; off < in.size(); off += 8) {
+      for (size_t i = 0; i < 8 && off + i < in.size(); i++) st[i] = gl::canon(in[off + i]);
+      ps::permute(st);
+    }
+    for (size_t i = 0; i < m; i++) {
+      if (i && i % 8 == 0) ps::permute(st);
+      v[i] = st[i % 8];
+    }
+  }
+  for (size_t i = 0; i < m; i++)
+    if (!w.set_slot(cd.zk_slots[i], v[i])) {
+      *code = QP_ERR_WITNESS;
+      return "Partition containing a target was set twice with different values";
+    }
+  *code = QP_OK;
+  return "";
+}
+
+static std::vector<uint64_t> bytes_as_u32_felts(const uint8_t *b, size_t n) {
+  std::vector<uint64_t> v;
+  for (size_t i = 0; i + 4 <= n; i += 4) v.push_back((uint64_t)b[i] | (uint64_t)b[i + 1] << 8 |
+                                                     (uint64_t)b[i + 2] << 16 | (uint64_t)b[i + 3] << 24);
+  return v;
+}
+
 std::string wormhole_fill(const qp_circuit *c, const void *vin, qc::Witness &w, int *code) {
   const qp_wormhole_inputs *in = (const qp_wormhole_inputs *)vin;
   *code = QP_ERR_ARG;
@@ -30,7 +75,13 @@ std::string wormhole_fill(const qp_circuit *c, const void *vin, qc::Witness &w, 
   }
   std::string e = qw::commit(c->wormhole, ci, w);
   *code = e.empty() ? QP_OK : e.find("set twice") != std::string::npos ? QP_ERR_WITNESS : QP_ERR_ARG;
-  return e;
+  if (!e.empty()) return e;
+  std::vector<uint64_t> priv = bytes_as_u32_felts(in->secret, 32);
+  for (const uint8_t *f : {in->funding_account, in->unspendable_account, in->nullifier, in->root_hash})
+    for (uint64_t x : bytes_as_u32_felts(f, 32)) priv.push_back(x);
+  priv.push_back(in->transfer_count & 0xFFFFFFFFu);
+  priv.push_back(in->transfer_count >> 32);
+  return zk_fill(c->cd, in->zk_randomness, priv, w, code);
 }
 
 std::string voting_fill(const qp_circuit *c, const void *vin, qc::Witness &w, int *code) {
@@ -51,7 +102,11 @@ std::string voting_fill(const qp_circuit *c, const void *vin, qc::Witness &w, in
   vi.actual_merkle_depth = in->actual_merkle_depth;
   std::string e = qv::fill_targets(c->voting, vi, w);
   *code = e.empty() ? QP_OK : QP_ERR_ARG;
-  return e;
+  if (!e.empty()) return e;
+  std::vector<uint64_t> priv(in->private_key, in->private_key + 4);
+  priv.insert(priv.end(), in->proposal_id, in->proposal_id + 4);
+  priv.push_back(in->vote != 0);
+  return zk_fill(c->cd, in->zk_randomness, priv, w, code);
 }
 
 extern "C" {

@@ -11,7 +11,7 @@ result of WormholeProver::commit (wormhole/prover/src/lib.rs:209-225).
 """
 import ctypes
 from dataclasses import dataclass, field
-from typing import List
+from typing import List, Optional
 
 import numpy as np
 
@@ -25,7 +25,7 @@ class _Inputs(ctypes.Structure):
                 ("exit_account", U8_32), ("secret", U8_32), ("transfer_count", ctypes.c_uint64),
                 ("funding_account", U8_32), ("unspendable_account", U8_32), ("num_nodes", ctypes.c_uint32),
                 ("nodes", ctypes.POINTER(ctypes.c_char_p)), ("node_lens", ctypes.POINTER(ctypes.c_uint32)),
-                ("indices", ctypes.POINTER(ctypes.c_uint64))]
+                ("indices", ctypes.POINTER(ctypes.c_uint64)), ("zk_randomness", ctypes.POINTER(ctypes.c_uint64))]
 
 
 @dataclass
@@ -61,6 +61,8 @@ class PrivateCircuitInputs:
 class CircuitInputs:
     public: PublicCircuitInputs
     private: PrivateCircuitInputs
+    # zk config only: the random cells of the PublicInputGate row (see _zk_ptr)
+    zk_randomness: Optional[List[int]] = None
 
     def to_c(self):
         s = _Inputs()
@@ -80,7 +82,8 @@ class CircuitInputs:
         s.nodes = (ctypes.c_char_p * max(n, 1))(*keep) if n else None
         s.node_lens = (ctypes.c_uint32 * max(n, 1))(*[len(p) for p in keep]) if n else None
         s.indices = (ctypes.c_uint64 * max(len(sp.indices), 1))(*sp.indices) if n else None
-        s._keep = keep
+        s.zk_randomness, zk_keep = _zk_ptr(self.zk_randomness)
+        s._keep = (keep, zk_keep)
         return s
 
 
@@ -91,7 +94,18 @@ class _VoteInputs(ctypes.Structure):
     _fields_ = [("proposal_id", U64_4), ("merkle_root", U64_4), ("nullifier", U64_4), ("vote", ctypes.c_uint8),
                 ("private_key", U64_4), ("num_siblings", ctypes.c_uint32),
                 ("siblings", ctypes.POINTER(ctypes.c_uint64)), ("num_path_indices", ctypes.c_uint32),
-                ("path_indices", ctypes.POINTER(ctypes.c_uint8)), ("actual_merkle_depth", ctypes.c_uint64)]
+                ("path_indices", ctypes.POINTER(ctypes.c_uint8)), ("actual_merkle_depth", ctypes.c_uint64),
+                ("zk_randomness", ctypes.POINTER(ctypes.c_uint64))]
+
+
+def _zk_ptr(values):
+    """zk config: values of the PublicInputGate row's unused wires (num_wires - 4
+    felts; plonky2 randomize_unused_pi_wires).  None = derived from the private
+    inputs by the library (deterministic Poseidon nonce)."""
+    if values is None:
+        return None, None
+    keep = (ctypes.c_uint64 * len(values))(*[int(v) for v in values])
+    return ctypes.cast(keep, ctypes.POINTER(ctypes.c_uint64)), keep
 
 
 @dataclass
@@ -117,6 +131,7 @@ class VoteCircuitData:
     """voting/src/lib.rs:113-121: the witness data fill_targets consumes."""
     public_inputs: VotePublicInputs
     private_inputs: VotePrivateInputs
+    zk_randomness: Optional[List[int]] = None
 
     def to_c(self):
         s = _VoteInputs()
@@ -134,7 +149,8 @@ class VoteCircuitData:
         keep_p = (ctypes.c_uint8 * max(len(prv.path_indices), 1))(*[1 if b else 0 for b in prv.path_indices])
         s.path_indices = ctypes.cast(keep_p, ctypes.POINTER(ctypes.c_uint8))
         s.actual_merkle_depth = prv.actual_merkle_depth
-        s._keep = (keep_s, keep_p)
+        s.zk_randomness, zk_keep = _zk_ptr(self.zk_randomness)
+        s._keep = (keep_s, keep_p, zk_keep)
         return s
 
 

@@ -77,10 +77,14 @@ def test_voting_device_witness():
 
 def test_zk_config_proves():
     """standard_recursion_zk_config (the reference prover's default, circuit.rs:68-73):
-    under `no_random` it has the non-zk preprocessing and proof shape
-    (tests/test_current_circuit_fixture.py), so its proofs verify under its own
-    verifier data and carry the same bytes as the non-zk config's."""
+    same preprocessing and proof shape as the non-zk config (the reference's
+    fixture pair, tests/test_zk.py), plus the PublicInputGate row's random cells.
+    With the same cells the device-witness path, the host-witness path and the
+    oracle prover give the same bytes; other cells give another wires cap, as the
+    reference's zk and non-zk proofs of the same inputs do."""
+    import dataclasses
     import qp_wormhole
+    from qp_wormhole.synthetic import synthetic_inputs
     from test_oracle_golden import current_common_bytes
     zk = qp_wormhole.WormholeProver("standard_recursion_zk_config")
     nz = qp_wormhole.WormholeProver("standard_recursion_config")
@@ -90,8 +94,21 @@ def test_zk_config_proves():
     cb = bytearray(current_common_bytes())
     cb[49] = 1
     assert vd.endswith(bytes(cb))
-    assert verify(vd, a) == 0
-    assert a == b
+    assert verify(vd, a) == 0 and verify(nz.prover.verifier_data(), b) == 0
+    assert a[:512] != b[:512]                    # wires caps differ, as in the fixture pair
+    assert a[-8 * 17:] == b[-8 * 17:]            # same public inputs
+    circ, prover = zk.circuit, zk.prover
+    r = [(0x9e3779b97f4a7c15 * (i + 3)) % 0xFFFFFFFF00000001 for i in range(circ.num_wires - 4)]
+    inputs = [dataclasses.replace(WI.test_inputs(), zk_randomness=r),
+              dataclasses.replace(synthetic_inputs(31, 2), zk_randomness=r[::-1]), synthetic_inputs(32, 0)]
+    dev = prover.prove_inputs(inputs)
+    host = prover.prove_witnesses([circ.commit(x) for x in inputs])
+    assert dev == host
+    w = circ.commit(inputs[0])
+    ob, ovd = oracle_prove(circ, w.wires(), w.public_inputs())
+    assert dev[0] == ob and ovd == vd
+    assert dev[0][:512] != a[:512]               # other random cells, other wires cap
+    assert all(verify(vd, p) == 0 for p in dev)
 
 
 def test_batch_256_two_provers():

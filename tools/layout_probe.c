@@ -180,3 +180,17 @@ long lp_shift_scan(const gl_t *target, const gl_t *xs, size_t nx, unsigned log_n
     free(pre0); free(suf); free(lag);
     return (long)nh;
 }
+
+/* out[k*ncols + c] = sum_r L[k*n + r] * vals[c*n + r]  (column evaluation at nx points) */
+void lp_matvec(const gl_t *L, size_t nx, size_t n, const gl_t *vals, size_t ncols, gl_t *out) {
+    for (size_t c = 0; c < ncols; c++) {
+        const gl_t *v = vals + c * n;
+        for (size_t k = 0; k < nx; k++) {
+            const gl_t *l = L + k * n;
+            gl_t t = 0;
+            for (size_t r = 0; r < n; r++)
+                if (v[r]) t = gl_add(t, gl_mul(v[r], l[r]));
+            out[k * ncols + c] = t;
+        }
+    }
+}
