@@ -24,7 +24,6 @@ import ctypes
 import json
 import os
 import sys
-import threading
 import time
 
 import numpy as np
@@ -83,6 +82,9 @@ def parse():
     ap.add_argument("--no-pipeline", dest="pipeline", action="store_false",
                     help="join the prover threads after every step (default: each prover runs its share of all "
                          "steps back to back)")
+    ap.add_argument("--host-threads", type=int, default=-1,
+                    help="host threads per prover (caller included); -1 = split the process's cores "
+                         "(OMP_NUM_THREADS, else min(cores, 16)) between the provers; 0 = library default")
     ap.add_argument("--cpu-sample", type=int, default=2, help="min proofs in the CPU baseline sample (0 = skip)")
     ap.add_argument("--cpu-seconds", type=float, default=10.0, help="min seconds of CPU baseline proving")
     return ap.parse_args()
@@ -159,6 +161,11 @@ def main():
     first = [sum(per[:i]) for i in range(NP)]
     provers = [qp_wormhole.Prover(qp_wormhole.Context(local), circuit, max_batch=per[i]) for i in range(NP)]
     prover = provers[0]
+    budget = int(os.environ.get("OMP_NUM_THREADS") or min(os.cpu_count() or 4, 16))
+    host_threads = max(2, budget // NP) if args.host_threads < 0 else args.host_threads
+    if host_threads:
+        for p in provers:
+            p.set_host_threads(host_threads)
     # the API input marshalled once into C-ABI structs (CircuitInputs -> qp_wormhole_inputs)
     cin = [prover.inputs_array(inputs[first[i]:first[i] + per[i]]) for i in range(NP)]
     # prove-only comparison path: wire matrices resident in HBM (host-generated)
@@ -169,63 +176,20 @@ def main():
     wstride = wires[0].nbytes if wires is not None else 0
     torch.cuda.synchronize()
 
-    from qp_wormhole.distributed import gather_proofs
+    from qp_wormhole.distributed import run_steps
 
-    def prove_all():
-        out = [None] * NP
+    def prove_share(i):
+        if args.mode == "e2e":
+            return provers[i].prove_inputs_array(cin[i], per[i])
+        return provers[i].prove_wires_dev(d_wires.data_ptr() + first[i] * wstride,
+                                          pis[first[i]:first[i] + per[i]], per[i])
 
-        def run(i):
-            if args.mode == "e2e":
-                out[i] = provers[i].prove_inputs_array(cin[i], per[i])
-            else:
-                out[i] = provers[i].prove_wires_dev(d_wires.data_ptr() + first[i] * wstride,
-                                                    pis[first[i]:first[i] + per[i]], per[i])
-        if NP == 1:
-            run(0)
-        else:
-            th = [threading.Thread(target=run, args=(i,)) for i in range(NP)]
-            for t in th:
-                t.start()
-            for t in th:
-                t.join()
-        if any(o is None for o in out):
-            raise RuntimeError("a prover thread failed")
-        return [p for o in out for p in o]
+    def steps(k, pipelined):
+        # leaf proofs -> aggregator rank over RCCL (raw gather) after every step
+        return run_steps(prove_share, NP, k, dist=dist, slot=prover.proof_size, device=f"cuda:{local}",
+                         pipelined=pipelined)
 
-    def step():
-        proofs = prove_all()
-        if dist is not None:  # leaf proofs -> aggregator rank over RCCL
-            gather_proofs(proofs, prover.proof_size, dist, device=f"cuda:{local}", raw=True)
-        return proofs
-
-    def steps_pipelined(k):
-        """k steps with each prover thread running its share of every step
-        back to back (no join between steps, so no prover idles the GPU while
-        the slowest finishes a step); the steps' leaf proofs are then gathered
-        step by step.  Same work as k calls of step()."""
-        outs = [[None] * k for _ in range(NP)]
-
-        def run(i):
-            for s in range(k):
-                if args.mode == "e2e":
-                    outs[i][s] = provers[i].prove_inputs_array(cin[i], per[i])
-                else:
-                    outs[i][s] = provers[i].prove_wires_dev(d_wires.data_ptr() + first[i] * wstride,
-                                                            pis[first[i]:first[i] + per[i]], per[i])
-        th = [threading.Thread(target=run, args=(i,)) for i in range(NP)]
-        for t in th:
-            t.start()
-        for t in th:
-            t.join()
-        if any(o is None for row in outs for o in row):
-            raise RuntimeError("a prover thread failed")
-        for s in range(k):
-            proofs = [p for i in range(NP) for p in outs[i][s]]
-            if dist is not None:
-                gather_proofs(proofs, prover.proof_size, dist, device=f"cuda:{local}", raw=True)
-
-    for _ in range(args.warmup):
-        proofs = step()
+    proofs = steps(args.warmup, False) if args.warmup else None
     # proofs of the warmup verify (rank 0 checks the first and last with the oracle verifier)
     verified = None
     if rank == 0 and args.warmup:
@@ -240,11 +204,7 @@ def main():
         dist.barrier()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
-    if args.pipeline and NP > 1:
-        steps_pipelined(args.steps)
-    else:
-        for _ in range(args.steps):
-            step()
+    steps(args.steps, args.pipeline)
     torch.cuda.synchronize()
     if dist is not None:
         dist.barrier()
@@ -326,7 +286,7 @@ def main():
                                                       "prove() from HBM-resident wire matrices"),
             "config": {"workload": f"batch{B}_{circuit.kind}_proofs_per_gpu",
                        "circuit": f"{circuit.kind} deg{circuit.degree_bits} (135 wires)",
-                       "batch_per_gpu": B, "provers_per_gpu": NP,
+                       "batch_per_gpu": B, "provers_per_gpu": NP, "host_threads_per_prover": host_threads,
                        "step_schedule": "pipelined" if (args.pipeline and NP > 1) else "joined per step",
                        "parallelism": f"proofs sharded x{world}, RCCL gather of leaf proofs"},
             "roofline": {"kernel": f"k_lde (wires LDE, 135 cols x 2^{circuit.degree_bits} -> "
@@ -350,7 +310,7 @@ def main():
                              if circuit.degree_bits == 13 else None,
                              "quotient_algorithmic_bytes_per_launch": per[0] * 8 * 243 * (8 << circuit.degree_bits)},
             "stage_ms_per_step": {k: v / args.steps for k, v in stages.items()},
-            "proof_bytes": len(proofs[0]),
+            "proof_bytes": prover.proof_size,
             "latency_1proof_ms": lat,
             "zk_config": zk,
             "prove_only_1prover_proofs_per_s": prove_only,

@@ -219,6 +219,10 @@ int qp_prover_prove_wires_dev(qp_prover *p, const uint64_t *d_wires, const uint6
  * 1 = wires leaf hashing (units = permutations), 2 = wires Merkle levels
  * (units = permutations), 3 = quotient evaluation (units = LDE points)     */
 int qp_prover_set_timing(qp_prover *p, int enable);
+/* host threads (the caller included) of the prover's pool for commit() and the
+ * per-proof host stages; default min(hardware threads, 16).  Several provers in
+ * one process should split the host cores (cores / provers each).           */
+int qp_prover_set_host_threads(qp_prover *p, uint32_t nthreads);
 int qp_prover_kernel_stats(qp_prover *p, double *ms, double *units, uint64_t *launches, uint32_t n, int reset);
 /* accumulated host wall time per stage (ms): [0] commit wires, [1] zs, [2] quotient,
  * [3] openings, [4] FRI, [5] PoW, [6] queries, [7] serialize, [8] commit() of the
@@ -227,11 +231,18 @@ int qp_prover_stage_times(qp_prover *p, double *ms, uint32_t n, int reset);
 
 /* ---- routine-level seams ---------------------------------
  * The pieces of plonky2's prove() (qp-plonky2 1.1.1 plonk/prover.rs,
- * fri/prover.rs) a patched crate routes to the GPU for ANY circuit over the
- * supported gate set — e.g. the aggregator's per-chunk circuits
- * (wormhole/aggregator/src/circuits/tree.rs:127-136), which the built-in
- * circuit path does not cover.  The Fiat-Shamir transcript stays with the
- * caller (INTEGRATION.md shows the call sequence).                            */
+ * fri/prover.rs) a patched crate routes to the GPU for any circuit over the
+ * supported gate set within the shape limits below — e.g. the aggregator's
+ * per-chunk circuits (wormhole/aggregator/src/circuits/tree.rs:127-136).  The
+ * Fiat-Shamir transcript stays with the caller (INTEGRATION.md shows the call
+ * sequence).
+ *
+ * Shape limits (a call outside them returns QP_ERR_ARG with the reason in the
+ * context's last error, never a wrong result): LDE domains up to 2^16 points
+ * (log_n + rate_bits <= 16, i.e. circuits up to degree 2^13 at rate 3);
+ * qp_quotient: 2 challenges, quotient_degree_factor == 2^rate_bits <= 16, at
+ * most 16 gates, unsalted batches of one; qp_fri_layer_commit: at most 2^13
+ * nonzero coefficients.                                                     */
 
 /* gate kinds of CommonCircuitData.gates (DefaultGateSerializer ids in brackets).
  * 0-5: the leaf circuits' gates (fast single-read quotient kernel); 6-13: the

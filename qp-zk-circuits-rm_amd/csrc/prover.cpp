@@ -400,6 +400,15 @@ int setup(qp_prover *P) {
   return QP_OK;
 }
 
+// host threads of this prover's commit()/query pool, the calling thread
+// included: several provers in one process split the host cores between them
+// (qp_prover_set_host_threads(p, cores / provers)) instead of each taking all
+extern "C" int qp_prover_set_host_threads(qp_prover *P, uint32_t nthreads) {
+  if (!P || nthreads == 0 || nthreads > 256) return QP_ERR_ARG;
+  P->pool.reset(new qh::ThreadPool(nthreads - 1));
+  return QP_OK;
+}
+
 // kernel timers: 0 = LDE of the wires (NTT), 1 = leaf hashing of the wires,
 // 2 = Merkle tree levels of the wires, 3 = quotient evaluation
 void kt_begin(qp_prover *P, int k) {

@@ -51,17 +51,28 @@ __global__ void k_witness_inputs(uint64_t *vals, uint64_t v_bstride, const uint3
   if (i < nin) vals[(uint64_t)b * v_bstride + in_slots[i]] = in_vals[(uint64_t)b * nin + i];
 }
 
+// a generator input still UNSET means a scheduling bug or a missing input: the
+// generator fails (reported like a conflict) instead of computing on 2^64-1
+__device__ __forceinline__ uint64_t rd(const uint64_t *v, uint32_t s, bool &ok) {
+  const uint64_t x = v[s];
+  ok &= x != UNSET;
+  return x;
+}
+
 __device__ bool run_gen(const DevGenD &g, uint64_t *v, const uint32_t *wslot, uint32_t W, uint32_t limbs,
                         uint32_t zslot, uint32_t num_consts) {
+  bool in_ok = true;
   switch (g.kind) {
     case WG_CONSTANT:
       return wset(v, g.s[0], g.k0) && (num_consts < 2 || wset(v, g.s[1], g.k1));
     case WG_ARITH: {
-      const uint64_t m = gl::mul(gl::mul(v[g.s[0]], v[g.s[1]]), g.k0);
-      return wset(v, g.s[3], gl::add(m, gl::mul(v[g.s[2]], g.k1)));
+      const uint64_t m = gl::mul(gl::mul(rd(v, g.s[0], in_ok), rd(v, g.s[1], in_ok)), g.k0);
+      const uint64_t a = rd(v, g.s[2], in_ok);
+      return in_ok && wset(v, g.s[3], gl::add(m, gl::mul(a, g.k1)));
     }
     case WG_BASE_SPLIT: {
-      const uint64_t sum = v[g.s[0]];
+      const uint64_t sum = rd(v, g.s[0], in_ok);
+      if (!in_ok) return false;
       const uint32_t *ws = wslot + (uint64_t)g.row * W + 1;
       bool ok = true;
       for (uint32_t l = 0; l < limbs; l++) {
@@ -72,7 +83,8 @@ __device__ bool run_gen(const DevGenD &g, uint64_t *v, const uint32_t *wslot, ui
       return ok;
     }
     case WG_EQUALITY: {
-      const uint64_t x = v[g.s[0]], y = v[g.s[1]];
+      const uint64_t x = rd(v, g.s[0], in_ok), y = rd(v, g.s[1], in_ok);
+      if (!in_ok) return false;
       const bool eq = x == y;
       return wset(v, g.s[2], eq ? 1 : 0) && wset(v, g.s[3], eq ? 0 : gl::inv(gl::sub(x, y)));
     }
@@ -80,8 +92,9 @@ __device__ bool run_gen(const DevGenD &g, uint64_t *v, const uint32_t *wslot, ui
       // PoseidonGenerator (gates/poseidon.rs), wire layout SURVEY.md A.5
       const uint32_t *ws = wslot + (uint64_t)g.row * W;
       uint64_t s[12];
-      for (int i = 0; i < 12; i++) s[i] = v[ws[i]];
-      const uint64_t swap = v[ws[24]];
+      for (int i = 0; i < 12; i++) s[i] = rd(v, ws[i], in_ok);
+      const uint64_t swap = rd(v, ws[24], in_ok);
+      if (!in_ok) return false;
       bool ok = true;
       for (int i = 0; i < 4; i++) ok &= wset(v, ws[25 + i], gl::mul(swap, gl::sub(s[i + 4], s[i])));
       if (swap == 1)

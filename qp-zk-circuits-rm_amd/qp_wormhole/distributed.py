@@ -52,11 +52,15 @@ def gather_proofs(proofs, slot: int, dist, device="cpu", dst: int = 0, raw: bool
     reading the packed buffer needs; no per-proof host copies)."""
     import torch
     rank, world = dist.get_rank(), dist.get_world_size()
-    if any(len(p) == 0 for p in proofs):
-        raise ValueError("empty proof")
-    cnt = torch.tensor([len(proofs)], dtype=torch.int64, device=device)
+    # a bad shard is reported through the count exchange (-1), so every rank
+    # raises the same error instead of its peers blocking in the gather
+    bad = any(len(p) == 0 or len(p) > slot for p in proofs)
+    cnt = torch.tensor([-1 if bad else len(proofs)], dtype=torch.int64, device=device)
     counts = [torch.zeros_like(cnt) for _ in range(world)]
     dist.all_gather(counts, cnt)
+    bad_ranks = [r for r, c in enumerate(counts) if int(c.item()) < 0]
+    if bad_ranks:
+        raise ValueError(f"empty or oversized proof in the shard of rank(s) {bad_ranks}")
     most = int(max(int(c.item()) for c in counts))
     t = torch.from_numpy(pack_proofs(list(proofs) + [b""] * (most - len(proofs)), slot)).to(device)
     bufs = [torch.empty_like(t) for _ in range(world)] if rank == dst else None
@@ -69,3 +73,59 @@ def gather_proofs(proofs, slot: int, dist, device="cpu", dst: int = 0, raw: bool
     for b in bufs:
         out.extend(p for p in unpack_proofs(b.cpu().numpy()) if p)
     return out
+
+
+def run_steps(prove_share, nprovers, steps, dist=None, slot=0, device="cpu", pipelined=True, on_leaves=None):
+    """bench.py's timed loop: `steps` steps of every prover's share of the batch,
+    then each step's leaf proofs to rank 0 (the aggregator's input).
+
+    prove_share(i) -> list of serialized proofs: prover i's share of one step
+    (its own HIP stream and host thread).  pipelined: each prover thread runs
+    its share of ALL steps back to back (no prover idles the GPU while the
+    slowest finishes a step) and the K per-step gathers follow; otherwise the
+    threads are joined after every step.  With dist (world > 1) every step's
+    proofs are gathered in raw mode (gather_proofs); on_leaves(step, result)
+    receives, on rank 0, the gathered (buffers, counts) -- or the step's local
+    proofs when dist is None.  Returns the last step's local proofs."""
+    import threading
+    outs = [[None] * steps for _ in range(nprovers)]
+    errors = []
+
+    def run(i, ks):
+        try:
+            for s in ks:
+                outs[i][s] = prove_share(i)
+        except BaseException as e:  # surfaced on the calling thread
+            errors.append(e)
+
+    def launch(ks):
+        if nprovers == 1:
+            run(0, ks)
+        else:
+            th = [threading.Thread(target=run, args=(i, ks)) for i in range(nprovers)]
+            for t in th:
+                t.start()
+            for t in th:
+                t.join()
+        if errors:
+            raise RuntimeError("a prover thread failed") from errors[0]
+
+    def finish(s):
+        proofs = [p for i in range(nprovers) for p in outs[i][s]]
+        res = proofs
+        if dist is not None:
+            res = gather_proofs(proofs, slot, dist, device=device, raw=True)
+        if on_leaves is not None and (dist is None or dist.get_rank() == 0):
+            on_leaves(s, res)
+        return proofs
+
+    last = None
+    if pipelined and nprovers > 1:
+        launch(range(steps))
+        for s in range(steps):
+            last = finish(s)
+    else:
+        for s in range(steps):
+            launch([s])
+            last = finish(s)
+    return last

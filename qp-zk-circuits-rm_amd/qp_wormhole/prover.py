@@ -12,6 +12,7 @@ import hashlib
 import os
 import struct
 import threading
+import warnings
 
 import numpy as np
 
@@ -108,6 +109,11 @@ class Prover:
     def set_timing(self, enable=True):
         lib().qp_prover_set_timing(self.h, int(enable))
 
+    def set_host_threads(self, nthreads):
+        """Host threads (caller included) of this prover's pool: several provers in
+        one process split the host cores instead of each taking min(cores, 16)."""
+        self.ctx.check(lib().qp_prover_set_host_threads(self.h, int(nthreads)), "qp_prover_set_host_threads")
+
     def kernel_stats(self, reset=False):
         ms = (ctypes.c_double * 8)()
         units = (ctypes.c_double * 8)()
@@ -168,10 +174,22 @@ PROVER_VERSION = 1
 _KINDS = {"wormhole": 0, "voting": 1}
 
 
+_common_memo = {}
+
+
+def _common_of(cfg):
+    """CommonCircuitData bytes of the native Wormhole circuit for a config (memoised:
+    building the degree-13 circuit takes ~0.3 s)."""
+    with _lock:
+        if cfg not in _common_memo:
+            _common_memo[cfg] = Circuit.wormhole(zero_knowledge=(cfg == CONFIGS[1])).common_data()
+        return _common_memo[cfg]
+
+
 def _config_of_common(common_bytes):
     """The Wormhole circuit config whose CommonCircuitData::to_bytes equals common_bytes."""
     for cfg in CONFIGS:
-        if Circuit.wormhole(zero_knowledge=(cfg == CONFIGS[1])).common_data() == bytes(common_bytes):
+        if _common_of(cfg) == bytes(common_bytes):
             return cfg
     return None
 
@@ -197,7 +215,9 @@ def _parse_prover_only(data, common_bytes):
     data = bytes(data)
     n = len(PROVER_MAGIC)
     if len(data) < n + 10 + 32 or data[:n] != PROVER_MAGIC:
-        raise ValueError("bad magic")
+        raise ValueError("not this backend's prover.bin (bad magic): an upstream plonky2 "
+                         "ProverOnlyCircuitData::to_bytes file is not supported; regenerate it with "
+                         "generate_circuit_binaries")
     version, kind, zk, degree_bits = struct.unpack_from("<IBBI", data, n)
     if version != PROVER_VERSION:
         raise ValueError(f"unsupported version {version}")
@@ -206,7 +226,30 @@ def _parse_prover_only(data, common_bytes):
     off = n + 10
     if data[off:off + 32] != hashlib.sha256(bytes(common_bytes)).digest():
         raise ValueError("prover data was written for different common data")
+    # the header's config must agree with the common data it was written for
+    # (CommonCircuitData: config.zero_knowledge at byte 49; FriParams.degree_bits
+    # follows the two FriConfigs and the reduction arity list)
+    cb = bytes(common_bytes)
+    if len(cb) > 49 and bool(cb[49]) != bool(zk):
+        raise ValueError("prover data header zk flag disagrees with the common data")
+    c_db = _common_degree_bits(cb)
+    if c_db is not None and c_db != degree_bits:
+        raise ValueError(f"prover data header degree_bits {degree_bits} disagrees with the common data ({c_db})")
     return bool(zk), degree_bits, data[off + 32:]
+
+
+def _common_degree_bits(cb):
+    """FriParams.degree_bits of CommonCircuitData bytes, or None."""
+    try:
+        off = 6 * 8 + 2                      # six u64 config fields, two u8 flags
+        fri = 8 * 3 + 4 + 1 + 16             # FriConfig: rate, cap, queries, pow u32, strategy tag + 2 u64
+        off += fri + fri                     # CircuitConfig.fri_config, FriParams.config
+        (na,) = struct.unpack_from("<Q", cb, off)
+        off += 8 + 8 * na
+        (db,) = struct.unpack_from("<Q", cb, off)
+        return int(db)
+    except struct.error:
+        return None
 
 
 def generate_circuit_binaries(output_dir, include_prover=True, config="standard_recursion_config", device=0):
@@ -279,10 +322,13 @@ class WormholeProver:
     @classmethod
     def default(cls, device=0):
         """WormholeProver::default (lib.rs:81-101): generated-bins/ if loadable, else build."""
+        pb, cb = os.path.join("generated-bins", "prover.bin"), os.path.join("generated-bins", "common.bin")
+        if not (os.path.exists(pb) and os.path.exists(cb)):
+            return cls("standard_recursion_config", device)
         try:
-            return cls.new_from_files(os.path.join("generated-bins", "prover.bin"),
-                                      os.path.join("generated-bins", "common.bin"), device)
-        except (OSError, ValueError):
+            return cls.new_from_files(pb, cb, device)
+        except (OSError, ValueError) as e:
+            warnings.warn(f"WormholeProver::default: ignoring generated-bins ({e}); building the circuit")
             return cls("standard_recursion_config", device)
 
     def commit(self, inputs: CircuitInputs):

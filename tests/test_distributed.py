@@ -133,3 +133,43 @@ def test_gather_real_proofs_verify(world, total):
     """Uneven shards (4 over 3 ranks) gather in order and every proof verifies on rank 0."""
     n, same, ok = _run(_worker_real, world, total)
     assert n == total and all(same) and all(ok)
+
+
+def _worker_steps(rank, world, port, q, pipelined):
+    """bench.py's timed loop (distributed.run_steps) with a stub prover: 3 prover
+    threads per rank, 3 steps; every step's leaf proofs reach rank 0 through
+    the raw gather, in rank/prover order."""
+    import torch.distributed as dist
+
+    from qp_wormhole.distributed import run_steps, unpack_proofs
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    calls = {}
+
+    def prove_share(i):
+        k = calls.get(i, 0)
+        calls[i] = k + 1
+        return [bytes([rank, i, k, j]) * 64 for j in range(2 + i)]
+    got = []
+
+    def on_leaves(s, res):
+        bufs, counts = res
+        got.append((s, counts, [unpack_proofs(b.numpy()) for b in bufs]))
+    last = run_steps(prove_share, 3, 3, dist=dist, slot=256, pipelined=pipelined, on_leaves=on_leaves)
+    if rank == 0:
+        q.put((got, len(last)))
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("pipelined", [True, False])
+def test_bench_step_loop_world2_gloo(pipelined):
+    got, nlast = _run(_worker_steps, 2, pipelined)
+    assert nlast == 2 + 3 + 4
+    assert [s for s, _, _ in got] == [0, 1, 2]
+    for s, counts, rows in got:
+        assert counts == [9, 9]
+        for r in range(2):
+            want = [bytes([r, i, s, j]) * 64 for i in range(3) for j in range(2 + i)]
+            assert rows[r] == want

@@ -35,6 +35,12 @@ for s in "$@"; do
     pmc_fetch) pmc fetch FETCH_SIZE ;;
     pmc_write) pmc write WRITE_SIZE ;;
     pmc_valu) pmc valu SQ_WAVES SQ_INSTS_VALU SQ_WAVE_CYCLES SQ_BUSY_CYCLES ;;
+    pmc_sq) pmc sq SQ_WAVES SQ_INSTS_VALU SQ_ACTIVE_INST_VALU SQ_WAVE_CYCLES SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_BUSY_CYCLES SQ_WAIT_ANY ;;
+    pmc_lds) pmc lds SQ_WAVES SQ_INSTS_LDS SQ_WAIT_INST_LDS SQ_LDS_BANK_CONFLICT SQ_ACTIVE_INST_LDS SQ_WAVE_CYCLES SQ_WAIT_INST_ANY SQ_INSTS_VALU ;;
+    ab_threads) for r in 1 2; do
+             step ab_thr_split_$r 300 python bench.py --cpu-sample 0 --steps 10 &&
+             step ab_thr_def_$r 300 python bench.py --cpu-sample 0 --steps 10 --host-threads 0
+           done ;;
     test_witness) step pytest_witness 600 python -u -m pytest tests/test_gpu_witness.py -x -v --timeout 300 --timeout-method thread ;;
     test_voting) step pytest_voting 300 python -u -m pytest tests/test_gpu_voting.py -x -v --timeout 120 --timeout-method thread ;;
     bench_voting) step bench_voting 600 python bench.py --circuit voting ;;
