@@ -170,6 +170,24 @@ int qp_voting_circuit_new(int zero_knowledge, qp_circuit **out);
  * conflicts (an invalid Merkle proof or nullifier: plonky2's prove() fails)
  * QP_ERR_WITNESS, both with the reference's message in err.               */
 int qp_voting_commit(const qp_circuit *c, const qp_voting_inputs *in, qp_witness **out, char *err, size_t errcap);
+/* ---- recursive aggregation (wormhole/aggregator/src/circuits/tree.rs) -----
+ * aggregate_chunk's circuit (tree.rs:106-127): a native recursive verifier
+ * (plonky2 verify_proof: in-circuit challenger, vanishing polynomial at zeta,
+ * FRI with Merkle paths to the caps, coset interpolation, PoW) of nproofs
+ * proofs of the circuit whose CommonCircuitData bytes are inner_common (this
+ * library's leaf or aggregation circuits), their public inputs registered in
+ * order.  The circuit's witness generators run on the host (commit below);
+ * prove it with qp_prover_new / qp_prover_prove like any other circuit.    */
+int qp_aggregation_circuit_new(const uint8_t *inner_common, size_t len, uint32_t nproofs, qp_circuit **out);
+/* aggregate_chunk's witness (tree.rs:129-134): verifier_only =
+ * VerifierOnlyCircuitData bytes of the inner circuit (cap height u64, cap,
+ * circuit digest), proofs = nproofs serialized ProofWithPublicInputs.  An
+ * invalid inner proof fails witness generation (QP_ERR_WITNESS), as plonky2's
+ * prove() of the aggregation circuit fails.  zk_randomness: as in
+ * qp_wormhole_inputs (NULL: derived from the inner proofs).                 */
+int qp_aggregation_commit(const qp_circuit *c, const uint8_t *verifier_only, size_t vlen,
+                          const uint8_t *const *proofs, const size_t *lens, uint32_t nproofs,
+                          const uint64_t *zk_randomness, qp_witness **out, char *err, size_t errcap);
 /* full wire matrix, column-major [num_wires][n] */
 int qp_witness_wires(const qp_witness *w, uint64_t *out);
 int qp_witness_public_inputs(const qp_witness *w, uint64_t *out, uint32_t cap, uint32_t *n);

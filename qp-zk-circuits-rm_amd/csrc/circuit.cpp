@@ -29,6 +29,7 @@ static inline int gate_degree(GateKind k) {
     case G_BASE_SUM: return 2;
     case G_ARITHMETIC: return 3;
     case G_POSEIDON: return 7;
+    case G_RANDOM_ACCESS: return RA_BITS + 1;
     default: return 0;
   }
 }
@@ -235,13 +236,22 @@ std::vector<Target> CircuitBuilder::split_le(Target x, uint32_t num_bits) {
   F base = gl::pow(2, L);
   for (size_t i = gates.size(); i-- > 0;) acc = mul_const_add(base, acc, Target::wire(gates[i], 0));
   connect(acc, x);
-  if (k > 1) throw std::runtime_error("split_le: more than one BaseSum gate is not supported");
+  if (k > 1) {
+    // WireSplitGenerator: the integer's L-bit chunks into the gates' sum wires
+    // (with one gate the sum wire is the integer itself)
+    Gen g{};
+    g.kind = GEN_WIRE_SPLIT;
+    g.a = x;
+    g.row = gates[0];
+    g.op = k;
+    gens_.push_back(g);
+  }
   return bits;
 }
 
-std::vector<Target> CircuitBuilder::permute(const std::vector<Target> &state) {
+std::vector<Target> CircuitBuilder::permute_swapped(const std::vector<Target> &state, Target swap) {
   uint32_t row = add_gate(G_POSEIDON);
-  connect(_false(), Target::wire(row, 24));
+  connect(swap, Target::wire(row, 24));
   for (uint32_t i = 0; i < 12; i++) connect(state[i], Target::wire(row, i));
   std::vector<Target> out(12);
   for (uint32_t i = 0; i < 12; i++) out[i] = Target::wire(row, 12 + i);
@@ -256,6 +266,30 @@ std::vector<Target> CircuitBuilder::hash_n_to_hash_no_pad(const std::vector<Targ
     state = permute(state);
   }
   return std::vector<Target>(state.begin(), state.begin() + 4);
+}
+
+std::vector<Target> CircuitBuilder::hash_or_noop(const std::vector<Target> &inputs) {
+  if (inputs.size() > 4) return hash_n_to_hash_no_pad(inputs);
+  std::vector<Target> out(inputs);
+  while (out.size() < 4) out.push_back(zero());
+  return out;
+}
+
+// gadgets/random_access.rs random_access: find_slot over RandomAccessGate copies
+Target CircuitBuilder::random_access(Target index, const std::vector<Target> &v) {
+  if (v.size() != RA_VEC) throw std::runtime_error("random_access: only 16-element vectors are supported");
+  if (ra_open_.second >= RA_COPIES) ra_open_ = {add_gate(G_RANDOM_ACCESS), 0};
+  const uint32_t row = ra_open_.first, copy = ra_open_.second++;
+  Target claimed = add_virtual_target();
+  for (uint32_t i = 0; i < RA_VEC; i++) connect(v[i], Target::wire(row, ra_wire_item(i, copy)));
+  connect(index, Target::wire(row, ra_wire_index(copy)));
+  connect(claimed, Target::wire(row, ra_wire_claimed(copy)));
+  Gen g{};
+  g.kind = GEN_RANDOM_ACCESS;
+  g.row = row;
+  g.op = copy;
+  gens_.push_back(g);
+  return claimed;
 }
 
 // ---------------------------------------------------------------- build
@@ -323,11 +357,15 @@ CircuitData CircuitBuilder::build() {
   // gate set in common-data order (degree, id string)
   bool present[G_NKINDS] = {false};
   for (auto &r : rows_) present[r.kind] = true;
-  const GateKind order[] = {G_NOOP, G_CONSTANT, G_PUBLIC_INPUT, G_BASE_SUM, G_ARITHMETIC, G_POSEIDON};
+  // CommonCircuitData.gates: sorted by (degree, id)
+  const GateKind order[] = {G_NOOP, G_CONSTANT, G_PUBLIC_INPUT, G_BASE_SUM, G_ARITHMETIC, G_RANDOM_ACCESS, G_POSEIDON};
   for (GateKind k : order)
     if (present[k]) {
       cd.gate_kinds.push_back(k);
-      cd.gate_params.push_back(k == G_CONSTANT ? ncg : k == G_BASE_SUM ? base_sum_limbs_ : k == G_ARITHMETIC ? arith_ops_ : 0);
+      cd.gate_params.push_back(k == G_CONSTANT ? ncg : k == G_BASE_SUM ? base_sum_limbs_ : k == G_ARITHMETIC ? arith_ops_
+                               : k == G_RANDOM_ACCESS ? RA_BITS : 0);
+      cd.gate_params2.push_back(k == G_RANDOM_ACCESS ? RA_COPIES : 0);
+      cd.gate_params3.push_back(k == G_RANDOM_ACCESS ? RA_EXTRA : 0);
     }
   const uint32_t num_gates = (uint32_t)cd.gate_kinds.size();
   uint32_t gate_index[G_NKINDS];
@@ -354,14 +392,16 @@ CircuitData CircuitBuilder::build() {
   const uint32_t nsel = (uint32_t)cd.groups.size();
   uint32_t max_gate_consts = 0;
   for (GateKind k : cd.gate_kinds)
-    max_gate_consts = std::max<uint32_t>(max_gate_consts, k == G_CONSTANT ? ncg : k == G_ARITHMETIC ? 2 : 0);
+    max_gate_consts = std::max<uint32_t>(max_gate_consts, k == G_CONSTANT ? ncg : k == G_ARITHMETIC ? 2
+                                                          : k == G_RANDOM_ACCESS ? RA_EXTRA : 0);
   cd.num_constants = nsel + max_gate_consts;
   // constraint count = max over gates
   cd.num_gate_constraints = 0;
   for (uint32_t i = 0; i < num_gates; i++) {
     GateKind k = cd.gate_kinds[i];
     uint32_t c = k == G_CONSTANT ? ncg : k == G_PUBLIC_INPUT ? 4 : k == G_BASE_SUM ? base_sum_limbs_ + 1
-               : k == G_ARITHMETIC ? arith_ops_ : k == G_POSEIDON ? 123 : 0;
+               : k == G_ARITHMETIC ? arith_ops_ : k == G_POSEIDON ? 123
+               : k == G_RANDOM_ACCESS ? RA_COPIES * (RA_BITS + 2) + RA_EXTRA : 0;
     cd.num_gate_constraints = std::max(cd.num_gate_constraints, c);
   }
   // num_partial_products: routed wires in chunks of qdf, minus one
@@ -449,6 +489,21 @@ CircuitData CircuitBuilder::build() {
           gin[gi].push_back(pt(g.b));
           gout[gi].push_back(pt(g.c));
           gout[gi].push_back(pt(g.d));
+          break;
+        case GEN_WIRE_SPLIT:
+          gin[gi].push_back(pt(g.a));
+          for (uint32_t j = 0; j < g.op; j++) gout[gi].push_back(wpt(g.row + j, 0));
+          break;
+        case GEN_EXT_DIV:
+          for (Target t : {g.a, g.b, g.c, g.d}) gin[gi].push_back(pt(t));
+          gout[gi].push_back(pt(g.e));
+          gout[gi].push_back(pt(g.f));
+          break;
+        case GEN_RANDOM_ACCESS:
+          gin[gi].push_back(wpt(g.row, ra_wire_index(g.op)));
+          for (uint32_t i = 0; i < RA_VEC; i++) gin[gi].push_back(wpt(g.row, ra_wire_item(i, g.op)));
+          gout[gi].push_back(wpt(g.row, ra_wire_claimed(g.op)));
+          for (uint32_t i = 0; i < RA_BITS; i++) gout[gi].push_back(wpt(g.row, ra_wire_bit(i, g.op)));
           break;
       }
       std::sort(gin[gi].begin(), gin[gi].end());
@@ -540,6 +595,17 @@ CircuitData CircuitBuilder::build() {
         case GEN_BASE_SPLIT:
           g.s[0] = ws(g.row, 0);
           break;
+        case GEN_WIRE_SPLIT:
+          g.s[0] = sid[pt(g.a)];
+          break;
+        case GEN_EXT_DIV:
+          g.s[0] = sid[pt(g.a)];
+          g.s[1] = sid[pt(g.b)];
+          g.s[2] = sid[pt(g.c)];
+          g.s[3] = sid[pt(g.d)];
+          g.s[4] = sid[pt(g.e)];
+          g.s[5] = sid[pt(g.f)];
+          break;
         default:
           break;
       }
@@ -547,8 +613,11 @@ CircuitData CircuitBuilder::build() {
     for (Target t : public_inputs_) cd.pi_slots.push_back(sid[pt(t)]);
     for (Target t : zk_cells) cd.zk_slots.push_back(sid[pt(t)]);
     // device schedule: a generator runs at the first level where all its
-    // inputs exist; its outputs exist from the next level on
-    {
+    // inputs exist; its outputs exist from the next level on (circuits with
+    // host-only generators, e.g. the recursive verifier, have none)
+    for (const Gen &g : cd.schedule)
+      if (g.kind == GEN_WIRE_SPLIT || g.kind == GEN_EXT_DIV || g.kind == GEN_RANDOM_ACCESS) cd.device_witness = false;
+    if (cd.device_witness) {
       std::vector<uint8_t> is_in(nslots, 0);
       for (Target t : inputs_) {
         const uint32_t s = sid[pt(t)];
@@ -685,6 +754,11 @@ std::vector<uint8_t> CircuitData::common_bytes() const {
     w.u32(gate_serial_id(gate_kinds[i]));
     GateKind k = gate_kinds[i];
     if (k == G_CONSTANT || k == G_BASE_SUM || k == G_ARITHMETIC) w.u64(gate_params[i]);
+    if (k == G_RANDOM_ACCESS) {  // RandomAccessGate { bits, num_copies, num_extra_constants }
+      w.u64(gate_params[i]);
+      w.u64(gate_params2[i]);
+      w.u64(gate_params3[i]);
+    }
   }
   return w.b;
 }
@@ -820,6 +894,35 @@ bool Witness::generate(std::string &err) {
       case GEN_EQUALITY: {
         const F x = v[g.s[0]], y = v[g.s[1]];
         ok = set_slot(g.s[2], x == y ? 1 : 0) && set_slot(g.s[3], x == y ? 0 : inv_diff(x, y));
+        break;
+      }
+      case GEN_WIRE_SPLIT: {
+        F x = v[g.s[0]];
+        for (uint32_t j = 0; j < g.op && ok; j++) {
+          const F sum = L < 64 ? (x & ((1ull << L) - 1)) : x;
+          x = L < 64 ? x >> L : 0;
+          ok = set_wire(g.row + j, 0, sum);
+        }
+        break;
+      }
+      case GEN_EXT_DIV: {
+        const gl::ext den{v[g.s[2]], v[g.s[3]]};
+        if (!den.c0 && !den.c1) {
+          err = "division by zero in an extension-field quotient";
+          return false;
+        }
+        const gl::ext q = gl::ext_mul(gl::ext{v[g.s[0]], v[g.s[1]]}, gl::ext_inv(den));
+        ok = set_slot(g.s[4], q.c0) && set_slot(g.s[5], q.c1);
+        break;
+      }
+      case GEN_RANDOM_ACCESS: {
+        const F idx = wire(g.row, ra_wire_index(g.op));
+        if (idx >= RA_VEC) {
+          err = "random access index " + std::to_string(idx) + " out of range";
+          return false;
+        }
+        ok = set_wire(g.row, ra_wire_claimed(g.op), wire(g.row, ra_wire_item((uint32_t)idx, g.op)));
+        for (uint32_t i = 0; i < RA_BITS && ok; i++) ok = set_wire(g.row, ra_wire_bit(i, g.op), (idx >> i) & 1);
         break;
       }
       case GEN_POSEIDON: {

@@ -36,7 +36,20 @@ struct Target {
   bool operator<(const Target &o) const { return v < o.v; }
 };
 
-enum GateKind : uint8_t { G_NOOP = 0, G_CONSTANT, G_PUBLIC_INPUT, G_BASE_SUM, G_ARITHMETIC, G_POSEIDON, G_NKINDS };
+enum GateKind : uint8_t {
+  G_NOOP = 0, G_CONSTANT, G_PUBLIC_INPUT, G_BASE_SUM, G_ARITHMETIC, G_POSEIDON,
+  G_RANDOM_ACCESS,  // RandomAccessGate{bits 4, copies 4, extra constants 2} (the recursive verifier's)
+  G_NKINDS
+};
+
+// RandomAccessGate::new_from_config(standard config, bits = 4) (gates/random_access.rs):
+// per copy c: access index at 18c, claimed element at 18c + 1, list items at
+// 18c + 2 + i; extra-constant wires 72..73; bit i of copy c at 74 + 4c + i
+constexpr uint32_t RA_BITS = 4, RA_VEC = 1u << RA_BITS, RA_COPIES = 4, RA_EXTRA = 2;
+constexpr uint32_t ra_wire_index(uint32_t c) { return (2 + RA_VEC) * c; }
+constexpr uint32_t ra_wire_claimed(uint32_t c) { return (2 + RA_VEC) * c + 1; }
+constexpr uint32_t ra_wire_item(uint32_t i, uint32_t c) { return (2 + RA_VEC) * c + 2 + i; }
+constexpr uint32_t ra_wire_bit(uint32_t i, uint32_t c) { return (2 + RA_VEC) * RA_COPIES + RA_EXTRA + RA_BITS * c + i; }
 
 // plonky2 DefaultGateSerializer ids
 inline uint32_t gate_serial_id(GateKind k) {
@@ -47,6 +60,7 @@ inline uint32_t gate_serial_id(GateKind k) {
     case G_BASE_SUM: return 2;
     case G_ARITHMETIC: return 0;
     case G_POSEIDON: return 11;
+    case G_RANDOM_ACCESS: return 13;
     default: return 0xFFFFFFFF;
   }
 }
@@ -73,15 +87,22 @@ struct GateInst {
 };
 
 // generator record: run by witness generation in schedule order
-enum GenKind : uint8_t { GEN_CONSTANT = 0, GEN_ARITH, GEN_POSEIDON, GEN_BASE_SPLIT, GEN_EQUALITY };
+// (the last three: host witness generation only -- circuits using them, e.g. the
+// recursive verifier, are not device-generated; CircuitData::device_witness)
+enum GenKind : uint8_t {
+  GEN_CONSTANT = 0, GEN_ARITH, GEN_POSEIDON, GEN_BASE_SPLIT, GEN_EQUALITY,
+  GEN_WIRE_SPLIT,     // WireSplitGenerator: integer -> the sums of `op` consecutive BaseSum gates from `row`
+  GEN_EXT_DIV,        // QuotientGeneratorExtension: (e, f) = (a + bX) / (c + dX)
+  GEN_RANDOM_ACCESS,  // RandomAccessGenerator of copy `op` of the RandomAccessGate at `row`
+};
 struct Gen {
   GenKind kind;
   uint32_t row = 0, op = 0;             // gate row / arithmetic op index
-  Target a, b, c, d;                    // EQUALITY: x, y, equal, inv
+  Target a, b, c, d, e, f;              // EQUALITY: x, y, equal, inv; EXT_DIV: num, den, quotient
   // resolved at build(): value slots the generator reads/writes
   //   ARITH: m0, m1, addend, output   EQUALITY: x, y, equal, inv
   //   CONSTANT: wire 0, wire 1         BASE_SPLIT: sum
-  uint32_t s[4] = {0, 0, 0, 0};
+  uint32_t s[6] = {0, 0, 0, 0, 0, 0};
   F k0 = 0, k1 = 0;                     // ARITH / CONSTANT gate constants
 };
 
@@ -105,7 +126,8 @@ struct CircuitData {
   uint32_t num_gate_constraints = 0, quotient_degree_factor = 0, num_partial_products = 0;
   uint32_t num_public_inputs = 0;
   std::vector<GateKind> gate_kinds;     // common-data gate order
-  std::vector<uint32_t> gate_params;    // parameter per gate kind (num_ops / num_limbs / num_consts)
+  std::vector<uint32_t> gate_params;    // parameter per gate kind (num_ops / num_limbs / num_consts / RA bits)
+  std::vector<uint32_t> gate_params2, gate_params3;  // RandomAccess copies, extra constants
   std::vector<uint32_t> selector_indices;
   std::vector<std::pair<uint32_t, uint32_t>> groups;
   std::vector<F> k_is;
@@ -130,6 +152,7 @@ struct CircuitData {
   // ABI input, so a proof is a pure function of its inputs); empty if not zk
   std::vector<uint32_t> zk_slots;
   uint32_t pi_row = 0;
+  bool device_witness = true;           // every generator kind has a device form (witness.hip)
   std::vector<DevGen> dev_gens;         // generators ordered by dependency level
   std::vector<uint32_t> level_off;      // [levels + 1] offsets into dev_gens
   // commitments (filled by the prover backend at setup)
@@ -189,6 +212,15 @@ class CircuitBuilder {
 
   // hash/hashing.rs hash_n_to_m_no_pad (Poseidon, overwrite mode)
   std::vector<Target> hash_n_to_hash_no_pad(const std::vector<Target> &inputs);
+  std::vector<Target> hash_or_noop(const std::vector<Target> &inputs);
+  // PoseidonHash::permute_swapped (hash/poseidon.rs): one PoseidonGate row;
+  // swap = 1 exchanges input lanes 0..3 with 4..7
+  std::vector<Target> permute(const std::vector<Target> &state) { return permute_swapped(state, _false()); }
+  std::vector<Target> permute_swapped(const std::vector<Target> &state, Target swap);
+  // gadgets/random_access.rs: v[index] for |v| = 16 through a RandomAccessGate copy
+  Target random_access(Target index, const std::vector<Target> &v);
+  // a generator the gadget layer creates (GEN_EXT_DIV ...); inputs must be targets
+  void add_generator(const Gen &g) { gens_.push_back(g); }
 
   // targets whose values the caller sets before witness generation (fill_targets)
   void mark_input(Target t) { inputs_.push_back(t); }
@@ -201,8 +233,10 @@ class CircuitBuilder {
 
  private:
   uint32_t add_gate(GateKind k, F c0 = 0, F c1 = 0);
+ public:
   bool as_const(Target t, F &v) const;
-  std::vector<Target> permute(const std::vector<Target> &state);
+
+ private:
 
   CircuitConfig cfg_;
   std::vector<GateInst> rows_;
@@ -215,6 +249,7 @@ class CircuitBuilder {
   std::unordered_map<uint32_t, F> target_to_const_;
   std::map<std::pair<F, F>, std::pair<uint32_t, uint32_t>> arith_open_;  // (c0,c1) -> (row, next op)
   std::map<std::tuple<F, F, uint32_t, uint32_t, uint32_t>, Target> arith_cache_;
+  std::pair<uint32_t, uint32_t> ra_open_{0, RA_COPIES};                  // (row, next copy) of the open RandomAccessGate
   uint32_t arith_ops_, base_sum_limbs_;
 };
 

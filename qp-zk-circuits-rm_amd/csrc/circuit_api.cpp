@@ -151,6 +151,36 @@ int qp_voting_circuit_new(int zk, qp_circuit **out) {
   }
 }
 
+// aggregate_chunk's circuit (wormhole/aggregator/src/circuits/tree.rs:106-127):
+// CircuitBuilder::new(inner config) + add_virtual_verifier_data + nproofs x
+// (add_virtual_proof_with_pis + verify_proof + register_public_inputs) + build
+int qp_aggregation_circuit_new(const uint8_t *inner_common, size_t len, uint32_t nproofs, qp_circuit **out) {
+  if (!out || !inner_common || !nproofs || nproofs > 64) return QP_ERR_ARG;
+  *out = nullptr;
+  try {
+    qr::InnerCommon ic;
+    if (!qr::parse_common(inner_common, len, ic).empty()) return QP_ERR_ARG;
+    qc::CircuitConfig cfg = ic.zero_knowledge ? qc::CircuitConfig::standard_recursion_zk_config()
+                                              : qc::CircuitConfig::standard_recursion_config();
+    if (ic.num_wires != cfg.num_wires || ic.num_routed_wires != cfg.num_routed_wires ||
+        ic.config_num_constants != cfg.num_constants || ic.rate_bits != cfg.rate_bits ||
+        ic.cap_height != cfg.cap_height || ic.num_query_rounds != cfg.num_query_rounds || ic.pow_bits != cfg.pow_bits)
+      return QP_ERR_ARG;
+    auto c = std::make_unique<qp_circuit>();
+    c->kind = qp_circuit::AGGREGATION;
+    qc::CircuitBuilder b(cfg);
+    c->aggregation = qr::build_aggregation(b, ic, nproofs);
+    c->gates_used = (uint32_t)b.num_gates();
+    c->cd = b.build();
+    *out = c.release();
+    return QP_OK;
+  } catch (const std::bad_alloc &) {
+    return QP_ERR_OOM;
+  } catch (const std::exception &) {
+    return QP_ERR_STATE;
+  }
+}
+
 void qp_circuit_free(qp_circuit *c) { delete c; }
 
 int qp_circuit_info(const qp_circuit *c, uint32_t *info) {
@@ -216,6 +246,41 @@ int qp_voting_commit(const qp_circuit *c, const qp_voting_inputs *in, qp_witness
     auto w = std::make_unique<qp_witness>(c);
     int code = QP_OK;
     std::string e = voting_fill(c, in, w->w, &code);
+    if (e.empty() && !w->w.generate(e)) code = QP_ERR_WITNESS;
+    if (!e.empty()) {
+      put_err(err, errcap, e);
+      return code ? code : QP_ERR_ARG;
+    }
+    *out = w.release();
+    return QP_OK;
+  } catch (const std::bad_alloc &) {
+    return QP_ERR_OOM;
+  }
+}
+
+// aggregate_chunk's witness: set_verifier_data_target + set_proof_with_pis_target
+// (tree.rs:129-134), then generation
+int qp_aggregation_commit(const qp_circuit *c, const uint8_t *verifier_only, size_t vlen,
+                          const uint8_t *const *proofs, const size_t *lens, uint32_t nproofs,
+                          const uint64_t *zk_randomness, qp_witness **out, char *err, size_t errcap) {
+  if (!c || !verifier_only || !proofs || !lens || !out || c->kind != qp_circuit::AGGREGATION) return QP_ERR_ARG;
+  *out = nullptr;
+  try {
+    auto w = std::make_unique<qp_witness>(c);
+    std::string e = qr::fill_aggregation(c->aggregation, verifier_only, vlen, proofs, lens, nproofs, w->w);
+    int code = e.empty() ? QP_OK : e.find("set twice") != std::string::npos ? QP_ERR_WITNESS : QP_ERR_ARG;
+    if (e.empty()) {
+      // zk: the PublicInputGate row's random cells; default: a Poseidon nonce
+      // of the inner proofs' wires caps
+      std::vector<uint64_t> priv;
+      for (uint32_t i = 0; i < nproofs; i++)
+        for (size_t k = 0; k < 64 && (k + 1) * 8 <= lens[i]; k++) {
+          uint64_t v;
+          memcpy(&v, proofs[i] + 8 * k, 8);
+          priv.push_back(v);
+        }
+      e = zk_fill(c->cd, zk_randomness, priv, w->w, &code);
+    }
     if (e.empty() && !w->w.generate(e)) code = QP_ERR_WITNESS;
     if (!e.empty()) {
       put_err(err, errcap, e);

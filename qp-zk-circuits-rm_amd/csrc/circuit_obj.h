@@ -2,14 +2,16 @@
 #pragma once
 #include <stdint.h>
 #include "circuit.h"
+#include "recursion.h"
 #include "voting.h"
 #include "wormhole.h"
 
 struct qp_circuit {
-  enum Kind { WORMHOLE = 1, VOTING = 2 } kind = WORMHOLE;
+  enum Kind { WORMHOLE = 1, VOTING = 2, AGGREGATION = 3 } kind = WORMHOLE;
   qc::CircuitData cd;
   qw::WormholeTargets wormhole;
   qv::VoteTargets voting;
+  qr::AggregationTargets aggregation;
   uint32_t gates_used = 0;
 };
 

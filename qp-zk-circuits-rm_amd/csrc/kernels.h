@@ -11,7 +11,7 @@
 
 namespace qpk {
 
-constexpr unsigned TW_LOG = 16;  // twiddle tables cover sizes up to 2^16
+constexpr unsigned TW_LOG = 17;  // twiddle tables cover sizes up to 2^17 (degree-2^14 circuits at rate 3)
 // LDS slots of a size-n NTT workgroup: one pad slot per 32 elements (ntt16.h lp())
 __host__ __device__ constexpr uint32_t ntt_lds_words(uint32_t n) { return n + (n >> 5); }
 #define QP_HAVE_LDS_WORDS 1

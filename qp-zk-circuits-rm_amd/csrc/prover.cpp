@@ -125,6 +125,7 @@ struct qp_prover {
   DevBuf wg_gens, wg_lvl, wg_wslot, wg_wslot_cm, wg_in_slots, wg_pi_slots, wg_vals, wg_in, wg_err, wg_pis;
   uint32_t wg_nslots = 0, wg_nin = 0, wg_nlev = 0;
   bool quotient_rereads = false;
+  bool generic_quotient = false;  // a gate outside k_quotient_1r's set (the recursive verifier's RandomAccess)
   bool pp_generic = false;  // QPGPU_PP_GENERIC=1: the runtime-shape k_pp_rows (A/B)
   uint64_t *h_in = nullptr;  // pinned [max_batch][wg_nin] commit() values
   std::vector<uint32_t> h_werr;
@@ -262,9 +263,17 @@ int setup(qp_prover *P) {
       case qc::G_BASE_SUM: g.kind[i] = qpk::GK_BASE_SUM; break;
       case qc::G_ARITHMETIC: g.kind[i] = qpk::GK_ARITHMETIC; break;
       case qc::G_POSEIDON: g.kind[i] = qpk::GK_POSEIDON; break;
-      default: break;
+      case qc::G_RANDOM_ACCESS:
+        g.kind[i] = qpk::GK_RANDOM_ACCESS;
+        P->generic_quotient = true;  // k_quotient_1r covers the leaf circuits' six gates only
+        break;
+      default:
+        c->err = "unsupported gate kind for the GPU prover";
+        return QP_ERR_ARG;
     }
     g.param[i] = cd.gate_params[i];
+    g.param2[i] = i < cd.gate_params2.size() ? cd.gate_params2[i] : 0;
+    g.param3[i] = i < cd.gate_params3.size() ? cd.gate_params3[i] : 0;
     g.sel_index[i] = cd.selector_indices[i];
   }
   for (uint32_t s = 0; s < g.nsel; s++) {
@@ -357,7 +366,7 @@ int setup(qp_prover *P) {
   P->h_pos.assign(B, 0);
   P->h_powst.assign((size_t)B * 24, 0);
   P->h_found.assign(B, 0);
-  {
+  if (cd.device_witness) {
     // device witness generation tables (structural, shared by all proofs)
     auto up32 = [&](DevBuf &d, const std::vector<uint32_t> &v) -> hipError_t {
       hipError_t e = d.alloc((v.size() + 1) / 2);
@@ -588,7 +597,7 @@ int prove_batch(qp_prover *P, const uint64_t *d_wires, const uint64_t *const *wi
     a.num_constants = P->NC;
     a.g = P->gdesc;
     kt_begin(P, 3);
-    if (P->quotient_rereads)  // A/B: the round-1 kernel (QPGPU_QUOTIENT=rereads)
+    if (P->quotient_rereads || P->generic_quotient)  // generic gate list (or A/B: QPGPU_QUOTIENT=rereads)
       qpk::k_quotient<2><<<dim3(cdiv(N, 256), nb), 256, 0, s>>>(a);
     else
       qpk::k_quotient_1r<<<dim3(cdiv(N, 256), nb), 256, 0, s>>>(a);
@@ -953,6 +962,10 @@ using FillFn = std::string (*)(const qp_circuit *, const void *, qc::Witness &, 
 int prove_inputs(qp_prover *P, FillFn fill, const uint8_t *inputs, size_t in_size, uint32_t nproofs, uint8_t *out,
                  size_t stride, size_t *lens) {
   const qc::CircuitData &cd = P->circuit->cd;
+  if (!cd.device_witness) {
+    P->ctx->err = "this circuit's witness generators run on the host only: commit() and prove the witnesses";
+    return QP_ERR_STATE;
+  }
   for (uint32_t done = 0; done < nproofs;) {
     const uint32_t nb = std::min(P->max_batch, nproofs - done);
     std::atomic<uint32_t> first_bad{UINT32_MAX};

@@ -112,6 +112,9 @@ def lib():
         "qp_wormhole_commit": (ctypes.c_int, [VP, VP, PP, ctypes.c_char_p, ctypes.c_size_t]),
         "qp_voting_circuit_new": (ctypes.c_int, [ctypes.c_int, PP]),
         "qp_voting_commit": (ctypes.c_int, [VP, VP, PP, ctypes.c_char_p, ctypes.c_size_t]),
+        "qp_aggregation_circuit_new": (ctypes.c_int, [ctypes.c_char_p, ctypes.c_size_t, ctypes.c_uint32, PP]),
+        "qp_aggregation_commit": (ctypes.c_int, [VP, ctypes.c_char_p, ctypes.c_size_t, VP, VP, ctypes.c_uint32,
+                                                 VP, PP, ctypes.c_char_p, ctypes.c_size_t]),
         "qp_witness_wires": (ctypes.c_int, [VP, U64P]),
         "qp_witness_public_inputs": (ctypes.c_int, [VP, U64P, ctypes.c_uint32, ctypes.POINTER(ctypes.c_uint32)]),
         "qp_witness_free": (None, [VP]),

@@ -218,6 +218,38 @@ class Circuit:
         c.zk = bool(zero_knowledge)
         return c
 
+    @classmethod
+    def aggregation(cls, inner_common: bytes, num_proofs: int):
+        """aggregate_chunk's circuit (wormhole/aggregator/src/circuits/tree.rs:106-127):
+        a recursive verifier of `num_proofs` proofs of the circuit with CommonCircuitData
+        `inner_common`, their public inputs registered in order."""
+        h = ctypes.c_void_p()
+        rc = lib().qp_aggregation_circuit_new(bytes(inner_common), len(inner_common), int(num_proofs),
+                                              ctypes.byref(h))
+        if rc:
+            raise QpError(rc, "qp_aggregation_circuit_new (unsupported inner common data?)")
+        c = cls(h, "aggregation")
+        c.zk = bool(inner_common[49])
+        c.num_proofs = int(num_proofs)
+        return c
+
+    def commit_proofs(self, verifier_only: bytes, proofs, zk_randomness=None) -> "Witness":
+        """aggregate_chunk's witness (tree.rs:129-134): the inner verifier-only data
+        (cap height, constants/sigmas cap, circuit digest) and the proofs to verify."""
+        proofs = [bytes(p) for p in proofs]
+        arr = (ctypes.c_char_p * len(proofs))(*proofs)
+        lens = (ctypes.c_size_t * len(proofs))(*[len(p) for p in proofs])
+        zk_ptr, zk_keep = _zk_ptr(zk_randomness)
+        h = ctypes.c_void_p()
+        err = ctypes.create_string_buffer(512)
+        rc = lib().qp_aggregation_commit(self.h, bytes(verifier_only), len(verifier_only),
+                                         ctypes.cast(arr, ctypes.c_void_p), ctypes.cast(lens, ctypes.c_void_p),
+                                         len(proofs), ctypes.cast(zk_ptr, ctypes.c_void_p) if zk_ptr else None,
+                                         ctypes.byref(h), err, 512)
+        if rc:
+            raise QpError(rc, err.value.decode())
+        return Witness(self, h)
+
     def common_data(self):
         ln = ctypes.c_size_t()
         lib().qp_circuit_common_data(self.h, None, 0, ctypes.byref(ln))
