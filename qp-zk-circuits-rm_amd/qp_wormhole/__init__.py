@@ -12,7 +12,10 @@ from .circuits import (Circuit, CircuitInputs, PrivateCircuitInputs, ProcessedSt
                        PublicCircuitInputs, VoteCircuitData, VotePrivateInputs, VotePublicInputs, Witness)
 from .prover import (Prover, ProofWithPublicInputs, WormholeProver, generate_circuit_binaries,  # noqa: F401,E402
                      prover_only_bytes)
+from .aggregator import (AggregatedProof, CircuitData, TreeAggregationConfig, WormholeProofAggregator,  # noqa: F401,E402
+                         aggregate_chunk, aggregate_level, aggregate_to_tree)
 
 __all__ = ["Circuit", "CircuitInputs", "PrivateCircuitInputs", "ProcessedStorageProof", "PublicCircuitInputs",
            "Witness", "VoteCircuitData", "VotePrivateInputs", "VotePublicInputs", "Prover", "ProofWithPublicInputs", "WormholeProver", "Context", "PolynomialBatch", "QpError", "ifft", "lde", "poseidon_permute", "lib", "header_symbols",
-           "generate_circuit_binaries", "prover_only_bytes", "GateDesc", "gate_desc", "quotient", "FriLayer", "fri_fold", "pow_grind"]
+           "generate_circuit_binaries", "prover_only_bytes", "AggregatedProof", "CircuitData", "TreeAggregationConfig",
+           "WormholeProofAggregator", "aggregate_chunk", "aggregate_level", "aggregate_to_tree", "GateDesc", "gate_desc", "quotient", "FriLayer", "fri_fold", "pow_grind"]

@@ -1,0 +1,257 @@
+"""Recursive tree aggregation of leaf proofs on the MI355X prover — the host
+mirror of qp-wormhole-aggregator (wormhole/aggregator/src):
+
+* TreeAggregationConfig, AggregatedProof   circuits/tree.rs:17-53
+* aggregate_to_tree / aggregate_level /
+  aggregate_chunk                           circuits/tree.rs:55-143
+* WormholeProofAggregator                  aggregator.rs:13-92
+* pad_with_dummy_proofs                    util.rs:11-29
+* PublicCircuitInputs.try_from_aggregated  wormhole/circuit/src/inputs.rs:57-131
+
+aggregate_chunk's circuit (add_virtual_verifier_data + verify_proof per
+proof + register_public_inputs) is the native recursive verifier
+(csrc/recursion.cpp); its witness is generated on the host and every level's
+chunks are proven in ONE batched GPU launch sequence (the reference proves
+chunks one by one, with rayon across chunks).  The reference rebuilds the
+circuit for every chunk (tree.rs:111-127); here a level's circuit and its
+device preprocessing are built once per (inner circuit, branching) and cached.
+The aggregation circuit is parity-unpinned: the reference commits no
+aggregated proof.
+"""
+import struct
+import threading
+from dataclasses import dataclass
+from typing import List, Optional
+
+from ._native import Context, QpError
+from .circuits import Circuit, PublicCircuitInputs
+from .prover import ProofWithPublicInputs, Prover
+
+DEFAULT_TREE_BRANCHING_FACTOR = 2  # tree.rs:17
+DEFAULT_TREE_DEPTH = 3             # tree.rs:20
+LEAF_PI_LEN = 16                   # inputs.rs:91
+
+
+@dataclass
+class TreeAggregationConfig:
+    """tree.rs:30-53: num_leaf_proofs = branching ** depth."""
+    num_leaf_proofs: int
+    tree_branching_factor: int
+    tree_depth: int
+
+    @classmethod
+    def new(cls, tree_branching_factor: int, tree_depth: int):
+        return cls(tree_branching_factor ** tree_depth, tree_branching_factor, tree_depth)
+
+    @classmethod
+    def default(cls):
+        return cls.new(DEFAULT_TREE_BRANCHING_FACTOR, DEFAULT_TREE_DEPTH)
+
+
+@dataclass
+class CircuitData:
+    """The parts of plonky2 CircuitData an aggregation level hands to the next:
+    CommonCircuitData bytes and VerifierOnlyCircuitData bytes (cap height, cap,
+    circuit digest)."""
+    common: bytes
+    verifier_only: bytes
+
+    def verifier_data(self) -> bytes:
+        """verifier.bin layout: VerifierOnlyCircuitData || CommonCircuitData."""
+        return self.verifier_only + self.common
+
+
+@dataclass
+class AggregatedProof:
+    """tree.rs:22-27."""
+    proof: ProofWithPublicInputs
+    circuit_data: CircuitData
+
+
+class _LevelProver:
+    """One aggregation circuit (inner common data, branching) with its device prover."""
+
+    def __init__(self, inner_common: bytes, branching: int, device: int, max_batch: int):
+        self.circuit = Circuit.aggregation(inner_common, branching)
+        self.ctx = Context(device)
+        self.max_batch = max_batch
+        self.prover = Prover(self.ctx, self.circuit, max_batch=max_batch)
+        vd = self.prover.verifier_data()
+        common = self.circuit.common_data()
+        assert vd.endswith(common)
+        self.data = CircuitData(common, vd[:len(vd) - len(common)])
+        self.lock = threading.Lock()
+
+    def prove_chunks(self, chunks, inner_vo: bytes) -> List[AggregatedProof]:
+        # aggregate_chunk's witnesses (host), then one batched prove per max_batch
+        witnesses = [self.circuit.commit_proofs(inner_vo, [p.to_bytes() for p in ch]) for ch in chunks]
+        out = []
+        with self.lock:
+            for i in range(0, len(witnesses), self.max_batch):
+                ws = witnesses[i:i + self.max_batch]
+                for w, data in zip(ws, self.prover.prove_witnesses(ws)):
+                    out.append(AggregatedProof(ProofWithPublicInputs(data, w.public_inputs()), self.data))
+        for w in witnesses:
+            w.free()
+        return out
+
+
+_levels = {}
+_levels_lock = threading.Lock()
+
+
+def _level_prover(inner_common: bytes, branching: int, device: int, max_batch: int) -> _LevelProver:
+    key = (bytes(inner_common), branching, device)
+    with _levels_lock:
+        lp = _levels.get(key)
+        if lp is None or lp.max_batch < max_batch:
+            lp = _LevelProver(inner_common, branching, device, max(max_batch, lp.max_batch if lp else 0))
+            _levels[key] = lp
+        return lp
+
+
+def _as_proof(p) -> ProofWithPublicInputs:
+    return p if isinstance(p, ProofWithPublicInputs) else ProofWithPublicInputs(bytes(p), [])
+
+
+def aggregate_chunk(chunk, common_data: bytes, verifier_only: bytes, device: int = 0,
+                    backend=None) -> AggregatedProof:
+    """tree.rs:106-143: verify every proof of the chunk in one circuit and prove it."""
+    return aggregate_level(list(chunk), common_data, verifier_only, TreeAggregationConfig.new(len(chunk), 1),
+                           device, backend)[0]
+
+
+def aggregate_level(proofs, common_data: bytes, verifier_only: bytes, config: TreeAggregationConfig,
+                    device: int = 0, backend=None) -> List[AggregatedProof]:
+    """tree.rs:80-103: chunks of `tree_branching_factor` proofs, each aggregated
+    (all chunks of the level proven as one GPU batch).  backend(inner_common,
+    branching, device, max_batch) -> an object with .data and .prove_chunks()
+    (default: the GPU level prover; tests inject a CPU one)."""
+    k = config.tree_branching_factor
+    proofs = [_as_proof(p) for p in proofs]
+    if len(proofs) % k:
+        raise ValueError(f"{len(proofs)} proofs do not split into chunks of {k}")
+    chunks = [proofs[i:i + k] for i in range(0, len(proofs), k)]
+    lp = (backend or _level_prover)(common_data, k, device, max(1, min(len(chunks), 16)))
+    return lp.prove_chunks(chunks, verifier_only)
+
+
+def aggregate_to_tree(leaf_proofs, common_data: bytes, verifier_only: bytes,
+                      config: Optional[TreeAggregationConfig] = None, device: int = 0,
+                      backend=None) -> AggregatedProof:
+    """tree.rs:55-77: aggregate the first level, then each next level with the
+    previous level's circuit data, down to one root proof."""
+    config = config or TreeAggregationConfig.default()
+    proofs = aggregate_level(leaf_proofs, common_data, verifier_only, config, device, backend)
+    while len(proofs) > 1:
+        cd = proofs[0].circuit_data
+        proofs = aggregate_level([p.proof for p in proofs], cd.common, cd.verifier_only, config, device, backend)
+    assert len(proofs) == 1
+    return proofs[0]
+
+
+def pad_with_dummy_proofs(proofs, proof_len: int, dummy_proof) -> list:
+    """util.rs:11-29 (the dummy is a proof of the leaf circuit on the default
+    test inputs, as the reference's dummy_proof*.bin)."""
+    if len(proofs) > proof_len:
+        raise ValueError("proofs to aggregate was more than the maximum allowed")
+    return list(proofs) + [dummy_proof] * (proof_len - len(proofs))
+
+
+def _felts_to_digest(f) -> bytes:
+    return b"".join(int(x).to_bytes(8, "little") for x in f)
+
+
+def public_inputs_from_slice(pis) -> PublicCircuitInputs:
+    """PublicCircuitInputs::try_from_slice (inputs.rs:91-131)."""
+    if len(pis) != LEAF_PI_LEN:
+        raise ValueError(f"public inputs should contain: {LEAF_PI_LEN} field elements, got: {len(pis)}")
+    amount = 0
+    for i, x in enumerate(pis[8:12]):
+        if int(x) >> 32:
+            raise ValueError("failed to deserialize funding amount")
+        amount |= int(x) << (96 - 32 * i)
+    return PublicCircuitInputs(funding_amount=amount, nullifier=_felts_to_digest(pis[0:4]),
+                               root_hash=_felts_to_digest(pis[4:8]), exit_account=_felts_to_digest(pis[12:16]))
+
+
+def public_inputs_from_aggregated(aggr: ProofWithPublicInputs, leaf_pi_len: int, num_leaves: int):
+    """PublicCircuitInputs::try_from_aggregated (inputs.rs:57-89)."""
+    pis = list(aggr.public_inputs)
+    expected = leaf_pi_len * num_leaves
+    if len(pis) != expected:
+        raise ValueError(f"aggregated public inputs should contain: {expected} (= {num_leaves} leaves × "
+                         f"{leaf_pi_len} fields), got: {len(pis)}")
+    return [public_inputs_from_slice(pis[i:i + leaf_pi_len]) for i in range(0, len(pis), leaf_pi_len)]
+
+
+class WormholeProofAggregator:
+    """aggregator.rs:13-92 over this library's Wormhole leaf circuit."""
+
+    def __init__(self, leaf_circuit_data: CircuitData, dummy_proof: Optional[ProofWithPublicInputs] = None,
+                 device: int = 0):
+        self.leaf_circuit_data = leaf_circuit_data
+        self.config = TreeAggregationConfig.default()
+        self.proofs_buffer = []
+        self.device = device
+        self._dummy = dummy_proof
+
+    @classmethod
+    def from_circuit_config(cls, config: str = "standard_recursion_zk_config", device: int = 0):
+        """aggregator.rs:40-45 (the leaf verifier data of WormholeVerifier::new(config))."""
+        from .prover import WormholeProver, _verifier_only
+        wp = WormholeProver(config, device)
+        with wp._prove_lock:
+            vo = _verifier_only(wp.circuit, wp.prover)
+        return cls(CircuitData(wp.circuit.common_data(), vo), device=device)
+
+    @classmethod
+    def default(cls, device: int = 0):
+        """aggregator.rs:19-24: standard_recursion_zk_config."""
+        return cls.from_circuit_config("standard_recursion_zk_config", device)
+
+    def with_config(self, config: TreeAggregationConfig):
+        self.config = config
+        return self
+
+    def push_proof(self, proof):
+        if len(self.proofs_buffer) >= self.config.num_leaf_proofs:
+            raise ValueError("tried to add proof when proof buffer is full")
+        self.proofs_buffer.append(_as_proof(proof))
+
+    def dummy_proof(self) -> ProofWithPublicInputs:
+        """The padding proof (util.rs:6-9 embeds the reference's proof of its test
+        inputs, which verifies only under the reference's own circuit): unless one is
+        passed in, a proof of this leaf circuit on the deterministic synthetic input
+        0 with an empty storage proof (SURVEY.md 8(d) variant A)."""
+        if self._dummy is None:
+            from .prover import CONFIGS, WormholeProver, _config_of_common
+            from .synthetic import synthetic_inputs
+            cfg = _config_of_common(self.leaf_circuit_data.common)
+            if cfg not in CONFIGS:
+                raise ValueError("no dummy proof for this leaf circuit: pass dummy_proof=")
+            self._dummy = WormholeProver(cfg, self.device).commit(synthetic_inputs(0, 0)).prove()
+        return self._dummy
+
+    def extract_leaf_public_inputs(self, aggr) -> List[PublicCircuitInputs]:
+        proof = aggr.proof if isinstance(aggr, AggregatedProof) else aggr
+        return public_inputs_from_aggregated(proof, LEAF_PI_LEN, self.config.num_leaf_proofs)
+
+    def aggregate(self) -> AggregatedProof:
+        if not self.proofs_buffer:
+            raise ValueError("there are no proofs to aggregate")
+        proofs, self.proofs_buffer = self.proofs_buffer, []
+        padded = pad_with_dummy_proofs(proofs, self.config.num_leaf_proofs, self.dummy_proof())
+        return aggregate_to_tree(padded, self.leaf_circuit_data.common, self.leaf_circuit_data.verifier_only,
+                                 self.config, self.device)
+
+
+def verifier_only_of(verifier_data: bytes, common: bytes) -> bytes:
+    """VerifierOnlyCircuitData bytes from a verifier.bin-layout blob."""
+    if not verifier_data.endswith(common):
+        raise ValueError("verifier data does not end with the common data")
+    vo = verifier_data[:len(verifier_data) - len(common)]
+    (h,) = struct.unpack_from("<Q", vo, 0)
+    if len(vo) != 8 + 32 * (1 << h) + 32:
+        raise QpError(1, "malformed VerifierOnlyCircuitData")
+    return vo

@@ -129,3 +129,37 @@ def run_steps(prove_share, nprovers, steps, dist=None, slot=0, device="cpu", pip
             launch([s])
             last = finish(s)
     return last
+
+
+def aggregate_subtrees(local_proofs, common: bytes, verifier_only: bytes, branching: int, dist,
+                       device="cpu", gpu: int = 0, dst: int = 0, backend=None):
+    """Per-rank subtree aggregation (the levels of tree.rs:92-103
+    are independent per chunk): each rank aggregates its own leaf proofs into one
+    subtree root (aggregate_to_tree with depth log_branching(local count)); only
+    the roots cross the interconnect (one gather of world proofs instead of every
+    leaf); rank dst aggregates the roots into the tree root.  Every rank must hold
+    branching**k leaves (equal k) and world must be a power of branching.
+    Returns the root AggregatedProof on dst, None elsewhere."""
+    from .aggregator import TreeAggregationConfig, aggregate_to_tree
+    from .prover import ProofWithPublicInputs
+    world, rank = dist.get_world_size(), dist.get_rank()
+    n, depth = len(local_proofs), 0
+    while branching ** depth < n:
+        depth += 1
+    if branching ** depth != n or n < branching:
+        raise ValueError(f"{n} local proofs are not a power (>= 1) of the branching factor {branching}")
+    sub = aggregate_to_tree(local_proofs, common, verifier_only, TreeAggregationConfig.new(branching, depth),
+                            gpu, backend)
+    roots = gather_proofs([sub.proof.to_bytes()], len(sub.proof.to_bytes()), dist, device=device, dst=dst)
+    if rank != dst:
+        return None
+    if world == 1:
+        return sub
+    wdepth = 0
+    while branching ** wdepth < world:
+        wdepth += 1
+    if branching ** wdepth != world:
+        raise ValueError(f"world size {world} is not a power of the branching factor {branching}")
+    cd = sub.circuit_data
+    return aggregate_to_tree([ProofWithPublicInputs(r, []) for r in roots], cd.common, cd.verifier_only,
+                             TreeAggregationConfig.new(branching, wdepth), gpu, backend)

@@ -173,3 +173,43 @@ def test_bench_step_loop_world2_gloo(pipelined):
         for r in range(2):
             want = [bytes([r, i, s, j]) * 64 for i in range(3) for j in range(2 + i)]
             assert rows[r] == want
+
+
+def _worker_subtrees(rank, world, port, q):
+    """Per-rank subtree aggregation: every rank aggregates its own
+    leaves (the reference's two proofs) into a subtree root; only the roots are
+    gathered; rank 0 aggregates them.  The prover is the oracle CPU stand-in."""
+    import struct
+
+    import torch.distributed as dist
+
+    from agg_oracle_backend import oracle_backend
+    from qp_wormhole.distributed import aggregate_subtrees
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    from current_circuit_vd import current_circuit_verifier_data
+    from oracle_lib import golden, lib as olib
+    from test_oracle_golden import current_common_bytes
+    cb = current_common_bytes()
+    vd = current_circuit_verifier_data(cb)[0]
+    leaves = [golden("dummy_proof.bin"), golden("dummy_proof_zk.bin")]
+    if rank == 1:
+        leaves = leaves[::-1]
+    root = aggregate_subtrees(leaves, cb, vd[:len(vd) - len(cb)], 2, dist, backend=oracle_backend)
+    if rank == 0:
+        rvd = root.circuit_data.verifier_data()
+        ok = olib().ora_verify(rvd, len(rvd), root.proof.to_bytes(), len(root.proof.to_bytes())) == 0
+        want = []
+        for r in range(world):
+            ls = [golden("dummy_proof.bin"), golden("dummy_proof_zk.bin")]
+            for pf in (ls if r == 0 else ls[::-1]):
+                want += list(struct.unpack_from("<16Q", pf, len(pf) - 128))
+        q.put((ok, [int(x) for x in root.proof.public_inputs] == want))
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+def test_subtree_aggregation_world2_gloo():
+    ok, pis_ok = _run(_worker_subtrees, 2)
+    assert ok and pis_ok

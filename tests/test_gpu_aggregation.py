@@ -1,0 +1,101 @@
+"""Recursive aggregation on the MI355X (BASELINE configs[3]):
+aggregate_chunk / aggregate_to_tree / WormholeProofAggregator
+(wormhole/aggregator/src/circuits/tree.rs:55-143, aggregator.rs:13-92).
+
+Parity: the aggregation circuits' GPU proofs (degree 2^14, generic quotient
+kernel with the RandomAccessGate) are byte-identical to the CPU oracle
+prover's for the same witness and verify under the oracle verifier.  The
+in-circuit verifier itself is pinned by the reference's own leaf proofs
+(tests/golden/dummy_proof{,_zk}.bin verify inside it).  The aggregation
+circuit's layout is parity-unpinned (no aggregated reference proof exists).
+"""
+import pytest
+
+from oracle_lib import golden, lib as olib
+from test_gpu_prover import oracle_prove
+
+pytestmark = pytest.mark.gpu
+
+
+def verify(vd, proof):
+    return olib().ora_verify(vd, len(vd), proof, len(proof))
+
+
+@pytest.fixture(scope="module")
+def reference_leaves():
+    from current_circuit_vd import current_circuit_verifier_data
+    from test_oracle_golden import current_common_bytes
+    cb = current_common_bytes()
+    vd = current_circuit_verifier_data(cb)[0]
+    return cb, vd[:len(vd) - len(cb)], [golden("dummy_proof.bin"), golden("dummy_proof_zk.bin")]
+
+
+def test_aggregate_reference_proofs_gpu_equals_oracle(reference_leaves):
+    """aggregate_chunk over the reference's own two proofs: GPU bytes == oracle
+    bytes of the same witness, and the aggregated proof verifies."""
+    import qp_wormhole
+    cb, vo, leaves = reference_leaves
+    agg = qp_wormhole.aggregate_chunk(leaves, cb, vo)
+    circ = qp_wormhole.Circuit.aggregation(cb, 2)
+    assert circ.degree_bits == 14
+    w = circ.commit_proofs(vo, leaves)
+    ob, ovd = oracle_prove(circ, w.wires(), w.public_inputs())
+    assert agg.proof.to_bytes() == ob
+    assert agg.circuit_data.verifier_data() == ovd
+    assert verify(ovd, ob) == 0
+    # public inputs: the two leaves' 16 each, in order
+    from oracle_lib import golden as g
+    import struct
+    want = []
+    for name in ("dummy_proof.bin", "dummy_proof_zk.bin"):
+        pf = g(name)
+        want += list(struct.unpack_from("<16Q", pf, len(pf) - 128))
+    assert agg.proof.public_inputs == want
+
+
+def test_tree_of_eight_native_leaves():
+    """WormholeProofAggregator with the default tree (branching 2, depth 3): five
+    native leaf proofs + three dummies -> 4 + 2 + 1 aggregation proofs on the GPU;
+    the root verifies, its bytes equal the oracle's for the same witness, and the
+    leaf public inputs come back out of it (extract_leaf_public_inputs)."""
+    import qp_wormhole
+    from qp_wormhole.aggregator import public_inputs_from_slice
+    from qp_wormhole.synthetic import synthetic_inputs
+    wp = qp_wormhole.WormholeProver("standard_recursion_zk_config")
+    leaves = [qp_wormhole.WormholeProver("standard_recursion_zk_config").commit(synthetic_inputs(40 + k, k % 3))
+              .prove() for k in range(5)]
+    agg = qp_wormhole.WormholeProofAggregator.default()
+    for p in leaves:
+        agg.push_proof(p)
+    root = agg.aggregate()
+    assert verify(root.circuit_data.verifier_data(), root.proof.to_bytes()) == 0
+    pis = agg.extract_leaf_public_inputs(root)
+    assert len(pis) == 8
+    for k in range(5):
+        assert pis[k] == public_inputs_from_slice(leaves[k].public_inputs)
+    dummy = public_inputs_from_slice(agg.dummy_proof().public_inputs)
+    assert pis[5:] == [dummy] * 3
+    del wp
+
+
+def test_level_two_gpu_equals_oracle(reference_leaves):
+    """A level-2 circuit (inner = the aggregation circuit, with RandomAccess gates):
+    GPU == oracle bytes; verifies."""
+    import qp_wormhole
+    cb, vo, leaves = reference_leaves
+    l1 = qp_wormhole.aggregate_chunk(leaves, cb, vo)
+    cd = l1.circuit_data
+    l2 = qp_wormhole.aggregate_chunk([l1.proof, l1.proof], cd.common, cd.verifier_only)
+    circ = qp_wormhole.Circuit.aggregation(cd.common, 2)
+    w = circ.commit_proofs(cd.verifier_only, [l1.proof.to_bytes()] * 2)
+    ob, ovd = oracle_prove(circ, w.wires(), w.public_inputs())
+    assert l2.proof.to_bytes() == ob and verify(ovd, ob) == 0
+
+
+def test_tampered_leaf_is_rejected(reference_leaves):
+    import qp_wormhole
+    cb, vo, leaves = reference_leaves
+    bad = bytearray(leaves[1])
+    bad[3 * 512 + 84 * 16 + 7] ^= 1
+    with pytest.raises(qp_wormhole.QpError, match="set twice"):
+        qp_wormhole.aggregate_chunk([leaves[0], bytes(bad)], cb, vo)
