@@ -366,8 +366,10 @@ int setup(qp_prover *P) {
   P->h_pos.assign(B, 0);
   P->h_powst.assign((size_t)B * 24, 0);
   P->h_found.assign(B, 0);
-  if (cd.device_witness) {
-    // device witness generation tables (structural, shared by all proofs)
+  {
+    // witness tables: the slot -> wire expansion (k_witness_expand: every
+    // circuit, also for host-generated witnesses) and, for circuits whose
+    // generators all have a device form, the level-scheduled generator list
     auto up32 = [&](DevBuf &d, const std::vector<uint32_t> &v) -> hipError_t {
       hipError_t e = d.alloc((v.size() + 1) / 2);
       if (!e && !v.empty()) e = hipMemcpy(d.p, v.data(), v.size() * 4, hipMemcpyHostToDevice);
@@ -375,24 +377,26 @@ int setup(qp_prover *P) {
     };
     P->wg_nslots = cd.num_slots;
     P->wg_nin = (uint32_t)cd.input_slots.size();
-    P->wg_nlev = (uint32_t)cd.level_off.size() - 1;
     if (P->npis > 256) {
       c->err = "too many public inputs for the device witness gather";
       return QP_ERR_ARG;
     }
-    TRY(P->wg_gens.alloc(cd.dev_gens.size() * 5));
-    TRY(hipMemcpy(P->wg_gens.p, cd.dev_gens.data(), cd.dev_gens.size() * sizeof(qc::DevGen), hipMemcpyHostToDevice));
-    TRY(up32(P->wg_lvl, cd.level_off));
-    TRY(up32(P->wg_wslot, cd.wire_slot));
     TRY(up32(P->wg_wslot_cm, cd.wire_slot_cm));
-    TRY(up32(P->wg_in_slots, cd.input_slots));
     TRY(up32(P->wg_pi_slots, cd.pi_slots));
     TRY(P->wg_vals.alloc((size_t)B * P->wg_nslots));
-    TRY(P->wg_in.alloc((size_t)B * std::max<uint32_t>(P->wg_nin, 1)));
-    TRY(P->wg_err.alloc((B + 1) / 2));
     TRY(P->wg_pis.alloc((size_t)B * std::max<uint32_t>(P->npis, 1)));
-    TRY(hipHostMalloc((void **)&P->h_in, (size_t)B * std::max<uint32_t>(P->wg_nin, 1) * 8, hipHostMallocDefault));
-    P->h_werr.assign(B, 0);
+    if (cd.device_witness) {
+      P->wg_nlev = (uint32_t)cd.level_off.size() - 1;
+      TRY(P->wg_gens.alloc(cd.dev_gens.size() * 5));
+      TRY(hipMemcpy(P->wg_gens.p, cd.dev_gens.data(), cd.dev_gens.size() * sizeof(qc::DevGen), hipMemcpyHostToDevice));
+      TRY(up32(P->wg_lvl, cd.level_off));
+      TRY(up32(P->wg_wslot, cd.wire_slot));
+      TRY(up32(P->wg_in_slots, cd.input_slots));
+      TRY(P->wg_in.alloc((size_t)B * std::max<uint32_t>(P->wg_nin, 1)));
+      TRY(P->wg_err.alloc((B + 1) / 2));
+      TRY(hipHostMalloc((void **)&P->h_in, (size_t)B * std::max<uint32_t>(P->wg_nin, 1) * 8, hipHostMallocDefault));
+      P->h_werr.assign(B, 0);
+    }
     P->h_wpis.assign((size_t)B * std::max<uint32_t>(P->npis, 1), 0);
   }
   TRY(hipStreamSynchronize(c->stream));
