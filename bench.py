@@ -85,6 +85,8 @@ def parse():
     ap.add_argument("--host-threads", type=int, default=-1,
                     help="host threads per prover (caller included); -1 = split the process's cores "
                          "(OMP_NUM_THREADS, else min(cores, 16)) between the provers; 0 = library default")
+    ap.add_argument("--agg-leaves", type=int, default=64,
+                    help="leaf proofs aggregated (one level, pairs) after the timed region (0 = skip)")
     ap.add_argument("--cpu-sample", type=int, default=2, help="min proofs in the CPU baseline sample (0 = skip)")
     ap.add_argument("--cpu-seconds", type=float, default=10.0, help="min seconds of CPU baseline proving")
     return ap.parse_args()
@@ -244,6 +246,37 @@ def main():
             prover.prove_inputs_array(one, 1)
             ts.append((time.perf_counter() - t1) * 1e3)
         lat = sorted(ts)[1]
+    # recursive aggregation of this run's leaf proofs (BASELINE
+    # configs[3]'s consumer; wormhole/aggregator/src/circuits/tree.rs): one level of
+    # `agg_leaves` leaves (agg_leaves/2 aggregation proofs, degree 2^14, batched) and a
+    # default tree (8 leaves, branching 2, depth 3) end to end; after the timed region
+    agg = None
+    if rank == 0 and not voting and args.agg_leaves and proofs is not None:
+        from qp_wormhole.aggregator import TreeAggregationConfig, aggregate_level, aggregate_to_tree
+        from qp_wormhole.prover import _common_degree_bits
+        from oracle_lib import lib as olib
+        vd = prover.verifier_data()
+        cb = circuit.common_data()
+        vo = vd[:len(vd) - len(cb)]
+        nl = min(args.agg_leaves, len(proofs)) // 2 * 2
+        cfg2 = TreeAggregationConfig.new(2, 1)
+        aggregate_level(proofs[:2], cb, vo, cfg2)  # circuit build + device preprocessing (cached)
+        t1 = time.perf_counter()
+        level = aggregate_level(proofs[:nl], cb, vo, cfg2)
+        lvl_s = time.perf_counter() - t1
+        aggregate_to_tree(proofs[:8], cb, vo)  # builds the level-2/3 circuits (cached)
+        t1 = time.perf_counter()
+        root = aggregate_to_tree(proofs[:8], cb, vo)
+        tree_ms = (time.perf_counter() - t1) * 1e3
+        rvd = root.circuit_data.verifier_data()
+        rp = root.proof.to_bytes()
+        agg = {"level_leaves": nl, "level_aggregation_proofs": len(level),
+               "aggregation_proofs_per_s": len(level) / lvl_s, "leaves_per_s_through_one_level": nl / lvl_s,
+               "tree8_root_ms": tree_ms, "root_verified": olib().ora_verify(rvd, len(rvd), rp, len(rp)) == 0,
+               "aggregation_circuit_degree_bits": _common_degree_bits(root.circuit_data.common),
+               "proof_bytes": len(rp),
+               "note": "aggregate_chunk circuits (native recursive verifier of 2 proofs, degree 2^14), host "
+                       "witness generation + batched GPU prove; one level = nl/2 chunks; tree = 4+2+1 proofs"}
     # standard_recursion_zk_config (the reference's cargo-bench and aggregator config):
     # under no_random it proves the same circuit without salts, one prover, one batch
     zk = None
@@ -313,6 +346,7 @@ def main():
             "proof_bytes": prover.proof_size,
             "latency_1proof_ms": lat,
             "zk_config": zk,
+            "aggregation": agg,
             "prove_only_1prover_proofs_per_s": prove_only,
             "warmup_proof_verified": verified,
         }
