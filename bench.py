@@ -33,19 +33,36 @@ sys.path.insert(0, os.path.join(ROOT, "qp-zk-circuits-rm_amd"))
 sys.path.insert(0, os.path.join(ROOT, "tests"))
 
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec peak (MI355X_MICROARCH.md)
-# VALU issue ceiling of the dominant (Poseidon) kernels: 1024 SIMDs x 2.4 GHz /
-# 2.56 cycles per VOP3 wave-instruction at 8 waves/SIMD (profiles/r02_isa_rates.log,
-# tools/gen_isa_rates.py); one (general) permutation = 15,356 VALU
-# instructions (PMC SQ_INSTS_VALU per wave of the one-permutation-per-lane
-# Merkle level kernel, profiles/r02_v9_pmc_valu_b128.txt: sparse partial rounds
-# in groups of 4; 18,617 at the start of round 2; the Merkle kernel itself now
-# runs the zero-capacity form, 15,020 in profiles/r02_v10_pmc_valu_b128.txt)
-VALU_PEAK_WAVE_INSTR_S = 1024 * 2.4e9 / 2.56
-PERM_VALU_INSTR = 15356
-# HBM traffic of the roofline kernel from rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE
-# passes (tools/pmc_summary.py applies the gfx950 corrections); per proof, scaled
-# to the bench's per-launch proof count
-PMC_FILE = os.path.join(ROOT, "profiles", "r02_v10_pmc_hbm_b128.json")
+# VALU issue peak (MI355X_MICROARCH.md: a wave64 VALU instruction issues over 2
+# cycles per SIMD): 1024 SIMDs x 2.4 GHz / 2 = 1228.8 G wave-instructions/s
+VALU_PEAK_WAVE_INSTR_S = 1024 * 2.4e9 / 2
+# the microbenchmark ceiling of round 2 (tools/isa_rates.hip, profiles/r02_isa_rates.log:
+# 2.56 cycles per VOP3 wave-instruction at 8 waves/SIMD), reported alongside
+VALU_ISA_CEILING_WAVE_INSTR_S = 1024 * 2.4e9 / 2.56
+# measured per-build inputs of the roofline fields, written by the profiling
+# session of this build (tools/gpu_session.sh prof3 / pmc_*; tools/kernel_summary.py,
+# tools/pmc_sq_summary.py, tools/pmc_summary.py)
+PROFILE_TAG = "r03"
+PMC_FILE = os.path.join(ROOT, "profiles", f"{PROFILE_TAG}_pmc_hbm_b128.json")
+PMC_SQ_FILE = os.path.join(ROOT, "profiles", f"{PROFILE_TAG}_pmc_sq_b128.json")
+KSUM_FILE = os.path.join(ROOT, "profiles", f"{PROFILE_TAG}_kernel_summary_3provers.json")
+
+
+def load_json(path):
+    try:
+        return json.load(open(path))
+    except (OSError, ValueError):
+        return None
+
+
+def perm_valu_instr():
+    """VALU instructions per Poseidon permutation: SQ_INSTS_VALU x 64 / lanes of the
+    wires leaf-hash dispatch (17 permutations per leaf) in this build's PMC pass."""
+    recs = load_json(PMC_SQ_FILE) or []
+    for r in recs:
+        if r.get("kernel") == "qpk::k_leaf_hash" and r.get("valu_per_lane_max"):
+            return r["valu_per_lane_max"] / 17.0
+    return None
 
 
 def pmc_traffic(kernel, ncols, log_n, proofs, lanes_per_proof=None):
@@ -330,7 +347,7 @@ def main():
                                                 per[0]) if circuit.degree_bits == 13 else None,
                          "traffic_unit": "bytes per launch",
                          "algorithmic_bytes_per_launch": lde["units"] / max(lde["launches"], 1),
-                         "traffic_source": "profiles/r02_v10_pmc_hbm_b128.json (rocprofv3 --pmc FETCH_SIZE, WRITE_SIZE "
+                         "traffic_source": f"{os.path.relpath(PMC_FILE, ROOT)} (rocprofv3 --pmc FETCH_SIZE, WRITE_SIZE "
                                            "passes of this bench at batch 128), per proof x proofs per launch",
                          "avg_launch_ms": lde["ms"] / max(lde["launches"], 1),
                          "note": "HIP events on the prover stream around each launch of the kernel"},
@@ -371,13 +388,25 @@ def main():
                                             "proofs_per_launch": per[0],
                                             "note": "isolated pass, as roofline.achieved; HBM bytes: PMC file"})
         vk = rec["valu_kernels"]
-        if vk.get("leaf_hash_wires_perms_per_s"):
-            ach = vk["leaf_hash_wires_perms_per_s"] / 64 * PERM_VALU_INSTR
+        ipp = perm_valu_instr()
+        ksum = load_json(KSUM_FILE)
+        if vk.get("leaf_hash_wires_perms_per_s") and ipp:
+            ach = vk["leaf_hash_wires_perms_per_s"] / 64 * ipp
             rec["dominant_kernel"] = {
-                "kernel": "k_leaf_hash (Poseidon Merkle leaves, ~58 % of GPU time, profiles/r02_v10_rocprof_bench_b256_1prover_kernel_stats.csv)", "bound": "valu",
+                "kernel": "k_leaf_hash (Poseidon Merkle leaves)", "bound": "valu",
+                "share_of_kernel_time": ksum["leaf_hash_share"] if ksum else None,
                 "achieved": ach, "peak": VALU_PEAK_WAVE_INSTR_S, "unit": "wave-instructions/s",
-                "frac": ach / VALU_PEAK_WAVE_INSTR_S, "instr_per_perm": PERM_VALU_INSTR,
-                "note": "issue-bound 64-bit integer work (no MFMA path); peak from the measured VOP3 issue cost"}
+                "frac": ach / VALU_PEAK_WAVE_INSTR_S, "instr_per_perm": ipp,
+                "frac_of_isa_microbench_ceiling": ach / VALU_ISA_CEILING_WAVE_INSTR_S,
+                "sources": {"instr_per_perm": os.path.relpath(PMC_SQ_FILE, ROOT),
+                            "share": os.path.relpath(KSUM_FILE, ROOT) if ksum else None,
+                            "perms_per_s": "this run (HIP events, isolated pass)"},
+                "note": "issue-bound 64-bit integer work (no MFMA path); peak = the guide's wave64 issue "
+                        "(1 VALU instruction / 2 cycles / SIMD)"}
+        if ksum:
+            rec["gpu_busy_frac"] = {"value": ksum["gpu_busy_frac"], "source": os.path.relpath(KSUM_FILE, ROOT),
+                                    "note": "union of kernel intervals / traced window, rocprofv3 kernel trace of "
+                                            "this bench (3 provers)"}
         rec["stage_ms_per_step"]["note"] = f"prover 0 ({per[0]} proofs), host + device"
         if world == 1 and args.cpu_sample > 0:
             rec["cpu_baseline"] = cpu_baseline(circuit, wires, pis, args.cpu_sample, args.cpu_seconds)

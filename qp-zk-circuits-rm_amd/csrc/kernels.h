@@ -12,6 +12,18 @@
 namespace qpk {
 
 constexpr unsigned TW_LOG = 17;  // twiddle tables cover sizes up to 2^17 (degree-2^14 circuits at rate 3)
+// Twiddle table layout (2^16 words per direction): [0, 2^15) holds w_{2^16}^j
+// (= w_{2^17}^{2j}), [2^15, 2^16) holds w_{2^17}^{2j+1}.  Every size <= 2^16
+// reads only the first half, with the locality of a plain 2^16 table; the odd
+// powers serve size-2^17 transforms (tw_get below: E = the w_{2^17} exponent).
+__host__ __device__ __forceinline__ uint64_t tw_get(const uint64_t *__restrict__ tw, uint32_t E) {
+  constexpr uint32_t Q = 1u << (TW_LOG - 2);  // 2^15
+  const uint32_t j = E >> 1;
+  const uint64_t *t = tw + ((E & 1) ? Q : 0);
+  if (j < Q) return t[j];
+  const uint64_t v = t[j - Q];
+  return v ? 0xFFFFFFFF00000001ull - v : 0;  // w^(2^16) = -1
+}
 // LDS slots of a size-n NTT workgroup: one pad slot per 32 elements (ntt16.h lp())
 __host__ __device__ constexpr uint32_t ntt_lds_words(uint32_t n) { return n + (n >> 5); }
 #define QP_HAVE_LDS_WORDS 1

@@ -39,8 +39,10 @@ static bool getenv_flag(const char *name) {
 __global__ void k_twiddles(uint64_t *fwd, uint64_t *inv, uint64_t w, uint64_t wi, uint32_t half) {
   uint32_t j = blockIdx.x * blockDim.x + threadIdx.x;
   if (j < half) {
-    fwd[j] = gl::pow(w, j);
-    inv[j] = gl::pow(wi, j);
+    // see kernels.h tw_get: even powers first, then odd ones
+    const uint32_t e = j < half / 2 ? 2 * j : 2 * (j - half / 2) + 1;
+    fwd[j] = gl::pow(w, e);
+    inv[j] = gl::pow(wi, e);
   }
 }
 
@@ -112,7 +114,7 @@ __global__ void __launch_bounds__(512) QP_NTT_OCC k_lde(const uint64_t *__restri
   uint64_t *dst = out + blockIdx.z * o_bstride + (uint64_t)col * o_stride +
                   ((uint64_t)gl::rev_bits(s, rate_bits) << log_n);
   // base = shift * w_N^s ; element k scaled by base^k
-  const uint64_t wN = tw[(uint64_t)s << (TW_LOG - log_n - rate_bits)];
+  const uint64_t wN = tw_get(tw, s << (TW_LOG - log_n - rate_bits));
   const uint64_t base = gl::mul(shift, wN);
   uint64_t f = gl::pow(base, threadIdx.x);
   const uint64_t step = gl::pow(base, blockDim.x);

@@ -183,9 +183,7 @@ __device__ __forceinline__ void dft16(uint64_t a[16]) {
 
 // w_S^e via the half table of w_{2^TW_LOG} (tw[j] = w^j, j < 2^(TW_LOG-1))
 __device__ __forceinline__ uint64_t tw_pow(const uint64_t *__restrict__ tw, uint32_t e, uint32_t log_S) {
-  const uint32_t E = e << (qpk::TW_LOG - log_S);
-  constexpr uint32_t HALF = 1u << (qpk::TW_LOG - 1);
-  return E < HALF ? tw[E] : gl::P - tw[E - HALF];  // tw entries are canonical and nonzero
+  return qpk::tw_get(tw, e << (qpk::TW_LOG - log_S));
 }
 
 #ifndef QP_PASS32

@@ -17,7 +17,7 @@ __device__ __forceinline__ void dif_lds(uint64_t *a, uint32_t log_n, const uint6
       uint32_t k = ((b >> s) << (s + 1)) + j;
       uint64_t u = a[k], v = a[k + h];
       a[k] = gl::add(u, v);
-      a[k + h] = gl::mul(gl::sub(u, v), tw[j << tsh]);
+      a[k + h] = gl::mul(gl::sub(u, v), tw_get(tw, j << tsh));
     }
     __syncthreads();
   }

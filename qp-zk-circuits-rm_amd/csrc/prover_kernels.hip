@@ -24,9 +24,7 @@ using gl::ext;
 
 __device__ __forceinline__ uint64_t wpow_N(const uint64_t *__restrict__ tw, uint32_t j, uint32_t logN) {
   // w_N^j from the half table of w_{2^TW_LOG}: w_N^j = w_T^{j << (TW_LOG-logN)}
-  uint32_t e = j << (TW_LOG - logN);
-  const uint32_t half = 1u << (TW_LOG - 1);
-  return e < half ? tw[e] : gl::neg(tw[e - half]);
+  return tw_get(tw, j << (TW_LOG - logN));
 }
 
 // ---------------------------------------------------------------- a9
@@ -661,6 +659,9 @@ __device__ __forceinline__ uint64_t mul_pow2_rt(uint64_t x, uint32_t e) {
 #ifndef QP_QSTASH
 #define QP_QSTASH 16
 #endif
+#ifndef QP_QPREFETCH
+#define QP_QPREFETCH 4
+#endif
 __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(QP_QUOTIENT_WAVES)))
 k_quotient_1r(QuotientArgs a) {
   const uint32_t logN = a.log_n + a.rate_bits;
@@ -715,11 +716,36 @@ k_quotient_1r(QuotientArgs a) {
   // QP_QSTASH of them are kept in LDS (per lane, conflict-free [j][lane])
   __shared__ uint64_t stash[(QP_QSTASH ? QP_QSTASH : 1) * 256];
   const uint32_t nst = g_pos >= 0 ? (R < QP_QSTASH ? R : QP_QSTASH) : 0;
+  // QP_QPREFETCH wires and sigmas loaded ahead of the sweep (the loads of
+  // iteration jj + QP_QPREFETCH are issued before iteration jj's arithmetic)
+  constexpr uint32_t PF = QP_QPREFETCH;
+  uint64_t wbuf[PF ? PF : 1], sbuf[PF ? PF : 1];
+  if constexpr (PF > 0) {
+#pragma unroll
+    for (uint32_t i = 0; i < PF; i++) {
+      wbuf[i] = i < R ? WV(i) : 0;
+      sbuf[i] = i < R ? cs[(uint64_t)(a.num_constants + i) * N] : 0;
+    }
+  }
   for (uint32_t jj = 0; jj < R; jj++) {
-    const uint64_t w = WV(jj);
+    uint64_t w, sg;
+    if constexpr (PF > 0) {
+      w = wbuf[0];
+      sg = sbuf[0];
+#pragma unroll
+      for (uint32_t i = 0; i + 1 < PF; i++) {
+        wbuf[i] = wbuf[i + 1];
+        sbuf[i] = sbuf[i + 1];
+      }
+      const uint32_t jn = jj + PF;
+      wbuf[PF - 1] = jn < R ? WV(jn) : 0;
+      sbuf[PF - 1] = jn < R ? cs[(uint64_t)(a.num_constants + jn) * N] : 0;
+    } else {
+      w = WV(jj);
+      sg = cs[(uint64_t)(a.num_constants + jj) * N];
+    }
     if (jj < nst) stash[jj * blockDim.x + threadIdx.x] = w;
     // permutation argument, both challenges (k_j = g^j folded into bkx)
-    const uint64_t sg = cs[(uint64_t)(a.num_constants + jj) * N];
     num0 = gfn::mul(num0, gfn::add(gfn::add_c(w, gamma0), bkx0));
     den0 = gfn::mul(den0, gfn::add(gfn::add_c(w, gamma0), gfn::mul(beta0, sg)));
     num1 = gfn::mul(num1, gfn::add(gfn::add_c(w, gamma1), bkx1));
