@@ -203,3 +203,34 @@ long ora_check_witness(const uint8_t *cb, size_t clen, const uint64_t *cs, const
     }
     return num == den ? -1 : -2;
 }
+
+/* Values-form polynomial evaluation at extension points (layout-parity tests):
+ * f(x) = (x^n - 1)/n * sum_r v_r w^r / (x - w^r) for v over H = <w>, |H| = n.
+ * vals col-major [ncols][n]; xs [nx][2] (c0, c1); out [ncols][nx][2].  The
+ * reference opens every preprocessed / wire column at the query points
+ * g * w_N^rev(i) (base field) and at zeta (extension), so this is what the
+ * fixture comparisons need. */
+void ora_eval_values(const uint64_t *vals, size_t ncols, unsigned log_n, const uint64_t *xs, size_t nx,
+                     uint64_t *out) {
+    size_t n = (size_t)1 << log_n;
+    gl_t w = gl_root_of_unity(log_n), ninv = gl_inv((gl_t)n);
+    glx_t *wt = malloc(n * sizeof(glx_t));
+    for (size_t k = 0; k < nx; k++) {
+        glx_t x = glx(xs[2 * k], xs[2 * k + 1]);
+        glx_t c = glx_scale(glx_sub(glx_exp_power_of_2(x, log_n), glx_from(1)), ninv);
+        gl_t wr = 1;
+        for (size_t r = 0; r < n; r++) {
+            wt[r] = glx_scale(glx_mul(c, glx_inv(glx_sub(x, glx_from(wr)))), wr);
+            wr = gl_mul(wr, w);
+        }
+        for (size_t col = 0; col < ncols; col++) {
+            glx_t acc = glx_from(0);
+            const uint64_t *v = vals + col * n;
+            for (size_t r = 0; r < n; r++)
+                if (v[r]) acc = glx_add(acc, glx_scale(wt[r], v[r]));
+            out[(col * nx + k) * 2] = acc.c0;
+            out[(col * nx + k) * 2 + 1] = acc.c1;
+        }
+    }
+    free(wt);
+}

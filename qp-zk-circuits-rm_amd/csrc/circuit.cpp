@@ -213,8 +213,15 @@ Target CircuitBuilder::is_equal(Target x, Target y) {
   Target diff = sub(x, y);
   Target not_equal_check = mul(equal, diff);
   Target eq_check = mul(diff, inv);
-  connect(not_equal_check, z);
   connect(eq_check, not_equal);
+  connect(not_equal_check, z);
+  // qp-plonky2 also range-checks `equal` as a bit (assert_bool: one more
+  // mul_sub op after the two products).  Pinned by the reference's current-
+  // circuit proofs: without it the fixture's PublicInputGate sits 181 rows
+  // (= 20 x 181 (1,-1) ops / 20 per gate) later than ours, and only this
+  // position of the op reproduces the fixture's constants columns
+  // (tools/layout_scan.py).
+  assert_bool(equal);
   return equal;
 }
 

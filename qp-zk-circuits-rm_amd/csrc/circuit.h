@@ -190,6 +190,8 @@ class CircuitBuilder {
   void connect(Target a, Target b);
   void connect_hashes(const std::vector<Target> &a, const std::vector<Target> &b);
   void assert_zero(Target t) { connect(t, zero()); }
+  // gadgets/range_check.rs assert_bool: b*b - b == 0
+  void assert_bool(Target b) { connect(mul_sub(b, b, b), zero()); }
 
   // plonky2 gadgets/arithmetic.rs
   Target arithmetic(F c0, F c1, Target m0, Target m1, Target addend);

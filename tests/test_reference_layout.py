@@ -1,0 +1,149 @@
+"""The native Wormhole circuit's preprocessing and witness against the
+reference's own current-circuit proofs (tests/golden/dummy_proof{,_zk}.bin,
+written by the Rust prover: wormhole/tests/src/prover/prover_tests.rs:56-82).
+
+Each proof opens every constants||sigmas and wire column at its 28 query
+points g * w_{2^16}^rev16(i) (g = 0xc65c18b67785d900, the qp-plonky2-field
+coset shift) and at zeta: 29 evaluations of a degree < 2^13 polynomial per
+column and proof, so equality at all of them is equality of the columns
+(a wrong column matches one random point with probability 2^13 / p).
+
+Pinned here:
+* the 4 constants columns (2 selectors, 2 gate constants) equal the
+  reference's: the gate kind and gate constants of every one of the 8192 rows,
+  hence plonky2's build order (user gadgets, PI hash, PublicInputGate at row
+  7039, ConstantGates in canonical constant order, Noop padding) and
+  qp-plonky2's is_equal (an assert_bool after the two products:
+  csrc/circuit.cpp is_equal);
+* the witness of CircuitInputs::test_inputs() (test-helpers/src/lib.rs:10-59)
+  equals the reference's in every Poseidon-only column (80..134: the gates'
+  round S-box inputs) and in every arithmetic-output column (3, 7, ..., 79),
+  at every row but the PublicInputGate row, whose unused wires the reference
+  fills with RandomValueGenerator values in both configs (different in the
+  two proofs).
+
+Not pinned: the sigma columns and the arithmetic input
+columns (4i, 4i+1, 4i+2) still differ from the reference's.
+"""
+import numpy as np
+import pytest
+
+from current_circuit_vd import current_circuit_verifier_data, parse_queries, query_indices
+from oracle_lib import P, golden, lib
+from test_oracle_golden import current_common_bytes
+from wormhole_inputs import test_inputs as reference_test_inputs
+
+GEN = 0xc65c18b67785d900
+LOG_N = 13
+N = 1 << LOG_N
+PI_ROW = 7039
+OPEN_OFF = 3 * 512          # openings follow the wires / zs / quotient caps
+NUM_CS = 84
+MATCHING_WIRE_COLS = [3] + list(range(7, 80, 4)) + list(range(80, 135))
+PROOFS = ["dummy_proof.bin", "dummy_proof_zk.bin"]
+
+
+def _rev(i, bits):
+    return int(format(i, f"0{bits}b")[::-1], 2)
+
+
+@pytest.fixture(scope="module")
+def points():
+    """per proof: (xs [m][2] ext points: 28 query points then zeta,
+    constants||sigmas values [m][84], wire values [m][135][2])"""
+    vd = current_circuit_verifier_data(current_common_bytes())[0]
+    L = lib()
+    w16 = int(L.ora_root_of_unity(16))
+    out = {}
+    for name in PROOFS:
+        pf = golden(name)
+        qs = parse_queries(pf)
+        xs = [(GEN * pow(w16, _rev(i, 16), P) % P, 0) for i in query_indices(name)]
+        ch = np.zeros(256, np.uint64)
+        L.ora_challenges(vd, len(vd), pf, len(pf), ch)
+        xs.append((int(ch[6]), int(ch[7])))
+        op = np.frombuffer(pf[OPEN_OFF:OPEN_OFF + 16 * (NUM_CS + 135)], np.uint64).reshape(-1, 2)
+        cs = [np.stack([q[0][0], np.zeros(NUM_CS, np.uint64)], 1) for q in qs] + [op[:NUM_CS]]
+        wires = [np.stack([q[1][0], np.zeros(135, np.uint64)], 1) for q in qs] + [op[NUM_CS:]]
+        out[name] = (np.array(xs, np.uint64), np.stack(cs), np.stack(wires))
+    return out
+
+
+def evaluate(cols, xs):
+    """[ncols][n] values -> [ncols][m][2] evaluations at ext points xs [m][2]"""
+    cols = np.ascontiguousarray(cols, np.uint64)
+    out = np.zeros(cols.shape[0] * len(xs) * 2, np.uint64)
+    lib().ora_eval_values(cols.reshape(-1), cols.shape[0], LOG_N, np.ascontiguousarray(xs).reshape(-1), len(xs), out)
+    return out.reshape(cols.shape[0], len(xs), 2)
+
+
+def _ext_mul(a, b):
+    return ((a[0] * b[0] + 7 * a[1] * b[1]) % P, (a[0] * b[1] + a[1] * b[0]) % P)
+
+
+def _ext_inv(a):
+    d = (a[0] * a[0] - 7 * a[1] * a[1]) % P
+    di = pow(d, P - 2, P)
+    return (a[0] * di % P, (P - a[1]) * di % P)
+
+
+@pytest.fixture(scope="module")
+def circuit():
+    from qp_wormhole import Circuit
+    return Circuit.wormhole(zero_knowledge=False)
+
+
+@pytest.mark.parametrize("name", PROOFS)
+def test_constants_columns_equal_the_reference(points, circuit, name):
+    xs, ref_cs, _ = points[name]
+    ours = evaluate(circuit.constants_sigmas()[:4], xs)
+    for c in range(4):
+        assert np.array_equal(ours[c], ref_cs[:, c]), f"constants column {c}"
+
+
+def test_public_input_gate_row(circuit):
+    sel0 = circuit.constants_sigmas()[0]
+    assert int(np.nonzero(sel0 == 2)[0][0]) == PI_ROW
+    # ConstantGates (selector value 1) right after it, Noop (0) padding after those
+    r = PI_ROW + 1
+    while sel0[r] == 1:
+        r += 1
+    assert r == PI_ROW + 1 + 93 and not sel0[r:].any()
+
+
+@pytest.mark.parametrize("name", PROOFS)
+def test_witness_equals_the_reference_outside_the_pi_row(points, circuit, name):
+    """ref - ours = delta_c * L_PI_ROW(x) at all 29 points, one delta per column."""
+    xs, _, ref_w = points[name]
+    wv = circuit.commit(reference_test_inputs()).wires()
+    ours = evaluate(wv[MATCHING_WIRE_COLS], xs)
+    unit = np.zeros((1, N), np.uint64)
+    unit[0, PI_ROW] = 1
+    lpi = evaluate(unit, xs)[0]
+    deltas = []
+    for k, col in enumerate(MATCHING_WIRE_COLS):
+        diff = [((int(ref_w[j, col, 0]) - int(ours[k, j, 0])) % P, (int(ref_w[j, col, 1]) - int(ours[k, j, 1])) % P)
+                for j in range(len(xs))]
+        delta = _ext_mul(diff[0], _ext_inv((int(lpi[0, 0]), int(lpi[0, 1]))))
+        assert delta[1] == 0, f"column {col}: PI-row value not in the base field"
+        for j in range(1, len(xs)):
+            assert diff[j] == _ext_mul(delta, (int(lpi[j, 0]), int(lpi[j, 1]))), f"column {col}, point {j}"
+        deltas.append(delta[0])
+    assert deltas[0] == 0  # column 3 of the PI row is a public-input-hash wire
+    assert all(deltas[1:])  # the reference's random PI-row cells (ours: zero)
+
+
+def test_pi_row_cells_differ_between_the_two_proofs(points, circuit):
+    """The PI row's random cells are fresh per proof (zk and non-zk alike)."""
+    wv = circuit.commit(reference_test_inputs()).wires()
+    col = 80
+    vals = []
+    for name in PROOFS:
+        xs, _, ref_w = points[name]
+        unit = np.zeros((1, N), np.uint64)
+        unit[0, PI_ROW] = 1
+        lpi = evaluate(unit, xs[:1])[0, 0]
+        ours = evaluate(wv[col:col + 1], xs[:1])[0, 0]
+        d = ((int(ref_w[0, col, 0]) - int(ours[0])) % P, 0)
+        vals.append(_ext_mul(d, _ext_inv((int(lpi[0]), int(lpi[1]))))[0])
+    assert vals[0] != vals[1]

@@ -21,6 +21,7 @@ sys.path[:0] = [os.path.join(ROOT, "tests"), os.path.join(ROOT, "qp-zk-circuits-
 P = 0xFFFFFFFF00000001
 LOG_N = 13
 N = 1 << LOG_N
+GEN = 0xc65c18b67785d900  # coset shift (qp-plonky2-field multiplicative generator, oracle/gl.h GL_GEN)
 SO = "/tmp/liblsparse.so"
 U64P = np.ctypeslib.ndpointer(np.uint64, flags="C_CONTIGUOUS")
 
@@ -63,7 +64,7 @@ def fixture_points():
             if i in seen:
                 continue
             seen.add(i)
-            xs.append(7 * pow(w16, rev(i, 16), P) % P)
+            xs.append(GEN * pow(w16, rev(i, 16), P) % P)
             leaves.append(q[0][0])
     return np.array(xs, np.uint64), np.stack(leaves)
 
