@@ -120,11 +120,14 @@ typedef struct {
     const uint8_t *const *nodes;       /* node byte strings */
     const uint32_t *node_lens;
     const uint64_t *indices;           /* hex-character child-hash indices */
-    /* zk config only (NULL otherwise): values of the PublicInputGate row's
-     * unused wires 4..num_wires-1 (num_wires - 4 canonical felts), which the
-     * reference fills from RandomValueGenerator (plonky2 CircuitBuilder::build,
-     * randomize_unused_pi_wires).  NULL under zk = derived deterministically
-     * from the private inputs (a Poseidon nonce; see DESIGN.md "zk").        */
+    /* values of the PublicInputGate row's unused wires 4..num_wires-1
+     * (num_wires - 4 canonical felts), which the reference fills from
+     * RandomValueGenerator (plonky2 CircuitBuilder::build,
+     * randomize_unused_pi_wires; qp-plonky2 under both configs).  Passing the
+     * values a reference proof holds reproduces that proof's wires.  NULL =
+     * zeros under standard_recursion_config; under the zk config derived
+     * deterministically from the private inputs (a Poseidon nonce; DESIGN.md
+     * "zk").                                                                 */
     const uint64_t *zk_randomness;
 } qp_wormhole_inputs;
 
@@ -132,8 +135,10 @@ typedef struct {
  * wormhole/prover/src/lib.rs:190-202) — host part.  zero_knowledge selects
  * standard_recursion_zk_config vs standard_recursion_config.  Under the
  * workspace's `no_random` feature the two share the preprocessing and proof
- * shape (no salt columns; tests/test_current_circuit_fixture.py); zk adds the
- * PublicInputGate row's random cells (qp_wormhole_inputs.zk_randomness).   */
+ * shape (no salt columns; tests/test_current_circuit_fixture.py) and both
+ * fill the PublicInputGate row's spare cells (qp_wormhole_inputs.zk_randomness);
+ * the constants||sigmas columns equal the reference's
+ * (tests/test_reference_layout.py).                                        */
 int qp_wormhole_circuit_new(int zero_knowledge, qp_circuit **out);
 void qp_circuit_free(qp_circuit *c);
 /* info[0..6] = degree_bits, num_wires, num_routed_wires, num_constants,
@@ -237,6 +242,13 @@ int qp_prover_prove_wires_dev(qp_prover *p, const uint64_t *d_wires, const uint6
  * 1 = wires leaf hashing (units = permutations), 2 = wires Merkle levels
  * (units = permutations), 3 = quotient evaluation (units = LDE points)     */
 int qp_prover_set_timing(qp_prover *p, int enable);
+/* TEST-ONLY: use `witness` as every proof's FRI proof-of-work witness instead
+ * of grinding the minimal one (enable = 0 restores grinding).  The reference's
+ * rayon find_any witness is nondeterministic, so reproducing one of its proofs
+ * byte for byte needs its witness (tests/test_gpu_reference_proof.py); a
+ * witness without the required leading zeros gives a proof that fails
+ * verification.                                                            */
+int qp_prover_debug_force_pow(qp_prover *p, uint64_t witness, int enable);
 /* host threads (the caller included) of the prover's pool for commit() and the
  * per-proof host stages; default min(hardware threads, 16).  Several provers in
  * one process should split the host cores (cores / provers each).           */

@@ -15,6 +15,18 @@
  * Reference call site: WormholeProver::prove (wormhole/prover/src/lib.rs:233-237).
  */
 #include "plonk.h"
+
+/* Test-only: force the PoW witness instead of grinding for the minimal one.
+ * The reference's find_any witness is nondeterministic, so
+ * reproducing one of its proofs byte for byte needs its witness; the
+ * transcript checks it like any other (ora_verify). */
+static int or_pow_forced_on = 0;
+static gl_t or_pow_forced = 0;
+void ora_force_pow_witness(uint64_t w, int on) {
+    or_pow_forced = w;
+    or_pow_forced_on = on;
+}
+
 #include "poseidon.h"
 #include "fft.h"
 #include "merkle.h"
@@ -363,8 +375,12 @@ int or_prove(const uint8_t *common_bytes, size_t clen, const gl_t *consts_sigmas
     free(fin);
     for (unsigned i = 0; i < d.final_poly_len; i++) or_chal_observe_ext(&t, p->final_poly[i]);
 
-    /* 6. proof of work: minimal witness */
-    {
+    /* 6. proof of work: minimal witness (or the forced one, test-only) */
+    if (or_pow_forced_on) {
+        p->pow_witness = or_pow_forced;
+        or_chal_observe(&t, or_pow_forced);
+        (void)or_chal_get(&t);
+    } else {
         gl_t st[12];
         memcpy(st, t.state, sizeof(st));
         for (unsigned i = 0; i < t.nin; i++) st[i] = t.in[i];

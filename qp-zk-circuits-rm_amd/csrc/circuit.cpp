@@ -212,16 +212,16 @@ Target CircuitBuilder::is_equal(Target x, Target y) {
   gens_.push_back(g);
   Target diff = sub(x, y);
   Target not_equal_check = mul(equal, diff);
-  Target eq_check = mul(diff, inv);
-  connect(eq_check, not_equal);
+  Target diff_normalized = mul(diff, inv);
   connect(not_equal_check, z);
-  // qp-plonky2 also range-checks `equal` as a bit (assert_bool: one more
-  // mul_sub op after the two products).  Pinned by the reference's current-
-  // circuit proofs: without it the fixture's PublicInputGate sits 181 rows
-  // (= 20 x 181 (1,-1) ops / 20 per gate) later than ours, and only this
-  // position of the op reproduces the fixture's constants columns
-  // (tools/layout_scan.py).
-  assert_bool(equal);
+  // qp-plonky2 checks diff * inv == not_equal with an arithmetic op
+  // (diff_normalized - not_equal == 0) instead of upstream's copy constraint.
+  // Pinned by the reference's current-circuit proofs (tests/test_reference_layout.py):
+  // the extra (1,-1) op puts the fixture's PublicInputGate at row 7039 (181 ops
+  // per storage node later than without it), its cells hold
+  // (diff_normalized, 1, not_equal) -- (1-eq, 1, 1-eq) in the fixture's wire
+  // openings -- and only this routing gives the fixture's 80 sigma columns.
+  connect(sub(diff_normalized, not_equal), z);
   return equal;
 }
 
@@ -325,11 +325,12 @@ CircuitData CircuitBuilder::build() {
   auto pih = hash_n_to_hash_no_pad(public_inputs_);
   uint32_t pi_row = add_gate(G_PUBLIC_INPUT);
   for (uint32_t i = 0; i < 4; i++) connect(pih[i], Target::wire(pi_row, i));
-  // randomize_unused_pi_wires: under the zk config the remaining wires of the
-  // PublicInputGate row carry random values; they are inputs of commit() here
+  // randomize_unused_pi_wires: the remaining wires of the PublicInputGate row
+  // carry random values -- in qp-plonky2 under both configs (the reference's
+  // non-zk dummy_proof.bin has them too: tests/test_reference_layout.py); they
+  // are inputs of commit() here
   std::vector<Target> zk_cells;
-  if (cfg_.zero_knowledge)
-    for (uint32_t j = 4; j < cfg_.num_wires; j++) zk_cells.push_back(Target::wire(pi_row, j));
+  for (uint32_t j = 4; j < cfg_.num_wires; j++) zk_cells.push_back(Target::wire(pi_row, j));
   mark_inputs(zk_cells);
   // constant gates: cfg.num_constants constants per ConstantGate row, in
   // ascending canonical value (plonky2 build(): constants_to_targets

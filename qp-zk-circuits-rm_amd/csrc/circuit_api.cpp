@@ -9,23 +9,26 @@
 #include "circuit_obj.h"
 #include "host_util.h"
 
-// zk config: the PublicInputGate row's unused wires (plonky2 randomize_unused_pi_wires
-// -> RandomValueGenerator).  `given` holds num_wires - 4 canonical values; when it is
-// null they are derived as hash_n_to_m_no_pad(domain tag || private felts): a
-// deterministic nonce that hides like fresh randomness while the private inputs
-// stay secret, so the proof remains a pure function of the inputs.
+// The PublicInputGate row's unused wires (plonky2 randomize_unused_pi_wires ->
+// RandomValueGenerator; qp-plonky2 fills them under both configs).  `given`
+// holds num_wires - 4 canonical values (e.g. the reference's own, to reproduce
+// one of its proofs byte for byte).  When it is null: zeros under the non-zk
+// config (no hiding is claimed there); under the zk config
+// hash_n_to_m_no_pad(domain tag || private felts), a deterministic nonce that
+// hides like fresh randomness while the private inputs stay secret, so the
+// proof remains a pure function of the inputs.
 static std::string zk_fill(const qc::CircuitData &cd, const uint64_t *given, const std::vector<uint64_t> &priv,
                            qc::Witness &w, int *code) {
   *code = QP_ERR_ARG;
   const size_t m = cd.zk_slots.size();
-  if (!m) return given ? "zk randomness given for a circuit built without zero_knowledge" : "";
-  std::vector<uint64_t> v(m);
+  if (!m) return "";
+  std::vector<uint64_t> v(m, 0);
   if (given) {
     for (size_t i = 0; i < m; i++) {
       if (given[i] >= gl::P) return "zk randomness value " + std::to_string(i) + " is not a canonical field element";
       v[i] = given[i];
     }
-  } else {
+  } else if (cd.config.zero_knowledge) {
     std::vector<uint64_t> in = {0x6b7a2d626c696e64ull % gl::P /* "zk-blind" */, (uint64_t)m};
     in.insert(in.end(), priv.begin(), priv.end());
     uint64_t st[12] = {0};

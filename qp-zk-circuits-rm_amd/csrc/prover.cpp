@@ -93,6 +93,8 @@ struct qp_prover {
   uint32_t max_batch = 0;
   uint32_t log_n = 0, rate_bits = 0, cap_h = 0, W = 0, R = 0, NC = 0, nc = 0, npp = 0, qdf = 0, nchunks = 0;
   uint32_t nq = 0, pow_bits = 0, npis = 0;
+  bool pow_forced = false;  // test-only: qp_prover_debug_force_pow
+  uint64_t pow_forced_witness = 0;
   std::vector<uint32_t> arity;
   uint32_t final_len = 0;
   uint64_t cs_cap[64 * 4] = {0};
@@ -751,7 +753,13 @@ int prove_batch(qp_prover *P, const uint64_t *d_wires, const uint64_t *const *wi
   TRY(hipMemcpyAsync(P->pow_state.p, P->h_powst.data(), (size_t)nb * 192, hipMemcpyHostToDevice, s));
   TRY(hipMemcpyAsync(P->pow_pos.p, P->h_pos.data(), (size_t)nb * 4, hipMemcpyHostToDevice, s));
   TRY(hipMemsetAsync(P->pow_found.p, 0xFF, (size_t)nb * 8, s));
-  {
+  if (P->pow_forced) {
+    // test-only: the given witness for every proof (reproducing a reference
+    // proof, whose find_any witness is nondeterministic); the transcript and
+    // any verifier check it like a ground one
+    TRY(hipStreamSynchronize(s));
+    for (uint32_t b = 0; b < nb; b++) P->h_found[b] = P->pow_forced_witness;
+  } else {
 #if QP_POW_SCAN
     // Minimal witness per proof in one launch (k_pow_scan): 2048 workgroups
     // claim 256-candidate blocks from per-proof counters, moving on to the
@@ -1193,6 +1201,13 @@ int qp_prover_prove_voting_inputs(qp_prover *P, const qp_voting_inputs *in, uint
   } catch (const std::bad_alloc &) {
     return QP_ERR_OOM;
   }
+}
+
+int qp_prover_debug_force_pow(qp_prover *P, uint64_t witness, int enable) {
+  if (!P) return QP_ERR_ARG;
+  P->pow_forced = enable != 0;
+  P->pow_forced_witness = witness;
+  return QP_OK;
 }
 
 int qp_prover_set_timing(qp_prover *P, int enable) {

@@ -135,6 +135,7 @@ def lib():
         "qp_prover_prove_voting_inputs": (ctypes.c_int, [VP, VP, ctypes.c_uint32, ctypes.c_char_p, ctypes.c_size_t,
                                                          ctypes.POINTER(ctypes.c_size_t)]),
         "qp_prover_set_timing": (ctypes.c_int, [VP, ctypes.c_int]),
+        "qp_prover_debug_force_pow": (ctypes.c_int, [VP, ctypes.c_uint64, ctypes.c_int]),
         "qp_prover_set_host_threads": (ctypes.c_int, [VP, ctypes.c_uint32]),
         "qp_prover_kernel_stats": (ctypes.c_int, [VP, ctypes.POINTER(ctypes.c_double), ctypes.POINTER(ctypes.c_double),
                                                   ctypes.POINTER(ctypes.c_uint64), ctypes.c_uint32, ctypes.c_int]),

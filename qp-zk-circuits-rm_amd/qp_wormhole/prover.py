@@ -109,6 +109,12 @@ class Prover:
     def set_timing(self, enable=True):
         lib().qp_prover_set_timing(self.h, int(enable))
 
+    def debug_force_pow(self, witness, enable=True):
+        """TEST-ONLY (qp_prover_debug_force_pow): every proof's PoW witness is
+        `witness` instead of the minimal one -- how a reference proof, whose
+        find_any witness is nondeterministic, is reproduced byte for byte."""
+        self.ctx.check(lib().qp_prover_debug_force_pow(self.h, int(witness), int(enable)), "qp_prover_debug_force_pow")
+
     def set_host_threads(self, nthreads):
         """Host threads (caller included) of this prover's pool: several provers in
         one process split the host cores instead of each taking min(cores, 16)."""

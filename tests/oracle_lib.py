@@ -63,6 +63,7 @@ def lib():
         L.ora_gate_eval.restype = ctypes.c_long
         L.ora_gate_eval.argtypes = [ctypes.c_void_p, ctypes.c_uint, U64P, U64P, U64P, U64P]
         L.ora_eval_values.argtypes = [U64P, ctypes.c_size_t, ctypes.c_uint, U64P, ctypes.c_size_t, U64P]
+        L.ora_force_pow_witness.argtypes = [ctypes.c_uint64, ctypes.c_int]
         L.ora_pow_grind.restype = ctypes.c_uint64
         L.ora_pow_grind.argtypes = [U64P, ctypes.c_uint, ctypes.c_uint]
         _lib = L

@@ -1,19 +1,22 @@
 """The zk config (standard_recursion_zk_config, the reference prover's default:
-wormhole/circuit/src/circuit.rs:68-73) and its random witness cells.
+wormhole/circuit/src/circuit.rs:68-73) and the PublicInputGate row's random
+witness cells.
 
 What the reference's own fixtures say (wormhole/aggregator/data/dummy_proof{,_zk}.bin,
 proofs of the same test_inputs() under the two configs, prover_tests.rs:56-82):
 * the constants||sigmas commitment is shared (test_current_circuit_fixture.py), and
   neither proof has salt columns -- the preprocessing and proof shape are the same;
-* but the WIRES commitments differ: the zk prover writes different values into
-  cells no constraint pins.  plonky2's build() gives exactly one such set of cells
-  to RandomValueGenerators without touching the preprocessing: the PublicInputGate
-  row's unused wires 4..num_wires-1 (randomize_unused_pi_wires).
+* the witnesses are equal except for the PublicInputGate row's unused wires
+  4..num_wires-1, which the reference fills from RandomValueGenerators
+  (randomize_unused_pi_wires) under BOTH configs, with different values in the
+  two proofs (tests/test_reference_layout.py reads them out of the fixtures'
+  openings and reproduces both proofs byte for byte with them).
 
-So here those cells are an input of commit() (CircuitInputs.zk_randomness), and a
-proof stays a pure function of its inputs.  Which values the reference's
-`no_random` RNG produces is not derivable (no qp-plonky2 source): parity unpinned
-for those values; the GPU tests check GPU == oracle bytes for given values.
+So here those cells are an input of commit() (CircuitInputs.zk_randomness) in
+both configs, and a proof stays a pure function of its inputs.  Left out they
+are zeros under the non-zk config and a Poseidon nonce of the private inputs
+under the zk config (the reference's RNG output is not reproducible by
+construction).
 """
 import ctypes
 
@@ -103,10 +106,21 @@ def test_zk_randomness_rejected_when_invalid(circuits):
     import dataclasses
     from qp_wormhole import QpError
     nz, zk = circuits
-    with pytest.raises(QpError, match="non-zk|without zero_knowledge"):
-        nz.commit(dataclasses.replace(WI.test_inputs(), zk_randomness=[1] * (nz.num_wires - 4)))
-    with pytest.raises(QpError, match="canonical"):
-        zk.commit(dataclasses.replace(WI.test_inputs(), zk_randomness=[P] * (zk.num_wires - 4)))
+    for c in (nz, zk):
+        with pytest.raises(QpError, match="canonical"):
+            c.commit(dataclasses.replace(WI.test_inputs(), zk_randomness=[P] * (c.num_wires - 4)))
+
+
+def test_non_zk_config_takes_given_pi_row_cells(circuits):
+    """The reference's non-zk proofs carry random PI-row cells too."""
+    import dataclasses
+    nz, _ = circuits
+    r = [(0x0fed_cba9_8765_4321 * (i + 3)) % P for i in range(nz.num_wires - 4)]
+    w = nz.commit(dataclasses.replace(WI.test_inputs(), zk_randomness=r))
+    row = _pi_row(nz)
+    assert [int(x) for x in w.wires()[4:, row]] == r
+    assert not nz.commit(WI.test_inputs()).wires()[4:, row].any()   # default: zeros
+    assert _check(nz, w) == -1
 
 
 def test_voting_zk_cells(circuits):
