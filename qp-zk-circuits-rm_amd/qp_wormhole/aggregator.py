@@ -18,6 +18,7 @@ device preprocessing are built once per (inner circuit, branching) and cached.
 The aggregation circuit is parity-unpinned: the reference commits no
 aggregated proof.
 """
+import os
 import struct
 import threading
 from dataclasses import dataclass
@@ -220,17 +221,26 @@ class WormholeProofAggregator:
         self.proofs_buffer.append(_as_proof(proof))
 
     def dummy_proof(self) -> ProofWithPublicInputs:
-        """The padding proof (util.rs:6-9 embeds the reference's proof of its test
-        inputs, which verifies only under the reference's own circuit): unless one is
-        passed in, a proof of this leaf circuit on the deterministic synthetic input
-        0 with an empty storage proof (SURVEY.md 8(d) variant A)."""
+        """The padding proof: util.rs:6-9 embeds the reference's own proof of its
+        test inputs (dummy_proof_zk.bin, or dummy_proof.bin under the `no_zk`
+        feature).  This library's Wormhole leaf circuit IS the reference's
+        (same constants||sigmas cap and circuit digest: tests/test_reference_layout.py),
+        so the same bytes are embedded here (qp_wormhole/data/, copied by
+        tests/golden/make_golden.py) and verify under the leaf verifier data."""
         if self._dummy is None:
-            from .prover import CONFIGS, WormholeProver, _config_of_common
-            from .synthetic import synthetic_inputs
+            from .prover import CONFIGS, _config_of_common
             cfg = _config_of_common(self.leaf_circuit_data.common)
             if cfg not in CONFIGS:
                 raise ValueError("no dummy proof for this leaf circuit: pass dummy_proof=")
-            self._dummy = WormholeProver(cfg, self.device).commit(synthetic_inputs(0, 0)).prove()
+            name = "dummy_proof_zk.bin" if cfg == "standard_recursion_zk_config" else "dummy_proof.bin"
+            with open(os.path.join(os.path.dirname(os.path.abspath(__file__)), "data", name), "rb") as f:
+                data = f.read()
+            # the proof ends with num_public_inputs (u64) and the public inputs
+            npis, = struct.unpack_from("<Q", data, len(data) - 8 * (LEAF_PI_LEN + 1))
+            if npis != LEAF_PI_LEN:
+                raise ValueError(f"dummy proof {name}: {npis} public inputs, expected {LEAF_PI_LEN}")
+            self._dummy = ProofWithPublicInputs(data, struct.unpack_from(f"<{LEAF_PI_LEN}Q", data,
+                                                                         len(data) - 8 * LEAF_PI_LEN))
         return self._dummy
 
     def extract_leaf_public_inputs(self, aggr) -> List[PublicCircuitInputs]:

@@ -5,6 +5,8 @@ Run in the build container only (the GPU box has no /root/reference):
 Outputs (data only, no reference source):
   * common.bin, verifier.bin, proof.bin      <- wormhole/bench-data/*.bin
   * dummy_proof.bin, dummy_proof_zk.bin      <- wormhole/aggregator/data/*.bin
+    (also into qp-zk-circuits-rm_amd/qp_wormhole/data/: the aggregator's padding
+    proofs, as util.rs:6-9 include_bytes! them)
   * storage_proof.json <- the DEFAULT_STORAGE_PROOF node hex strings and indices of
     wormhole/tests/test-helpers/src/lib.rs:64-80 (test input data)
 """
@@ -15,6 +17,7 @@ import shutil
 
 REF = "/root/reference"
 HERE = os.path.dirname(os.path.abspath(__file__))
+PKG_DATA = os.path.join(HERE, "..", "..", "qp-zk-circuits-rm_amd", "qp_wormhole", "data")
 
 
 def main():
@@ -22,6 +25,8 @@ def main():
                        ("wormhole/aggregator/data", ["dummy_proof.bin", "dummy_proof_zk.bin"])):
         for n in names:
             shutil.copyfile(os.path.join(REF, sub, n), os.path.join(HERE, n))
+            if n.startswith("dummy_proof"):
+                shutil.copyfile(os.path.join(REF, sub, n), os.path.join(PKG_DATA, n))
     src = open(os.path.join(REF, "wormhole/tests/test-helpers/src/lib.rs")).read()
     block = src[src.index("DEFAULT_STORAGE_PROOF: [&str; 7]"):]
     block = block[:block.index("];")]

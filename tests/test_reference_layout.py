@@ -9,28 +9,24 @@ column and proof, so equality at all of them is equality of the columns
 (a wrong column matches one random point with probability 2^13 / p).
 
 Pinned here:
-* the 4 constants columns (2 selectors, 2 gate constants) equal the
-  reference's: the gate kind and gate constants of every one of the 8192 rows,
-  hence plonky2's build order (user gadgets, PI hash, PublicInputGate at row
-  7039, ConstantGates in canonical constant order, Noop padding) and
-  qp-plonky2's is_equal (an assert_bool after the two products:
-  csrc/circuit.cpp is_equal);
+* the 4 constants columns (2 selectors, 2 gate constants) and the 80 sigma
+  columns equal the reference's: the gate kind and gate constants of every one
+  of the 8192 rows -- plonky2's build order (user gadgets, PI hash,
+  PublicInputGate at row 7039, ConstantGates in canonical constant order, Noop
+  padding) -- and the copy-constraint routing, including qp-plonky2's is_equal
+  (diff * inv == not_equal checked by a sub op connected to zero instead of
+  upstream's copy constraint: csrc/circuit.cpp is_equal); so the
+  constants||sigmas Merkle cap and the circuit digest are the reference's own,
+  and the reference's proofs verify under the library's verifier data;
 * the witness of CircuitInputs::test_inputs() (test-helpers/src/lib.rs:10-59)
-  equals the reference's in every Poseidon-only column (80..134: the gates'
-  round S-box inputs) and in every arithmetic-output column (3, 7, ..., 79),
-  at every row but the PublicInputGate row, whose unused wires the reference
-  fills with RandomValueGenerator values in both configs (different in the
-  two proofs).
-
-* all 80 sigma columns (the copy-constraint routing) equal the reference's
-  too -- qp-plonky2's is_equal checks diff * inv == not_equal with an
-  arithmetic op instead of a copy constraint -- so the constants||sigmas Merkle
-  cap and the circuit digest are the reference's own;
+  equals the reference's in all 135 columns at every row but the
+  PublicInputGate row, whose spare wires the reference fills with
+  RandomValueGenerator values in both configs (different in the two proofs);
 * with those cells taken from a reference proof and its PoW witness forced
   (find_any's witness is nondeterministic), the CPU oracle prover's bytes ARE
   the reference's proof, for both fixtures (the GPU prover is held to the
-  oracle's bytes by tests/test_gpu_prover.py and to the fixture itself by
-  tests/test_gpu_reference_proof.py).
+  fixtures themselves by tests/test_gpu_reference_proof.py);
+* the aggregator pads with the reference's own dummy proof (util.rs:6-9).
 """
 import numpy as np
 import pytest
@@ -126,7 +122,9 @@ def test_public_input_gate_row(circuit):
 def test_witness_equals_the_reference_outside_the_pi_row(points, circuit, name):
     """ref - ours = delta_c * L_PI_ROW(x) at all 29 points, one delta per column."""
     xs, _, ref_w = points[name]
-    wv = circuit.commit(reference_test_inputs()).wires()
+    inp = reference_test_inputs()
+    inp.zk_randomness = [0] * 131
+    wv = circuit.commit(inp).wires()
     ours = evaluate(wv[MATCHING_WIRE_COLS], xs)
     unit = np.zeros((1, N), np.uint64)
     unit[0, PI_ROW] = 1
@@ -146,7 +144,9 @@ def test_witness_equals_the_reference_outside_the_pi_row(points, circuit, name):
 
 def test_pi_row_cells_differ_between_the_two_proofs(points, circuit):
     """The PI row's random cells are fresh per proof (zk and non-zk alike)."""
-    wv = circuit.commit(reference_test_inputs()).wires()
+    inp = reference_test_inputs()
+    inp.zk_randomness = [0] * 131
+    wv = circuit.commit(inp).wires()
     col = 80
     vals = []
     for name in PROOFS:
@@ -225,3 +225,32 @@ def test_oracle_prover_reproduces_the_reference_proof(points, name):
     assert np.array_equal(cap.reshape(16, 4), ref_cap)
     assert np.array_equal(dig, ref_dig)
     assert proof == golden(name)
+
+
+@pytest.mark.parametrize("name", PROOFS)
+def test_reference_proofs_verify_under_the_library_verifier_data(name):
+    """VerifierOnlyCircuitData assembled from the native circuit alone (oracle
+    commit of its constants||sigmas, circuit digest) accepts the reference's
+    proofs -- what the aggregator's padding with them relies on."""
+    import struct
+    from qp_wormhole import Circuit
+    circ = Circuit.wormhole(zero_knowledge=name.endswith("_zk.bin"))
+    cs = np.ascontiguousarray(circ.constants_sigmas(), np.uint64)
+    cap = np.zeros(64, np.uint64)
+    assert lib().ora_commit_values(cs.reshape(-1), NUM_CS, LOG_N, 3, 4, None, 0, 0, None, None, cap) == 0
+    dig = np.zeros(4, np.uint64)
+    lib().ora_circuit_digest(cap, 16, LOG_N, dig)
+    vd = struct.pack("<Q", 4) + cap.tobytes() + dig.tobytes() + circ.common_data()
+    pf = golden(name)
+    assert lib().ora_verify(vd, len(vd), pf, len(pf)) == 0
+
+
+def test_aggregator_pads_with_the_reference_dummy_proof():
+    """util.rs:6-9: the padding proof is the reference's own (zk unless no_zk)."""
+    from qp_wormhole.aggregator import CircuitData, WormholeProofAggregator
+    from qp_wormhole import Circuit
+    for zk, name in ((True, "dummy_proof_zk.bin"), (False, "dummy_proof.bin")):
+        agg = WormholeProofAggregator(CircuitData(Circuit.wormhole(zero_knowledge=zk).common_data(), b""))
+        d = agg.dummy_proof()
+        assert d.to_bytes() == golden(name)
+        assert len(d.public_inputs) == 16
