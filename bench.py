@@ -169,6 +169,31 @@ def cpu_baseline(circuit, wires, pis, sample, min_seconds):
                       f"oracle/prover.c, {dt:.1f} s"}
 
 
+def reference_parity(qp_wormhole, device):
+    """The reference's own current-circuit proofs (tests/golden/dummy_proof{,_zk}.bin)
+    reproduced byte for byte by the GPU prover: test_inputs() with the proofs'
+    PublicInputGate-row cells and PoW witness (tests/golden/reference_pi_cells.json,
+    derived from the fixtures by tests/golden/make_pi_cells.py)."""
+    import wormhole_inputs
+    cells = load_json(os.path.join(ROOT, "tests", "golden", "reference_pi_cells.json"))
+    if not cells:
+        return None
+    out = {}
+    for name in ("dummy_proof.bin", "dummy_proof_zk.bin"):
+        with open(os.path.join(ROOT, "tests", "golden", name), "rb") as f:
+            ref = f.read()
+        circ = qp_wormhole.Circuit.wormhole(zero_knowledge=name.endswith("_zk.bin"))
+        p = qp_wormhole.Prover(qp_wormhole.Context(device), circ, max_batch=1)
+        inp = wormhole_inputs.test_inputs()
+        inp.zk_randomness = cells[name]["pi_row_cells"]
+        p.debug_force_pow(cells[name]["pow_witness"])
+        out[name] = p.prove_inputs([inp])[0] == ref
+        p.free()
+    out["note"] = ("GPU proof bytes == the reference's own proof of test_inputs() given its PI-row random cells "
+                   "and PoW witness (its find_any witness is nondeterministic); after the timed region")
+    return out
+
+
 def main():
     args = parse()
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -326,6 +351,9 @@ def main():
         zk = {"proofs_per_s_1prover": per[0] / zdt, "proofs_per_launch": per[0], "proof_verified": zok,
               "note": "standard_recursion_zk_config, e2e, one prover (the headline runs --provers, default 3)"}
         zp.free()
+    ref_parity = None
+    if rank == 0 and not voting and args.mode == "e2e":
+        ref_parity = reference_parity(qp_wormhole, local)
     if rank == 0:
         total = world * B * args.steps
         lde = ks["lde_wires"]
@@ -379,6 +407,7 @@ def main():
             "aggregation": agg,
             "prove_only_1prover_proofs_per_s": prove_only,
             "warmup_proof_verified": verified,
+            "reference_proof_bytes_equal": ref_parity,
         }
         if iso is not None and iso["lde_wires"]["ms"]:
             # with concurrent provers a launch's event-to-event time includes the

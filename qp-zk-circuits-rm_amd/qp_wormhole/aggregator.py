@@ -84,17 +84,39 @@ class _LevelProver:
         self.lock = threading.Lock()
 
     def prove_chunks(self, chunks, inner_vo: bytes) -> List[AggregatedProof]:
-        # aggregate_chunk's witnesses (host), then one batched prove per max_batch
-        witnesses = [self.circuit.commit_proofs(inner_vo, [p.to_bytes() for p in ch]) for ch in chunks]
+        # aggregate_chunk's witnesses on host threads (the C call releases the GIL;
+        # ~50 ms each for two leaves), each max_batch group proven on the GPU as
+        # soon as its witnesses exist while the next group's are generated
+        def commit(ch):
+            return self.circuit.commit_proofs(inner_vo, [p.to_bytes() for p in ch])
+
+        futs = [_witness_pool().submit(commit, ch) for ch in chunks]
         out = []
-        with self.lock:
-            for i in range(0, len(witnesses), self.max_batch):
-                ws = witnesses[i:i + self.max_batch]
-                for w, data in zip(ws, self.prover.prove_witnesses(ws)):
-                    out.append(AggregatedProof(ProofWithPublicInputs(data, w.public_inputs()), self.data))
-        for w in witnesses:
-            w.free()
+        try:
+            with self.lock:
+                for i in range(0, len(futs), self.max_batch):
+                    ws = [f.result() for f in futs[i:i + self.max_batch]]
+                    for w, data in zip(ws, self.prover.prove_witnesses(ws)):
+                        out.append(AggregatedProof(ProofWithPublicInputs(data, w.public_inputs()), self.data))
+        finally:
+            for f in futs:
+                if f.done() and f.exception() is None:
+                    f.result().free()
         return out
+
+
+_pool = None
+
+
+def _witness_pool():
+    """Host threads for aggregation witnesses: QP_AGG_THREADS, else the
+    process's CPU budget (OMP_NUM_THREADS on the GPU boxes), at most 16."""
+    global _pool
+    if _pool is None:
+        import concurrent.futures
+        n = int(os.environ.get("QP_AGG_THREADS") or os.environ.get("OMP_NUM_THREADS") or min(os.cpu_count() or 4, 16))
+        _pool = concurrent.futures.ThreadPoolExecutor(max_workers=max(1, min(n, 16)))
+    return _pool
 
 
 _levels = {}

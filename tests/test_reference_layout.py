@@ -254,3 +254,15 @@ def test_aggregator_pads_with_the_reference_dummy_proof():
         d = agg.dummy_proof()
         assert d.to_bytes() == golden(name)
         assert len(d.public_inputs) == 16
+
+
+def test_committed_pi_cells_fixture_is_current():
+    """tests/golden/reference_pi_cells.json (what bench.py's parity check and the
+    GPU test read) equals a fresh derivation from the fixtures."""
+    import json
+    import os
+    import sys
+    sys.path.insert(0, os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden"))
+    from make_pi_cells import cells
+    with open(os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden", "reference_pi_cells.json")) as f:
+        assert json.load(f) == json.loads(json.dumps(cells()))
