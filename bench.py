@@ -315,7 +315,7 @@ def main():
         vo = vd[:len(vd) - len(cb)]
         nl = min(args.agg_leaves, len(proofs)) // 2 * 2
         cfg2 = TreeAggregationConfig.new(2, 1)
-        aggregate_level(proofs[:2], cb, vo, cfg2)  # circuit build + device preprocessing (cached)
+        aggregate_level(proofs[:nl], cb, vo, cfg2)  # circuit build + device preprocessing at this batch (cached)
         t1 = time.perf_counter()
         level = aggregate_level(proofs[:nl], cb, vo, cfg2)
         lvl_s = time.perf_counter() - t1

@@ -155,7 +155,9 @@ def aggregate_level(proofs, common_data: bytes, verifier_only: bytes, config: Tr
     if len(proofs) % k:
         raise ValueError(f"{len(proofs)} proofs do not split into chunks of {k}")
     chunks = [proofs[i:i + k] for i in range(0, len(proofs), k)]
-    lp = (backend or _level_prover)(common_data, k, device, max(1, min(len(chunks), 16)))
+    # up to 32 aggregation proofs per GPU batch (2.7 vs 3.2 ms per proof at 16;
+    # tools/agg_bench.py, profiles/r03_agg_bench.log)
+    lp = (backend or _level_prover)(common_data, k, device, max(1, min(len(chunks), 32)))
     return lp.prove_chunks(chunks, verifier_only)
 
 
