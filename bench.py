@@ -106,6 +106,9 @@ def parse():
                          "cores (OMP_NUM_THREADS, else min(cores, 16)) between the provers")
     ap.add_argument("--agg-leaves", type=int, default=64,
                     help="leaf proofs aggregated (one level, pairs) after the timed region (0 = skip)")
+    ap.add_argument("--subtree", type=int, default=1,
+                    help="after the timed region, aggregate the GPU's batch of leaf proofs (largest power of two) "
+                         "into one subtree root and time it (configs[3]'s per-GPU share; 0 = skip)")
     ap.add_argument("--cpu-sample", type=int, default=2, help="min proofs in the CPU baseline sample (0 = skip)")
     ap.add_argument("--cpu-seconds", type=float, default=10.0, help="min seconds of CPU baseline proving")
     return ap.parse_args()
@@ -323,13 +326,27 @@ def main():
         t1 = time.perf_counter()
         root = aggregate_to_tree(proofs[:8], cb, vo)
         tree_ms = (time.perf_counter() - t1) * 1e3
+        # configs[3]'s per-GPU share: this GPU's whole batch of leaf proofs ->
+        # one subtree root (the levels of tree.rs:92-103; only the roots of the
+        # GPUs' subtrees would cross xGMI), timed end to end
+        sub = None
+        if args.subtree:
+            ns = 1 << (min(len(proofs), B).bit_length() - 1)
+            aggregate_to_tree(proofs[:ns], cb, vo, TreeAggregationConfig.new(2, ns.bit_length() - 1))  # warm caches
+            t1 = time.perf_counter()
+            sroot = aggregate_to_tree(proofs[:ns], cb, vo, TreeAggregationConfig.new(2, ns.bit_length() - 1))
+            sub_s = time.perf_counter() - t1
+            srvd, srp = sroot.circuit_data.verifier_data(), sroot.proof.to_bytes()
+            sub = {"leaves": ns, "aggregation_proofs": ns - 1, "seconds": sub_s,
+                   "aggregation_proofs_per_s": (ns - 1) / sub_s,
+                   "root_verified": olib().ora_verify(srvd, len(srvd), srp, len(srp)) == 0}
         rvd = root.circuit_data.verifier_data()
         rp = root.proof.to_bytes()
         agg = {"level_leaves": nl, "level_aggregation_proofs": len(level),
                "aggregation_proofs_per_s": len(level) / lvl_s, "leaves_per_s_through_one_level": nl / lvl_s,
                "tree8_root_ms": tree_ms, "root_verified": olib().ora_verify(rvd, len(rvd), rp, len(rp)) == 0,
                "aggregation_circuit_degree_bits": _common_degree_bits(root.circuit_data.common),
-               "proof_bytes": len(rp),
+               "proof_bytes": len(rp), "subtree_to_root": sub,
                "note": "aggregate_chunk circuits (native recursive verifier of 2 proofs, degree 2^14), host "
                        "witness generation + batched GPU prove; one level = nl/2 chunks; tree = 4+2+1 proofs"}
     # standard_recursion_zk_config (the reference's cargo-bench and aggregator config):
