@@ -379,10 +379,6 @@ int setup(qp_prover *P) {
     };
     P->wg_nslots = cd.num_slots;
     P->wg_nin = (uint32_t)cd.input_slots.size();
-    if (P->npis > 256) {
-      c->err = "too many public inputs for the device witness gather";
-      return QP_ERR_ARG;
-    }
     TRY(up32(P->wg_wslot_cm, cd.wire_slot_cm));
     TRY(up32(P->wg_pi_slots, cd.pi_slots));
     TRY(P->wg_vals.alloc((size_t)B * P->wg_nslots));

@@ -163,9 +163,12 @@ __global__ void k_witness_expand(const uint64_t *vals, uint64_t v_bstride, const
     const uint64_t x = v[wslot_cm[i]];
     wires[(uint64_t)b * w_bstride + i] = x == UNSET ? 0 : x;
   }
-  if (blockIdx.x == 0 && threadIdx.x < npis) {
-    const uint64_t x = v[pi_slots[threadIdx.x]];
-    pis[(uint64_t)b * npis + threadIdx.x] = x == UNSET ? 0 : x;
+  if (blockIdx.x == 0) {
+    // any number of public inputs (an aggregation root registers 16 per leaf)
+    for (uint32_t k = threadIdx.x; k < npis; k += blockDim.x) {
+      const uint64_t x = v[pi_slots[k]];
+      pis[(uint64_t)b * npis + k] = x == UNSET ? 0 : x;
+    }
   }
 }
 

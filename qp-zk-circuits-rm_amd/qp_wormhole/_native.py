@@ -116,7 +116,7 @@ def lib():
         "qp_aggregation_commit": (ctypes.c_int, [VP, ctypes.c_char_p, ctypes.c_size_t, VP, VP, ctypes.c_uint32,
                                                  VP, PP, ctypes.c_char_p, ctypes.c_size_t]),
         "qp_witness_wires": (ctypes.c_int, [VP, U64P]),
-        "qp_witness_public_inputs": (ctypes.c_int, [VP, U64P, ctypes.c_uint32, ctypes.POINTER(ctypes.c_uint32)]),
+        "qp_witness_public_inputs": (ctypes.c_int, [VP, VP, ctypes.c_uint32, ctypes.POINTER(ctypes.c_uint32)]),
         "qp_witness_free": (None, [VP]),
         "qp_hash_no_pad": (ctypes.c_int, [U64P, ctypes.c_size_t, U64P]),
         "qp_prover_new": (ctypes.c_int, [VP, VP, ctypes.c_uint32, PP]),

@@ -166,9 +166,12 @@ class Witness:
         return out
 
     def public_inputs(self):
-        out = np.zeros(256, np.uint64)
         n = ctypes.c_uint32()
-        rc = lib().qp_witness_public_inputs(self.h, out, 256, ctypes.byref(n))
+        rc = lib().qp_witness_public_inputs(self.h, None, 0, ctypes.byref(n))
+        if rc:
+            raise QpError(rc, "qp_witness_public_inputs")
+        out = np.zeros(max(n.value, 1), np.uint64)
+        rc = lib().qp_witness_public_inputs(self.h, out.ctypes.data, len(out), ctypes.byref(n))
         if rc:
             raise QpError(rc, "qp_witness_public_inputs")
         return out[:n.value].copy()

@@ -99,3 +99,20 @@ def test_tampered_leaf_is_rejected(reference_leaves):
     bad[3 * 512 + 84 * 16 + 7] ^= 1
     with pytest.raises(qp_wormhole.QpError, match="set twice"):
         qp_wormhole.aggregate_chunk([leaves[0], bytes(bad)], cb, vo)
+
+
+def test_deep_subtree_root_carries_every_leaf_public_input(reference_leaves):
+    """A subtree of 32 leaves (depth 5, as bench.py's per-GPU subtree): the
+    root's 512 public inputs (past the 256 the device gather once capped) are
+    the leaves' 16 each, in order, and the root verifies."""
+    import struct
+    import qp_wormhole
+    from qp_wormhole.aggregator import TreeAggregationConfig
+    cb, vo, leaves = reference_leaves
+    ls = [leaves[k % 2] for k in range(32)]
+    root = qp_wormhole.aggregate_to_tree(ls, cb, vo, TreeAggregationConfig.new(2, 5))
+    assert verify(root.circuit_data.verifier_data(), root.proof.to_bytes()) == 0
+    want = []
+    for pf in ls:
+        want += list(struct.unpack_from("<16Q", pf, len(pf) - 128))
+    assert root.proof.public_inputs == want
