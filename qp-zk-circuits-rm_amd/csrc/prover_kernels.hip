@@ -522,7 +522,14 @@ template <int PH>
 #ifndef QP_QUOTIENT_WAVES
 #define QP_QUOTIENT_WAVES 4
 #endif
-__global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(QP_QUOTIENT_WAVES))) k_quotient(QuotientArgs a) {
+// occupancy target of the generic (any gate list) kernel: at 4 waves/SIMD its
+// 128-VGPR budget spills ~400 B per lane for the aggregation circuits' gate set,
+// yet the spill-free 2-wave form (225 VGPRs) measured slower
+// (profiles/r03_ab_quotient_generic_waves.log)
+#ifndef QP_QGEN_WAVES
+#define QP_QGEN_WAVES QP_QUOTIENT_WAVES
+#endif
+__global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(QP_QGEN_WAVES))) k_quotient(QuotientArgs a) {
   const uint32_t logN = a.log_n + a.rate_bits;
   const uint64_t N = 1ull << logN;
   const uint32_t t = blockIdx.x * blockDim.x + threadIdx.x;
