@@ -257,7 +257,9 @@ void lde(const Twiddles &t, const uint64_t *coeffs, uint64_t c_stride, uint64_t 
          uint32_t ncols, uint32_t log_n, uint32_t rate_bits, uint64_t shift, uint32_t nbat, uint64_t c_bstride,
          uint64_t o_bstride, hipStream_t s) {
   if (!ncols || !nbat) return;
-  if (rate_bits >= 1 && rate_bits <= LDE_MAX_RATE && log_n >= 10 && log_n <= 13 && log_n + rate_bits <= TW_LOG &&
+  // n = 2^14 (the aggregation circuits): 1024 threads x 16 and 135 KB of LDS,
+  // one workgroup per CU
+  if (rate_bits >= 1 && rate_bits <= LDE_MAX_RATE && log_n >= 10 && log_n <= 14 && log_n + rate_bits <= TW_LOG &&
       !getenv_flag("QPGPU_LDE_PERCOSET")) {
     dim3 g(ncols, nbat);
     const size_t lds_bytes = (size_t)8 * qpk::ntt_lds_words(1u << log_n);
@@ -276,7 +278,8 @@ void lde(const Twiddles &t, const uint64_t *coeffs, uint64_t c_stride, uint64_t 
       case 10: QP_LDE_COSETS(6); break;
       case 11: QP_LDE_COSETS(7); break;
       case 12: QP_LDE_COSETS(8); break;
-      default: QP_LDE_COSETS(9); break;
+      case 13: QP_LDE_COSETS(9); break;
+      default: QP_LDE_COSETS(10); break;
     }
 #undef QP_LDE_COSETS
     return;
