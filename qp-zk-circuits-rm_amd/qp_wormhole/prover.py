@@ -175,6 +175,16 @@ CONFIGS = ("standard_recursion_config", "standard_recursion_zk_config")
 # common.bin, then the VerifierOnlyCircuitData bytes (constants||sigmas cap +
 # circuit digest).  Loading rebuilds the native circuit for that identity and
 # refuses data whose commitment differs.
+#
+# An upstream prover.bin (ProverOnlyCircuitData::to_bytes of the reference's
+# generate_circuit_binaries, circuit-builder/src/lib.rs:54-60) is accepted by
+# its circuit digest: plonky2 writes the digest (HashOut, 4 u64) right before
+# the lookup tables, which are two empty vectors (u64 length 0 each) for a
+# lookup-free circuit such as Wormhole, so the file ends with digest || 0u64 ||
+# 0u64.  The native circuit IS the reference's (same constants||sigmas cap and
+# circuit digest: tests/test_reference_layout.py), so an equal digest means the
+# file describes this circuit's preprocessing; its generators are not needed
+# (witness generation is native).
 PROVER_MAGIC = b"QPGPU-PROVER-ONLY\0"
 PROVER_VERSION = 1
 _KINDS = {"wormhole": 0, "voting": 1}
@@ -217,13 +227,31 @@ def prover_only_bytes(circuit, prover):
     return head + hashlib.sha256(common).digest() + _verifier_only(circuit, prover)
 
 
+def upstream_prover_digest(data):
+    """Circuit digest (4 u64) of an upstream ProverOnlyCircuitData::to_bytes file of a
+    lookup-free circuit, or None when `data` does not end like one."""
+    data = bytes(data)
+    if data[:len(PROVER_MAGIC)] == PROVER_MAGIC or len(data) < 8 + 48 or data[-16:] != bytes(16):
+        return None
+    (ngen,) = struct.unpack_from("<Q", data, 0)   # generators.len() opens the file
+    dig = struct.unpack_from("<4Q", data, len(data) - 48)
+    if not 0 < ngen < len(data) or any(x >= 0xFFFFFFFF00000001 for x in dig):
+        return None
+    return dig
+
+
 def _parse_prover_only(data, common_bytes):
+    """-> (zk, degree_bits, VerifierOnlyCircuitData bytes) for this backend's
+    prover.bin, or (None, None, circuit digest) for an upstream one."""
     data = bytes(data)
     n = len(PROVER_MAGIC)
+    if data[:n] != PROVER_MAGIC:
+        dig = upstream_prover_digest(data)
+        if dig is not None:
+            return None, None, dig
     if len(data) < n + 10 + 32 or data[:n] != PROVER_MAGIC:
-        raise ValueError("not this backend's prover.bin (bad magic): an upstream plonky2 "
-                         "ProverOnlyCircuitData::to_bytes file is not supported; regenerate it with "
-                         "generate_circuit_binaries")
+        raise ValueError("neither this backend's prover.bin (bad magic) nor an upstream plonky2 "
+                         "ProverOnlyCircuitData::to_bytes file of a lookup-free circuit")
     version, kind, zk, degree_bits = struct.unpack_from("<IBBI", data, n)
     if version != PROVER_VERSION:
         raise ValueError(f"unsupported version {version}")
@@ -242,6 +270,15 @@ def _parse_prover_only(data, common_bytes):
     if c_db is not None and c_db != degree_bits:
         raise ValueError(f"prover data header degree_bits {degree_bits} disagrees with the common data ({c_db})")
     return bool(zk), degree_bits, data[off + 32:]
+
+
+def _same_preprocessing(mine, parsed):
+    """This circuit's VerifierOnlyCircuitData bytes vs what a prover.bin holds:
+    the whole VerifierOnlyCircuitData (this backend's file) or the circuit
+    digest (an upstream file; the last 32 bytes of VerifierOnlyCircuitData)."""
+    if isinstance(parsed, tuple):
+        return struct.unpack_from("<4Q", mine, len(mine) - 32) == parsed
+    return mine == parsed
 
 
 def _common_degree_bits(cb):
@@ -300,7 +337,7 @@ class WormholeProver:
         self = cls(cfg, device)
         with self._prove_lock:
             mine = _verifier_only(self.circuit, self.prover)
-        if mine != vd:
+        if not _same_preprocessing(mine, vd):
             raise ValueError("Failed to deserialize prover only data: preprocessed commitment differs")
         return self
 
@@ -320,7 +357,7 @@ class WormholeProver:
             raise ValueError(f"Failed to deserialize prover only data from {str(prover_data_path)!r}: {e}") from None
         self = cls(cfg, device)
         with self._prove_lock:
-            if _verifier_only(self.circuit, self.prover) != vd:
+            if not _same_preprocessing(_verifier_only(self.circuit, self.prover), vd):
                 raise ValueError(f"Failed to deserialize prover only data from {str(prover_data_path)!r}: "
                                  "preprocessed commitment differs")
         return self
