@@ -38,7 +38,17 @@ struct Twiddles {
   uint64_t *ptw = nullptr;
   // the same for the radix-8 LDE: ptw8[8 (2^r - 2) + 8 s + m] = w_{8*2^r}^(s*m), m < 8
   uint64_t *ptw8 = nullptr;
+  // twiddles of the radix-16 LDS passes laid out per pass so a wave's lanes
+  // (consecutive t) read consecutive words: for S = 2^L, 4 <= L <= TW_LOG, at
+  // pt_offset(L): pt[m (S/16) + t] = w_S^(+-t brev4(m)), t < S/16, m < 16
+  uint64_t *pt_fwd = nullptr, *pt_inv = nullptr;
+  // merged first-pass twiddles of k_lde_cosets per (log_n, r), n = 16 T,
+  // N = n 2^r: at mtw_off[log_n][r], mtw[(16 s + m) T + t] = w_N^(t (s + 2^r brev4(m)))
+  uint64_t *mtw = nullptr;
+  uint64_t mtw_off[TW_LOG + 1][LDE_MAX_RATE + 1] = {};
 };
+__host__ __device__ constexpr uint32_t pt_offset(uint32_t log_S) { return (1u << log_S) - 16u; }
+constexpr uint32_t LDE_COSETS_MIN_LOG = 10, LDE_COSETS_MAX_LOG = 14;  // k_lde_cosets sizes
 __host__ __device__ inline uint32_t ptw_offset(uint32_t rate_bits) { return 16u * ((1u << rate_bits) - 2u); }
 __host__ __device__ inline uint32_t ptw8_offset(uint32_t rate_bits) { return 8u * ((1u << rate_bits) - 2u); }
 

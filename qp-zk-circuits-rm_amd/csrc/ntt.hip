@@ -46,6 +46,25 @@ __global__ void k_twiddles(uint64_t *fwd, uint64_t *inv, uint64_t w, uint64_t wi
   }
 }
 
+// pass twiddles (kernels.h Twiddles::pt_*): entry i of the concatenated
+// tables, looked up in the power table so the values are the ones the
+// gathers read before
+__global__ void k_pass_twiddles(uint64_t *pt, const uint64_t *__restrict__ tw, uint32_t total) {
+  const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= total) return;
+  const uint32_t L = 31 - __builtin_clz(i + 16u), loc = i + 16u - (1u << L), log_q = L - 4;
+  const uint32_t m = loc >> log_q, t = loc & ((1u << log_q) - 1);
+  pt[i] = nt::tw_pow(tw, t * nt::brev4(m), L);
+}
+
+// merged first-pass twiddles of k_lde_cosets for one (log_n, rate)
+__global__ void k_merged_twiddles(uint64_t *mtw, const uint64_t *__restrict__ tw, uint32_t log_n, uint32_t rate_bits) {
+  const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x, log_T = log_n - 4, logN = log_n + rate_bits;
+  if (i >= (1u << logN)) return;
+  const uint32_t t = i & ((1u << log_T) - 1), sm = i >> log_T, s = sm >> 4, m = sm & 15;
+  mtw[i] = nt::tw_pow(tw, t * (s + (nt::brev4(m) << rate_bits)), logN);
+}
+
 hipError_t twiddles_init(Twiddles &t, hipStream_t s) {
   uint32_t half = 1u << (TW_LOG - 1);
   hipError_t e = hipMalloc(&t.fwd, half * 8ull);
@@ -77,6 +96,21 @@ hipError_t twiddles_init(Twiddles &t, hipStream_t s) {
   if (e) return e;
   e = hipMemcpyAsync(t.ptw8, ptw8.data(), ptw8.size() * 8, hipMemcpyHostToDevice, s);
   if (e) return e;
+  const uint32_t npt = pt_offset(TW_LOG + 1);
+  if ((e = hipMalloc(&t.pt_fwd, npt * 8ull)) || (e = hipMalloc(&t.pt_inv, npt * 8ull))) return e;
+  k_pass_twiddles<<<(npt + 255) / 256, 256, 0, s>>>(t.pt_fwd, t.fwd, npt);
+  k_pass_twiddles<<<(npt + 255) / 256, 256, 0, s>>>(t.pt_inv, t.inv, npt);
+  uint64_t nm = 0;
+  for (uint32_t ln = LDE_COSETS_MIN_LOG; ln <= LDE_COSETS_MAX_LOG; ln++)
+    for (uint32_t r = 1; r <= LDE_MAX_RATE && ln + r <= TW_LOG; r++) {
+      t.mtw_off[ln][r] = nm;
+      nm += 1ull << (ln + r);
+    }
+  if ((e = hipMalloc(&t.mtw, nm * 8))) return e;
+  for (uint32_t ln = LDE_COSETS_MIN_LOG; ln <= LDE_COSETS_MAX_LOG; ln++)
+    for (uint32_t r = 1; r <= LDE_MAX_RATE && ln + r <= TW_LOG; r++)
+      k_merged_twiddles<<<((1u << (ln + r)) + 255) / 256, 256, 0, s>>>(t.mtw + t.mtw_off[ln][r], t.fwd, ln, r);
+  if ((e = hipGetLastError())) return e;
   return hipStreamSynchronize(s);
 }
 
@@ -85,12 +119,15 @@ void twiddles_free(Twiddles &t) {
   if (t.inv) (void)hipFree(t.inv);
   if (t.ptw) (void)hipFree(t.ptw);
   if (t.ptw8) (void)hipFree(t.ptw8);
-  t.fwd = t.inv = t.ptw = t.ptw8 = nullptr;
+  if (t.pt_fwd) (void)hipFree(t.pt_fwd);
+  if (t.pt_inv) (void)hipFree(t.pt_inv);
+  if (t.mtw) (void)hipFree(t.mtw);
+  t.fwd = t.inv = t.ptw = t.ptw8 = t.pt_fwd = t.pt_inv = t.mtw = nullptr;
 }
 
 __global__ void __launch_bounds__(512) QP_NTT_OCC k_intt(const uint64_t *__restrict__ in, uint64_t in_stride,
                                               uint64_t *__restrict__ out, uint64_t out_stride, uint32_t log_n,
-                                              uint64_t n_inv, const uint64_t *__restrict__ tw_inv,
+                                              uint64_t n_inv, const uint64_t *__restrict__ pt_inv,
                                               uint64_t in_bstride, uint64_t out_bstride) {
   extern __shared__ __attribute__((aligned(16))) uint64_t lds[];
   const uint32_t n = 1u << log_n;
@@ -98,14 +135,14 @@ __global__ void __launch_bounds__(512) QP_NTT_OCC k_intt(const uint64_t *__restr
   uint64_t *dst = out + blockIdx.y * out_bstride + (uint64_t)blockIdx.x * out_stride;
   for (uint32_t i = threadIdx.x; i < n; i += blockDim.x) lds[nt::lp(i)] = src[i];
   __syncthreads();
-  nt::ntt_lds<true>(lds, log_n, tw_inv);
+  nt::ntt_lds<true>(lds, log_n, pt_inv);
   for (uint32_t m = threadIdx.x; m < n; m += blockDim.x) dst[m] = gl::mul(lds[nt::lp(gl::rev_bits(m, log_n))], n_inv);
 }
 
 __global__ void __launch_bounds__(512) QP_NTT_OCC k_lde(const uint64_t *__restrict__ coeffs, uint64_t c_stride,
                                              uint64_t *__restrict__ out, uint64_t o_stride, uint32_t log_n,
                                              uint32_t rate_bits, uint64_t shift, const uint64_t *__restrict__ tw,
-                                             uint64_t c_bstride, uint64_t o_bstride) {
+                                             const uint64_t *__restrict__ pt, uint64_t c_bstride, uint64_t o_bstride) {
   extern __shared__ __attribute__((aligned(16))) uint64_t lds[];
   const uint32_t n = 1u << log_n;
   const uint32_t s = blockIdx.x;        // coset index
@@ -123,7 +160,7 @@ __global__ void __launch_bounds__(512) QP_NTT_OCC k_lde(const uint64_t *__restri
     f = gl::mul(f, step);
   }
   __syncthreads();
-  nt::ntt_lds<false>(lds, log_n, tw);
+  nt::ntt_lds<false>(lds, log_n, pt);
   for (uint32_t p = threadIdx.x; p < n; p += blockDim.x) dst[p] = nt::canon(lds[nt::lp(p)]);
 }
 
@@ -142,7 +179,8 @@ __global__ void __launch_bounds__(1 << LOG_T) QP_NTT_OCC k_lde_cosets(const uint
                                                           uint64_t c_bstride, uint64_t *__restrict__ out,
                                                           uint64_t o_stride, uint64_t o_bstride, uint32_t rate_bits,
                                                           uint64_t shift, uint64_t shift_T,
-                                                          const uint64_t *__restrict__ tw,
+                                                          const uint64_t *__restrict__ mtw,
+                                                          const uint64_t *__restrict__ pt,
                                                           const uint64_t *__restrict__ ptw) {
   constexpr uint32_t T = 1u << LOG_T, LOG_N = LOG_T + 4;
   extern __shared__ __attribute__((aligned(16))) uint64_t lds[];
@@ -160,22 +198,24 @@ __global__ void __launch_bounds__(1 << LOG_T) QP_NTT_OCC k_lde_cosets(const uint
       f = nt::mul(f, shift_T);
     }
   }
-  const uint32_t logN = LOG_N + rate_bits, B = 1u << rate_bits;
-  const uint64_t *pt = ptw + ptw_offset(rate_bits);
+  const uint32_t B = 1u << rate_bits;
+  const uint64_t *pw = ptw + ptw_offset(rate_bits);
   for (uint32_t s = 0; s < B; s++) {
     uint64_t r[16];
     r[0] = a[0];
 #pragma unroll
-    for (int m = 1; m < 16; m++) r[m] = nt::mul(a[m], pt[16 * s + m]);
+    for (int m = 1; m < 16; m++) r[m] = nt::mul(a[m], pw[16 * s + m]);
     nt::dft16<false>(r);
+    // merged twiddles w_N^{t(s + B brev4(m))}: row (s, m) of the table, lane t
+    // (a product by w^0 = 1 returns its input unchanged)
+    const uint64_t *ms = mtw + (uint64_t)16 * T * s + t;
 #pragma unroll
     for (int m = 0; m < 16; m++) {
-      const uint32_t e = t * (s + (nt::brev4(m) << rate_bits));
-      if (e) r[m] = nt::mul(r[m], nt::tw_pow(tw, e, logN));
+      if (s || m) r[m] = nt::mul(r[m], ms[T * m]);
       lds[nt::lp(t) + nt::lp(T * m)] = r[m];
     }
     __syncthreads();
-    nt::ntt_lds_from<false>(lds, LOG_N, LOG_T, tw);
+    nt::ntt_lds_from<false>(lds, LOG_N, LOG_T, pt);
     uint64_t *dst = dst0 + ((uint64_t)gl::rev_bits(s, rate_bits) << LOG_N);
 #pragma unroll
     for (int m = 0; m < 16; m++) dst[t + T * m] = nt::canon(lds[nt::lp(t) + nt::lp(T * m)]);
@@ -249,7 +289,7 @@ void intt(const Twiddles &t, const uint64_t *in, uint64_t in_stride, uint64_t *o
   if (!ncols || !nbat) return;
   uint64_t n_inv = gl::inv((uint64_t)1 << log_n);
   dim3 grid(ncols, nbat);
-  k_intt<<<grid, ntt_threads(log_n), 8u * qpk::ntt_lds_words(1u << log_n), s>>>(in, in_stride, out, out_stride, log_n, n_inv, t.inv,
+  k_intt<<<grid, ntt_threads(log_n), 8u * qpk::ntt_lds_words(1u << log_n), s>>>(in, in_stride, out, out_stride, log_n, n_inv, t.pt_inv,
                                                          in_bstride, out_bstride);
 }
 
@@ -259,7 +299,8 @@ void lde(const Twiddles &t, const uint64_t *coeffs, uint64_t c_stride, uint64_t 
   if (!ncols || !nbat) return;
   // n = 2^14 (the aggregation circuits): 1024 threads x 16 and 135 KB of LDS,
   // one workgroup per CU
-  if (rate_bits >= 1 && rate_bits <= LDE_MAX_RATE && log_n >= 10 && log_n <= 14 && log_n + rate_bits <= TW_LOG &&
+  if (rate_bits >= 1 && rate_bits <= LDE_MAX_RATE && log_n >= LDE_COSETS_MIN_LOG && log_n <= LDE_COSETS_MAX_LOG &&
+      log_n + rate_bits <= TW_LOG &&
       !getenv_flag("QPGPU_LDE_PERCOSET")) {
     dim3 g(ncols, nbat);
     const size_t lds_bytes = (size_t)8 * qpk::ntt_lds_words(1u << log_n);
@@ -273,7 +314,7 @@ void lde(const Twiddles &t, const uint64_t *coeffs, uint64_t c_stride, uint64_t 
     const uint64_t shift_T = gl::pow(shift, T);
 #define QP_LDE_COSETS(LT)                                                                                      \
   k_lde_cosets<LT><<<g, 1u << LT, lds_bytes, s>>>(coeffs, c_stride, c_bstride, out, o_stride, o_bstride, rate_bits, \
-                                                  shift, shift_T, t.fwd, t.ptw)
+                                                  shift, shift_T, t.mtw + t.mtw_off[log_n][rate_bits], t.pt_fwd, t.ptw)
     switch (log_n) {
       case 10: QP_LDE_COSETS(6); break;
       case 11: QP_LDE_COSETS(7); break;
@@ -286,7 +327,7 @@ void lde(const Twiddles &t, const uint64_t *coeffs, uint64_t c_stride, uint64_t 
   }
   dim3 grid(1u << rate_bits, ncols, nbat);
   k_lde<<<grid, ntt_threads(log_n), 8u * qpk::ntt_lds_words(1u << log_n), s>>>(coeffs, c_stride, out, o_stride, log_n, rate_bits, shift,
-                                                        t.fwd, c_bstride, o_bstride);
+                                                        t.fwd, t.pt_fwd, c_bstride, o_bstride);
 }
 
 }  // namespace qpk

@@ -278,9 +278,12 @@ __device__ __forceinline__ void pass32(uint64_t *a, uint32_t n) {
 // In-place DIF over LDS a[lp(0..2^log_n)), all threads of the block participate,
 // starting at sub-problem size 2^log_S (log_S = log_n: the whole transform;
 // smaller: the levels above were already done, e.g. from registers).
-// tw = forward or inverse twiddle table matching INV.  Ends with a barrier.
+// pt = the pass twiddles (Twiddles::pt_fwd or pt_inv, matching INV): a pass's
+// 15 twiddles per group are read as [m][t] rows, so the lanes of a wave
+// (consecutive t) read consecutive words instead of a gather with stride
+// brev4(m) through the power table.  Ends with a barrier.
 template <bool INV>
-__device__ __forceinline__ void ntt_lds_from(uint64_t *a, uint32_t log_n, uint32_t log_S, const uint64_t *__restrict__ tw) {
+__device__ __forceinline__ void ntt_lds_from(uint64_t *a, uint32_t log_n, uint32_t log_S, const uint64_t *__restrict__ pt) {
   const uint32_t n = 1u << log_n;
   const uint32_t T = blockDim.x;
   // radix-16 passes
@@ -299,8 +302,9 @@ __device__ __forceinline__ void ntt_lds_from(uint64_t *a, uint32_t log_n, uint32
       for (int m = 0; m < 16; m++) r[m] = base[lp(m * q)];
       dft16<INV>(r);
       if (t) {
+        const uint64_t *ptS = pt + qpk::pt_offset(log_S) + t;
 #pragma unroll
-        for (int m = 1; m < 16; m++) r[m] = mul(r[m], tw_pow(tw, t * brev4(m), log_S));
+        for (int m = 1; m < 16; m++) r[m] = mul(r[m], ptS[m * q]);
       }
 #pragma unroll
       for (int m = 0; m < 16; m++) base[lp(m * q)] = r[m];
@@ -315,8 +319,8 @@ __device__ __forceinline__ void ntt_lds_from(uint64_t *a, uint32_t log_n, uint32
 }
 
 template <bool INV>
-__device__ __forceinline__ void ntt_lds(uint64_t *a, uint32_t log_n, const uint64_t *__restrict__ tw) {
-  ntt_lds_from<INV>(a, log_n, log_n, tw);
+__device__ __forceinline__ void ntt_lds(uint64_t *a, uint32_t log_n, const uint64_t *__restrict__ pt) {
+  ntt_lds_from<INV>(a, log_n, log_n, pt);
 }
 
 // ---- radix-8 variant: 8 elements per thread (n/8 threads per transform), so

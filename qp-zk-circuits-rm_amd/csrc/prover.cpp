@@ -607,7 +607,7 @@ int prove_batch(qp_prover *P, const uint64_t *d_wires, const uint64_t *const *wi
     const uint64_t n_inv = gl::inv(n);
     qpk::k_qintt_blocks<<<dim3(B, nc, nb), 512, 8u * qpk::ntt_lds_words(1u << P->log_n), s>>>(P->qvals.p, P->cbuf.p, P->log_n, P->rate_bits,
                                                                      (uint64_t)nc * N, (uint64_t)nc * N, c->tw.fwd,
-                                                                     c->tw.inv, n_inv, gl::inv(gl::GEN));
+                                                                     c->tw.pt_inv, n_inv, gl::inv(gl::GEN));
     const uint64_t winv_r = gl::inv(gl::root_of_unity(P->rate_bits));
     const uint64_t gninv = gl::inv(gl::pow(gl::GEN, n));
     qpk::k_qintt_radix<<<dim3(cdiv(n, 256), nc, nb), 256, 0, s>>>(P->cbuf.p, P->quot.coeffs.p, P->log_n, P->rate_bits,

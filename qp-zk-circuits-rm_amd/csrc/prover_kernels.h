@@ -70,7 +70,7 @@ template <int PH>
 __global__ void k_quotient(QuotientArgs a);
 __global__ void k_quotient_1r(QuotientArgs a);
 __global__ void k_qintt_blocks(const uint64_t *vals, uint64_t *out, uint32_t log_n, uint32_t rate_bits,
-                               uint64_t v_bstride, uint64_t o_bstride, const uint64_t *tw, const uint64_t *tw_inv,
+                               uint64_t v_bstride, uint64_t o_bstride, const uint64_t *tw, const uint64_t *pt_inv,
                                uint64_t n_inv, uint64_t ginv);
 __global__ void k_qintt_radix(const uint64_t *cbuf, uint64_t *coeffs, uint32_t log_n, uint32_t rate_bits,
                               uint64_t c_bstride, uint64_t o_bstride, uint64_t winv_r, uint64_t r_inv, uint64_t gninv);

@@ -849,7 +849,7 @@ template __global__ void k_quotient<2>(QuotientArgs);
 __global__ void __launch_bounds__(512) k_qintt_blocks(const uint64_t *__restrict__ vals, uint64_t *__restrict__ out,
                                                       uint32_t log_n, uint32_t rate_bits, uint64_t v_bstride,
                                                       uint64_t o_bstride, const uint64_t *__restrict__ tw,
-                                                      const uint64_t *__restrict__ tw_inv, uint64_t n_inv,
+                                                      const uint64_t *__restrict__ pt_inv, uint64_t n_inv,
                                                       uint64_t ginv) {
   extern __shared__ __attribute__((aligned(16))) uint64_t lds[];
   const uint32_t n = 1u << log_n, logN = log_n + rate_bits;
@@ -859,7 +859,7 @@ __global__ void __launch_bounds__(512) k_qintt_blocks(const uint64_t *__restrict
   const uint64_t *src = vals + b * v_bstride + c * N + ((uint64_t)sp << log_n);
   for (uint32_t p = threadIdx.x; p < n; p += blockDim.x) lds[nt::lp(gl::rev_bits(p, log_n))] = src[p];
   __syncthreads();
-  nt::ntt_lds<true>(lds, log_n, tw_inv);
+  nt::ntt_lds<true>(lds, log_n, pt_inv);
   // base^-1 = g^-1 w_N^-s
   const uint64_t wNs = wpow_N(tw, s, logN);
   const uint64_t binv = gl::mul(ginv, gl::inv(wNs));

@@ -231,7 +231,7 @@ int qp_quotient(qp_ctx *ctx, const qp_batch *cs, const qp_batch *wires, const qp
     else qpk::k_quotient<2><<<dim3(cdiv(N, 256), 1), 256, 0, s>>>(a);  // any gate list
     const uint64_t n_inv = gl::inv(n);
     qpk::k_qintt_blocks<<<dim3(B, nc, 1), 512, 8u * qpk::ntt_lds_words(1u << log_n), s>>>(
-        d_q.p, d_cbuf.p, log_n, rb, 2 * N, 2 * N, ctx->tw.fwd, ctx->tw.inv, n_inv, gl::inv(gl::GEN));
+        d_q.p, d_cbuf.p, log_n, rb, 2 * N, 2 * N, ctx->tw.fwd, ctx->tw.pt_inv, n_inv, gl::inv(gl::GEN));
     qpk::k_qintt_radix<<<dim3(cdiv(n, 256), nc, 1), 256, 0, s>>>(d_cbuf.p, d_out.p, log_n, rb, 2 * N,
                                                                  (uint64_t)nc * qdf * n,
                                                                  gl::inv(gl::root_of_unity(rb)), gl::inv(B),

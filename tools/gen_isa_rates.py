@@ -34,6 +34,12 @@ INSTRS = [
     ("v_lshlrev_b64", 64, "v_lshlrev_b64 %0, 3, %0"),
     ("v_mov_b64", 64, "v_mov_b64 %0, %2"),
     ("v_fma_f32", 0, "v_fma_f32 %0, %0, %1, %1"),
+    # VOP2 carry forms through VCC (the e32 encodings of the ops above)
+    ("v_add_co_u32_e32", 32, "v_add_co_u32_e32 %0, vcc, %0, %1"),
+    ("v_addc_co_u32_e32", 32, "v_addc_co_u32_e32 %0, vcc, %0, %1, vcc"),
+    ("v_subb_co_u32_e32", 32, "v_subb_co_u32_e32 %0, vcc, %0, %1, vcc"),
+    ("v_cndmask_b32_e32", 32, "v_cndmask_b32_e32 %0, %0, %1, vcc"),
+    ("v_mad_u64_u32_vcc", 64, "v_mad_u64_u32 %0, vcc, %1, 13, %0"),
 ]
 # hazard-pad cost: VALU instructions with the wait states the gfx950 hazard
 # rules make hipcc insert, per VALU instruction (4th field = VALU count)
@@ -43,6 +49,8 @@ NOPS = [
     ("mad+2xs_nop0", 64, "v_mad_u64_u32 %0, s[40:41], %1, 13, %0\\n\\ts_nop 0\\n\\ts_nop 0", 1),
     ("mad+s_nop1", 64, "v_mad_u64_u32 %0, s[40:41], %1, 13, %0\\n\\ts_nop 1", 1),
     ("addco,addc", 32, "v_add_co_u32_e64 %0, s[40:41], %0, %1\\n\\tv_addc_co_u32_e64 %0, s[42:43], %0, %1, s[40:41]", 2),
+    ("addco,addc e32", 32, "v_add_co_u32_e32 %0, vcc, %0, %1\\n\\tv_addc_co_u32_e32 %0, vcc, %0, %1, vcc", 2),
+    ("addco e32,cndmask e32", 32, "v_add_co_u32_e32 %0, vcc, %0, %1\\n\\tv_cndmask_b32_e32 %0, %0, %1, vcc", 2),
     ("addco,2nop,addc", 32, "v_add_co_u32_e64 %0, s[40:41], %0, %1\\n\\ts_nop 0\\n\\ts_nop 0\\n\\tv_addc_co_u32_e64 %0, s[42:43], %0, %1, s[40:41]", 2),
 ]
 ITERS = 65536
@@ -52,13 +60,13 @@ def kernel(i, name, kind, asm, nvalu=1):
     lines = []
     if kind == 64:
         decl = "uint64_t c[8]; for (int i = 0; i < 8; i++) c[i] = seed + i + threadIdx.x;"
-        cons = '"+v"(c[{k}]) : "v"(x), "v"(z) : "s40","s41","s42","s43"'
+        cons = '"+v"(c[{k}]) : "v"(x), "v"(z) : "s40","s41","s42","s43","vcc"'
     elif kind == 0:
         decl = "float c[8]; for (int i = 0; i < 8; i++) c[i] = 1.0f + i * 1e-3f;"
-        cons = '"+v"(c[{k}]) : "v"(g) : "s40","s41","s42","s43"'
+        cons = '"+v"(c[{k}]) : "v"(g) : "s40","s41","s42","s43","vcc"'
     else:
         decl = "uint32_t c[8]; for (int i = 0; i < 8; i++) c[i] = seed + i + threadIdx.x;"
-        cons = '"+v"(c[{k}]) : "v"(x) : "s40","s41","s42","s43"'
+        cons = '"+v"(c[{k}]) : "v"(x) : "s40","s41","s42","s43","vcc"'
     body = "\n".join(f'    asm volatile("{asm}" : {cons.format(k=k)});' for k in range(8))
     lines.append(f"""__global__ void k{i}(uint64_t *out, uint64_t *ticks, uint32_t seed) {{
   // {name}
@@ -82,6 +90,8 @@ def main():
     global INSTRS
     if len(sys.argv) > 1 and sys.argv[1] == "nops":
         INSTRS = NOPS
+    elif len(sys.argv) > 1 and sys.argv[1] == "all":
+        INSTRS = INSTRS + NOPS
     INSTRS = [t if len(t) == 4 else t + (1,) for t in INSTRS]
     print("// isa_rates.hip -- GENERATED by tools/gen_isa_rates.py; see that file.")
     print("#include <hip/hip_runtime.h>\n#include <stdint.h>\n#include <stdio.h>\n#include <vector>")
