@@ -202,18 +202,17 @@ __global__ void __launch_bounds__(1 << LOG_T) QP_NTT_OCC k_lde_cosets(const uint
   const uint64_t *pw = ptw + ptw_offset(rate_bits);
   for (uint32_t s = 0; s < B; s++) {
     uint64_t r[16];
-    r[0] = a[0];
 #pragma unroll
-    for (int m = 1; m < 16; m++) r[m] = nt::mul(a[m], pw[16 * s + m]);
+    for (int m = 0; m < 16; m++) r[m] = a[m];
+    nt::mul_rows(r, [&](int m) { return pw[16 * s + m]; });
     nt::dft16<false>(r);
     // merged twiddles w_N^{t(s + B brev4(m))}: row (s, m) of the table, lane t
     // (a product by w^0 = 1 returns its input unchanged)
     const uint64_t *ms = mtw + (uint64_t)16 * T * s + t;
+    if (s) r[0] = nt::mul(r[0], ms[0]);
+    nt::mul_rows(r, [&](int m) { return ms[T * m]; });
 #pragma unroll
-    for (int m = 0; m < 16; m++) {
-      if (s || m) r[m] = nt::mul(r[m], ms[T * m]);
-      lds[nt::lp(t) + nt::lp(T * m)] = r[m];
-    }
+    for (int m = 0; m < 16; m++) lds[nt::lp(t) + nt::lp(T * m)] = r[m];
     __syncthreads();
     nt::ntt_lds_from<false>(lds, LOG_N, LOG_T, pt);
     uint64_t *dst = dst0 + ((uint64_t)gl::rev_bits(s, rate_bits) << LOG_N);

@@ -70,8 +70,39 @@ __device__ __forceinline__ uint64_t reduce(uint64_t lo, uint64_t hi) {
   return r + (r < t1 ? EPS : 0);
 }
 
-// general product: the asm form (5 mads + 8-op reduction, poseidon_fast.h)
-__device__ __forceinline__ uint64_t mul(uint64_t a, uint64_t b) { return pf::mul(a, b); }
+// general product: the asm form (5 mads + 8-op reduction, poseidon_fast.h);
+// QP_NTT_MUL_C=1: the C form the compiler schedules itself (A/B)
+#ifndef QP_NTT_MUL_C
+#define QP_NTT_MUL_C 0
+#endif
+__device__ __forceinline__ uint64_t mul(uint64_t a, uint64_t b) {
+  if constexpr (QP_NTT_MUL_C) return pf::mul_c(a, b);
+  else return pf::mul(a, b);
+}
+
+// r[m] *= tw(m) for m = 1..15 (a group's twiddles); QP_NTT_MULK=1 issues them
+// as five interleaved triples (pf::mulk<3>: each carry is read two products
+// later instead of after hazard pads)
+#ifndef QP_NTT_MULK
+#define QP_NTT_MULK 1
+#endif
+template <class TW>
+__device__ __forceinline__ void mul_rows(uint64_t r[16], const TW &tw) {
+  if constexpr (QP_NTT_MULK) {
+#pragma unroll
+    for (int m = 1; m < 16; m += 3) {
+      const uint64_t a[3] = {r[m], r[m + 1], r[m + 2]}, b[3] = {tw(m), tw(m + 1), tw(m + 2)};
+      uint64_t o[3];
+      pf::mulk<3>(a, b, o);
+      r[m] = o[0];
+      r[m + 1] = o[1];
+      r[m + 2] = o[2];
+    }
+  } else {
+#pragma unroll
+    for (int m = 1; m < 16; m++) r[m] = mul(r[m], tw(m));
+  }
+}
 
 __device__ __forceinline__ uint64_t canon(uint64_t x) { return x >= gl::P ? x - gl::P : x; }
 
@@ -303,8 +334,7 @@ __device__ __forceinline__ void ntt_lds_from(uint64_t *a, uint32_t log_n, uint32
       dft16<INV>(r);
       if (t) {
         const uint64_t *ptS = pt + qpk::pt_offset(log_S) + t;
-#pragma unroll
-        for (int m = 1; m < 16; m++) r[m] = mul(r[m], ptS[m * q]);
+        mul_rows(r, [&](int m) { return ptS[m * q]; });
       }
 #pragma unroll
       for (int m = 0; m < 16; m++) base[lp(m * q)] = r[m];

@@ -127,6 +127,8 @@ struct qp_prover {
   DevBuf wg_gens, wg_lvl, wg_wslot, wg_wslot_cm, wg_in_slots, wg_pi_slots, wg_vals, wg_in, wg_err, wg_pis;
   uint32_t wg_nslots = 0, wg_nin = 0, wg_nlev = 0;
   bool quotient_rereads = false;
+  bool quotient_fused = false;  // A/B: QPGPU_QUOTIENT=fused selects k_quotient_fused where it applies
+  bool has_poseidon_gate = false;
   bool generic_quotient = false;  // a gate outside k_quotient_1r's set (the recursive verifier's RandomAccess)
   bool pp_generic = false;  // QPGPU_PP_GENERIC=1: the runtime-shape k_pp_rows (A/B)
   uint64_t *h_in = nullptr;  // pinned [max_batch][wg_nin] commit() values
@@ -264,7 +266,10 @@ int setup(qp_prover *P) {
       case qc::G_PUBLIC_INPUT: g.kind[i] = qpk::GK_PUBLIC_INPUT; break;
       case qc::G_BASE_SUM: g.kind[i] = qpk::GK_BASE_SUM; break;
       case qc::G_ARITHMETIC: g.kind[i] = qpk::GK_ARITHMETIC; break;
-      case qc::G_POSEIDON: g.kind[i] = qpk::GK_POSEIDON; break;
+      case qc::G_POSEIDON:
+        g.kind[i] = qpk::GK_POSEIDON;
+        P->has_poseidon_gate = true;
+        break;
       case qc::G_RANDOM_ACCESS:
         g.kind[i] = qpk::GK_RANDOM_ACCESS;
         P->generic_quotient = true;  // k_quotient_1r covers the leaf circuits' six gates only
@@ -402,6 +407,7 @@ int setup(qp_prover *P) {
   {
     const char *qv = getenv("QPGPU_QUOTIENT");
     P->quotient_rereads = qv && !strcmp(qv, "rereads");
+    P->quotient_fused = qv && !strcmp(qv, "fused");
     const char *pv = getenv("QPGPU_PP_GENERIC");
     P->pp_generic = pv && pv[0] && pv[0] != '0';
   }
@@ -601,6 +607,8 @@ int prove_batch(qp_prover *P, const uint64_t *d_wires, const uint64_t *const *wi
     kt_begin(P, 3);
     if (P->quotient_rereads || P->generic_quotient)  // generic gate list (or A/B: QPGPU_QUOTIENT=rereads)
       qpk::k_quotient<2><<<dim3(cdiv(N, 256), nb), 256, 0, s>>>(a);
+    else if (P->R == 80 && P->qdf == 8 && P->has_poseidon_gate && P->quotient_fused)
+      qpk::k_quotient_fused<<<dim3(cdiv(N, 256), nb), 256, 0, s>>>(a);
     else
       qpk::k_quotient_1r<<<dim3(cdiv(N, 256), nb), 256, 0, s>>>(a);
     kt_end(P, 3, (double)nb * N);

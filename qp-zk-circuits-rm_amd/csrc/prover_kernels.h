@@ -69,6 +69,9 @@ __global__ void k_z_scan(const uint64_t *prods, uint64_t *zs, uint32_t log_n, ui
 template <int PH>
 __global__ void k_quotient(QuotientArgs a);
 __global__ void k_quotient_1r(QuotientArgs a);
+// k_quotient_1r for R = 80 routed wires in chunks of 8 with the Poseidon gate:
+// the sweep rides on the gate's wire reads (every wire read once)
+__global__ void k_quotient_fused(QuotientArgs a);
 __global__ void k_qintt_blocks(const uint64_t *vals, uint64_t *out, uint32_t log_n, uint32_t rate_bits,
                                uint64_t v_bstride, uint64_t o_bstride, const uint64_t *tw, const uint64_t *pt_inv,
                                uint64_t n_inv, uint64_t ginv);

@@ -839,6 +839,249 @@ k_quotient_1r(QuotientArgs a) {
   q[N + t] = gfn::canon(gfn::mul(acc1, zh_inv));
 }
 
+// ---- k_quotient_fused: k_quotient_1r for the standard layout (80 routed
+// wires in chunks of 8, Poseidon gate on wires 0..134) with every wire read
+// from HBM exactly once.  The Poseidon gate reads its wires in the order
+// 24, 25..28 / 0..7 interleaved, 8..11, 29..64 (full rounds), 65..86
+// (partial), 87..134, 12..23 (outputs); within every chunk of 8 routed wires
+// the highest index comes last.  The reader (FusedRead) copies each routed
+// wire into an LDS slot as the gate reads it and runs the permutation-
+// argument / gate-term sweep over complete chunks at six read points: after
+// wire 7 chunk 0, 39 chunks 3-4, 47 chunk 5, 63 chunks 6-7, 87 (the first
+// read after the partial rounds, whose grouped code has no registers to
+// spare) chunks 8-9, 23 chunks 1-2.  Slots: chunk parity * 8 + j % 8,
+// wires 8..11 at 16..19 (pending from the gate's start to its outputs), so
+// no two pending wires share a slot: 20 slots = 40 KB per 256-lane workgroup.
+// Every term goes to its own alpha power (emit_at), so the chunk order does
+// not change the sums mod p; the base-sum gate's closing term is emitted
+// after all chunks.  In k_quotient_1r the gate re-reads wires 16..79 after
+// the sweep (L2 cannot hold a workgroup's 160 KB of routed wires): 1.28x the
+// algorithmic HBM bytes.  Opt-in (QPGPU_QUOTIENT=fused): bit-exact, but the
+// sweep's temporaries on top of the gate's live state do not fit 128 VGPRs
+// (368 spilled at 4 waves/SIMD, 27 at 3), and at 3 waves it measured slower:
+// 9.43 vs 7.46 ms per 86-proof launch, 1123 vs 1165 proofs/s e2e
+// (profiles/r03_ab_quotient_fused.log).
+constexpr uint32_t QF_SLOTS = 20;
+
+// GEN^(8k): the coset factor k_j = GEN^j at the first wire of chunk k
+constexpr uint64_t qf_mulmod(uint64_t a, uint64_t b) { return (uint64_t)(((unsigned __int128)a * b) % gl::P); }
+constexpr uint64_t qf_pow(uint64_t b, uint32_t e) { return e ? qf_mulmod(b, qf_pow(b, e - 1)) : 1; }
+__device__ const uint64_t QF_GPOW8[10] = {qf_pow(gl::GEN, 0),  qf_pow(gl::GEN, 8),  qf_pow(gl::GEN, 16), qf_pow(gl::GEN, 24),
+                                          qf_pow(gl::GEN, 32), qf_pow(gl::GEN, 40), qf_pow(gl::GEN, 48), qf_pow(gl::GEN, 56),
+                                          qf_pow(gl::GEN, 64), qf_pow(gl::GEN, 72)};
+
+__device__ __forceinline__ uint32_t qf_slot(uint32_t j) {
+  return (j >> 3) == 1 && j < 12 ? 16 + (j - 8) : ((j >> 3) & 1) * 8 + (j & 7);
+}
+
+struct QfState {
+  const uint64_t *cs, *zl, *gc, *ch, *p0, *p1, *gpow8;
+  uint64_t *stash;
+  uint64_t N;
+  uint32_t t, tn, nchunks, npp, num_constants, n_const, n_pi, L, n_ar;
+  uint64_t gamma0, gamma1, beta0, beta1, bx0, bx1;
+  uint64_t z[2], nxk[2];
+  int lastk;
+  uint64_t acc0, acc1, sc0, sc1, sp0, sp1, sb0, sb1, sa0, sa1, bs_acc, w0;
+};
+
+// chunks k0 .. k1-1: their 8 wires from the LDS slots, sigmas from HBM
+// (two loads ahead), the chunk's Z/partial-product check and the per-wire
+// terms of the constant / public-input / base-sum / arithmetic gates
+__device__ __forceinline__ void qf_sweep(QfState &S, uint32_t k0, uint32_t k1) {
+#ifndef QF_FENCE
+#define QF_FENCE 0
+#endif
+  if (QF_FENCE) asm volatile("" ::: "memory");
+  const uint32_t pre = 2 * (1 + S.nchunks);
+#pragma unroll 1
+  for (uint32_t k = k0; k < k1; k++) {
+    const uint32_t j0 = 8 * k;
+    uint64_t num0 = 1, den0 = 1, num1 = 1, den1 = 1;
+    uint64_t bkx0 = gfn::mul(S.bx0, S.gpow8[k]), bkx1 = gfn::mul(S.bx1, S.gpow8[k]);
+    const uint64_t *sgp = S.cs + (uint64_t)(S.num_constants + j0) * S.N;
+    uint64_t sgn0 = sgp[0], sgn1 = sgp[S.N];
+#pragma unroll 1
+    for (uint32_t u = 0; u < 8; u++) {
+      const uint32_t jj = j0 + u;
+      const uint64_t w = S.stash[qf_slot(jj) * blockDim.x + threadIdx.x];
+      const uint64_t sg = sgn0;
+      sgn0 = sgn1;
+      if (u + 2 < 8) sgn1 = sgp[(uint64_t)(u + 2) * S.N];
+      num0 = gfn::mul(num0, gfn::add(gfn::add_c(w, S.gamma0), bkx0));
+      den0 = gfn::mul(den0, gfn::add(gfn::add_c(w, S.gamma0), gfn::mul(S.beta0, sg)));
+      num1 = gfn::mul(num1, gfn::add(gfn::add_c(w, S.gamma1), bkx1));
+      den1 = gfn::mul(den1, gfn::add(gfn::add_c(w, S.gamma1), gfn::mul(S.beta1, sg)));
+      bkx0 = gfn::mul(bkx0, gl::GEN);
+      bkx1 = gfn::mul(bkx1, gl::GEN);
+      if (jj < S.n_const) emit_at(S.p0, S.p1, pre + jj, gfn::sub(S.gc[(uint64_t)jj * S.N], w), S.sc0, S.sc1);
+      if (jj < S.n_pi) emit_at(S.p0, S.p1, pre + jj, gfn::sub(w, S.ch[CH_PIH + jj]), S.sp0, S.sp1);
+      if (S.L) {
+        if (jj == 0) {
+          S.w0 = w;
+        } else if (jj <= S.L) {
+          S.bs_acc = gfn::add(S.bs_acc, mul_pow2_rt(w, jj - 1));
+          emit_at(S.p0, S.p1, pre + jj, gfn::mul(w, gfn::sub(w, 1)), S.sb0, S.sb1);
+        }
+      }
+      if (jj < 4 * S.n_ar && (jj & 3) == 3) {
+        // the op's other three wires from their slots (same chunk)
+        const uint64_t wa0 = S.stash[qf_slot(jj - 3) * blockDim.x + threadIdx.x];
+        const uint64_t wa1 = S.stash[qf_slot(jj - 2) * blockDim.x + threadIdx.x];
+        const uint64_t wa2 = S.stash[qf_slot(jj - 1) * blockDim.x + threadIdx.x];
+        const uint64_t comp = gfn::add(gfn::mul(gfn::mul(wa0, wa1), S.gc[0]), gfn::mul(wa2, S.gc[S.N]));
+        emit_at(S.p0, S.p1, pre + jj / 4, gfn::sub(w, comp), S.sa0, S.sa1);
+      }
+    }
+#pragma unroll
+    for (uint32_t c = 0; c < 2; c++) {
+      const uint64_t prev = k == 0 ? S.z[c]
+                          : S.lastk == (int)k - 1 ? S.nxk[c]
+                                                  : S.zl[((uint64_t)2 + c * S.npp + k - 1) * S.N + S.t];
+      const uint64_t nx = k == S.nchunks - 1 ? S.zl[(uint64_t)c * S.N + S.tn]
+                                             : S.zl[((uint64_t)2 + c * S.npp + k) * S.N + S.t];
+      const uint64_t num = c ? num1 : num0, den = c ? den1 : den0;
+      emit_at(S.p0, S.p1, 2 + c * S.nchunks + k, gfn::sub(gfn::mul(prev, num), gfn::mul(nx, den)), S.acc0, S.acc1);
+      S.nxk[c] = nx;
+    }
+    S.lastk = (int)k;
+  }
+  if (QF_FENCE) asm volatile("" ::: "memory");
+}
+
+struct FusedRead {
+  const uint64_t *__restrict__ wl;
+  uint64_t N;
+  QfState *S;
+  __device__ __forceinline__ uint64_t operator()(uint32_t j) const {
+    const uint64_t w = wl[(uint64_t)j * N];
+    if (j < 80) S->stash[qf_slot(j) * blockDim.x + threadIdx.x] = w;
+#ifndef QF_SITES
+#define QF_SITES 0x3F
+#endif
+    switch (j) {
+      case 7: if (QF_SITES & 1) qf_sweep(*S, 0, 1); break;
+      case 39: if (QF_SITES & 2) qf_sweep(*S, 3, 5); break;
+      case 47: if (QF_SITES & 4) qf_sweep(*S, 5, 6); break;
+      case 63: if (QF_SITES & 8) qf_sweep(*S, 6, 8); break;
+      case 87: if (QF_SITES & 16) qf_sweep(*S, 8, 10); break;  // after the partial rounds (less live state)
+      case 23: if (QF_SITES & 32) qf_sweep(*S, 1, 3); break;
+      default: break;
+    }
+    return w;
+  }
+};
+
+#ifndef QP_QFUSED_WAVES
+#define QP_QFUSED_WAVES 3
+#endif
+__global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(QP_QFUSED_WAVES)))
+k_quotient_fused(QuotientArgs a) {
+  const uint32_t logN = a.log_n + a.rate_bits;
+  const uint64_t N = 1ull << logN;
+  const uint32_t t = blockIdx.x * blockDim.x + threadIdx.x;
+  if (t >= N) return;
+  const uint32_t b = blockIdx.y;
+  __shared__ uint64_t stash[QF_SLOTS * 256];
+  QfState S;
+  S.ch = a.chal + b * CHAL_STRIDE;
+  S.cs = a.cs_lde + t;
+  const uint64_t *wl = a.w_lde + b * a.w_bstride + t;
+  S.zl = a.z_lde + b * a.z_bstride;
+  const uint32_t j = gl::rev_bits(t, logN);
+  uint64_t *q = a.q_out + b * a.q_bstride;
+  S.p0 = a.apow + (uint64_t)b * 2 * APOW_STRIDE;
+  S.p1 = S.p0 + APOW_STRIDE;
+  S.gpow8 = QF_GPOW8;
+  S.stash = stash;
+  S.N = N;
+  S.t = t;
+  S.nchunks = 10;
+  S.npp = 9;
+  S.tn = gl::rev_bits((j + (1u << a.rate_bits)) & (uint32_t)(N - 1), logN);
+  S.gc = S.cs + (uint64_t)a.g.nsel * N;
+  S.num_constants = a.num_constants;
+  int g_const = -1, g_pi = -1, g_bs = -1, g_ar = -1, g_pos = -1;
+  for (uint32_t gi = 0; gi < a.g.ngates; gi++) {
+    switch (a.g.kind[gi]) {
+      case GK_CONSTANT: g_const = (int)gi; break;
+      case GK_PUBLIC_INPUT: g_pi = (int)gi; break;
+      case GK_BASE_SUM: g_bs = (int)gi; break;
+      case GK_ARITHMETIC: g_ar = (int)gi; break;
+      case GK_POSEIDON: g_pos = (int)gi; break;
+      default: break;
+    }
+  }
+  S.n_const = g_const >= 0 ? a.g.param[g_const] : 0;
+  S.n_pi = g_pi >= 0 ? 4 : 0;
+  S.L = g_bs >= 0 ? a.g.param[g_bs] : 0;
+  S.n_ar = g_ar >= 0 ? a.g.param[g_ar] : 0;
+  S.acc0 = S.acc1 = 0;
+  const uint64_t x = a.xtab[t], l0 = a.l0tab[t];
+  for (uint32_t c = 0; c < 2; c++) {
+    S.z[c] = S.zl[(uint64_t)c * N + t];
+    emit_at(S.p0, S.p1, c, gfn::mul(l0, gfn::sub(S.z[c], 1)), S.acc0, S.acc1);
+  }
+  S.beta0 = S.ch[CH_BETA];
+  S.beta1 = S.ch[CH_BETA + 1];
+  S.gamma0 = S.ch[CH_GAMMA];
+  S.gamma1 = S.ch[CH_GAMMA + 1];
+  S.bx0 = gfn::mul(S.beta0, x);
+  S.bx1 = gfn::mul(S.beta1, x);
+  S.lastk = -1;
+  S.sc0 = S.sc1 = S.sp0 = S.sp1 = S.sb0 = S.sb1 = S.sa0 = S.sa1 = 0;
+  S.bs_acc = S.w0 = 0;
+  // the Poseidon gate, sweeping the routed wires as it reads them
+  TermAcc A;
+  A.p0 = S.p0;
+  A.p1 = S.p1;
+  A.s0 = A.s1 = 0;
+  A.i = 2 * (1 + S.nchunks);
+  FusedRead rd{wl, N, &S};
+  poseidon_gate_rd(rd, A);
+  const uint32_t pre = 2 * (1 + S.nchunks);
+  if (S.L && S.L < 80) emit_at(S.p0, S.p1, pre, gfn::sub(S.bs_acc, S.w0), S.sb0, S.sb1);
+  const uint32_t nsel = a.g.nsel;
+  auto filter = [&](int gi) -> uint64_t {
+    const uint32_t si = a.g.sel_index[gi];
+    const uint64_t sv = S.cs[(uint64_t)si * N];
+    uint64_t f = 1;
+    for (uint32_t jg = a.g.grp_lo[si]; jg < a.g.grp_hi[si]; jg++)
+      if (jg != (uint32_t)gi) f = gfn::mul(f, gfn::sub(jg, sv));
+    if (nsel > 1) f = gfn::mul(f, gfn::sub(0xFFFFFFFFull, sv));
+    return f;
+  };
+  uint64_t acc0 = S.acc0, acc1 = S.acc1;
+  if (g_const >= 0) {
+    const uint64_t f = filter(g_const);
+    acc0 = gfn::add(acc0, gfn::mul(f, S.sc0));
+    acc1 = gfn::add(acc1, gfn::mul(f, S.sc1));
+  }
+  if (g_pi >= 0) {
+    const uint64_t f = filter(g_pi);
+    acc0 = gfn::add(acc0, gfn::mul(f, S.sp0));
+    acc1 = gfn::add(acc1, gfn::mul(f, S.sp1));
+  }
+  if (g_bs >= 0) {
+    const uint64_t f = filter(g_bs);
+    acc0 = gfn::add(acc0, gfn::mul(f, S.sb0));
+    acc1 = gfn::add(acc1, gfn::mul(f, S.sb1));
+  }
+  if (g_ar >= 0) {
+    const uint64_t f = filter(g_ar);
+    acc0 = gfn::add(acc0, gfn::mul(f, S.sa0));
+    acc1 = gfn::add(acc1, gfn::mul(f, S.sa1));
+  }
+  {
+    const uint64_t f = filter(g_pos);
+    acc0 = gfn::add(acc0, gfn::mul(f, A.s0));
+    acc1 = gfn::add(acc1, gfn::mul(f, A.s1));
+  }
+  const uint64_t zh_inv = a.zh_inv[j & ((1u << a.rate_bits) - 1)];
+  q[t] = gfn::canon(gfn::mul(acc0, zh_inv));
+  q[N + t] = gfn::canon(gfn::mul(acc1, zh_inv));
+}
+
 template __global__ void k_quotient<0>(QuotientArgs);
 template __global__ void k_quotient<1>(QuotientArgs);
 template __global__ void k_quotient<2>(QuotientArgs);

@@ -115,3 +115,24 @@ def test_wormhole_prover_api():
         p2.commit(WI.test_inputs())
     with pytest.raises(qp_wormhole.QpError):
         qp_wormhole.WormholeProver().prove()
+
+
+def test_fused_quotient_kernel_bit_exact(env, monkeypatch):
+    """The opt-in k_quotient_fused (QPGPU_QUOTIENT=fused, read when a prover
+    is created) sweeps the routed wires out of order from LDS slots while the
+    Poseidon gate reads them; its proofs equal the default kernel's."""
+    import qp_wormhole
+    ctx, circ, prover = env
+    w = circ.commit(WI.test_inputs())
+    # a satisfied witness and one with a corrupted routed wire (nonzero
+    # gate and permutation terms everywhere)
+    wires = np.stack([w.wires(), w.wires()])
+    wires[1, 41, 5] ^= 1
+    pis = np.stack([w.public_inputs(), w.public_inputs()])
+    ref = prover.prove_wires(wires, pis)
+    monkeypatch.setenv("QPGPU_QUOTIENT", "fused")
+    fused = qp_wormhole.Prover(ctx, circ, max_batch=4)
+    try:
+        assert fused.prove_wires(wires, pis) == ref
+    finally:
+        fused.free()
