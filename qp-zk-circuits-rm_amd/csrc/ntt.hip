@@ -214,10 +214,28 @@ __global__ void __launch_bounds__(1 << LOG_T) QP_NTT_OCC k_lde_cosets(const uint
 #pragma unroll
     for (int m = 0; m < 16; m++) lds[nt::lp(t) + nt::lp(T * m)] = r[m];
     __syncthreads();
-    nt::ntt_lds_from<false>(lds, LOG_N, LOG_T, pt);
+    // the last radix-2^g levels (g = LOG_N mod 4) run in the store loop: each
+    // thread takes 16 / 2^g groups of 2^g contiguous values, transforms them in
+    // registers and stores them contiguously (leaf order = DIF order)
+    constexpr uint32_t G = LOG_N % 4;
+    nt::ntt_lds_from<false, false>(lds, LOG_N, LOG_T, pt);
     uint64_t *dst = dst0 + ((uint64_t)gl::rev_bits(s, rate_bits) << LOG_N);
+    if constexpr (G == 0) {
 #pragma unroll
-    for (int m = 0; m < 16; m++) dst[t + T * m] = nt::canon(lds[nt::lp(t) + nt::lp(T * m)]);
+      for (int m = 0; m < 16; m++) dst[t + T * m] = nt::canon(lds[nt::lp(t) + nt::lp(T * m)]);
+    } else {
+      constexpr uint32_t S = 1u << G;
+#pragma unroll
+      for (uint32_t k = 0; k < 16 / S; k++) {
+        const uint32_t g0 = (t + T * k) * S;  // group start: n / S groups over T threads
+        uint64_t r[S];
+#pragma unroll
+        for (uint32_t e = 0; e < S; e++) r[e] = lds[nt::lp(g0 + e)];
+        nt::tail_group<false, G>(r);
+#pragma unroll
+        for (uint32_t e = 0; e < S; e++) dst[g0 + e] = nt::canon(r[e]);
+      }
+    }
     __syncthreads();
   }
 }

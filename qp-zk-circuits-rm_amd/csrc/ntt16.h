@@ -313,8 +313,11 @@ __device__ __forceinline__ void pass32(uint64_t *a, uint32_t n) {
 // 15 twiddles per group are read as [m][t] rows, so the lanes of a wave
 // (consecutive t) read consecutive words instead of a gather with stride
 // brev4(m) through the power table.  Ends with a barrier.
-template <bool INV>
-__device__ __forceinline__ void ntt_lds_from(uint64_t *a, uint32_t log_n, uint32_t log_S, const uint64_t *__restrict__ pt) {
+// TAIL = false: stop before the last radix-2^log_S (log_S < 4) levels and
+// return log_S (after the barrier of the last pass), for callers that fold
+// those levels into their output loop (tail_group)
+template <bool INV, bool TAIL = true>
+__device__ __forceinline__ uint32_t ntt_lds_from(uint64_t *a, uint32_t log_n, uint32_t log_S, const uint64_t *__restrict__ pt) {
   const uint32_t n = 1u << log_n;
   const uint32_t T = blockDim.x;
   // radix-16 passes
@@ -343,14 +346,25 @@ __device__ __forceinline__ void ntt_lds_from(uint64_t *a, uint32_t log_n, uint32
     log_S -= 4;
   }
   // remaining radix-2^log_S levels (log_S < 4): groups of S contiguous elements
+  if (!TAIL) return log_S;
   if (log_S == 1) tail<INV, 1>(a, n);
   else if (log_S == 2) tail<INV, 2>(a, n);
   else if (log_S == 3) tail<INV, 3>(a, n);
+  return 0;
+}
+
+// the last LOGS levels of a DIF on one group of S = 2^LOGS contiguous values
+template <bool INV, int LOGS>
+__device__ __forceinline__ void tail_group(uint64_t r[1 << LOGS]) {
+  constexpr int S = 1 << LOGS;
+  if constexpr (S >= 8) stage_small<INV, S / 2, S>(r);
+  if constexpr (S >= 4) stage_small<INV, 2, S>(r);
+  if constexpr (S >= 2) stage_small<INV, 1, S>(r);
 }
 
 template <bool INV>
 __device__ __forceinline__ void ntt_lds(uint64_t *a, uint32_t log_n, const uint64_t *__restrict__ pt) {
-  ntt_lds_from<INV>(a, log_n, log_n, pt);
+  ntt_lds_from<INV, true>(a, log_n, log_n, pt);
 }
 
 // ---- radix-8 variant: 8 elements per thread (n/8 threads per transform), so
