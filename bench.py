@@ -36,9 +36,6 @@ HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec peak (MI355X_MICROARCH.md)
 # VALU issue peak (MI355X_MICROARCH.md: a wave64 VALU instruction issues over 2
 # cycles per SIMD): 1024 SIMDs x 2.4 GHz / 2 = 1228.8 G wave-instructions/s
 VALU_PEAK_WAVE_INSTR_S = 1024 * 2.4e9 / 2
-# the microbenchmark ceiling of round 2 (tools/isa_rates.hip, profiles/r02_isa_rates.log:
-# 2.56 cycles per VOP3 wave-instruction at 8 waves/SIMD), reported alongside
-VALU_ISA_CEILING_WAVE_INSTR_S = 1024 * 2.4e9 / 2.56
 # measured per-build inputs of the roofline fields, written by the profiling
 # session of this build (tools/gpu_session.sh prof3 / pmc_*; tools/kernel_summary.py,
 # tools/pmc_sq_summary.py, tools/pmc_summary.py)
@@ -47,6 +44,10 @@ PMC_FILE = os.path.join(ROOT, "profiles", f"{PROFILE_TAG}_pmc_hbm_b128.json")
 PMC_SQ_FILE = os.path.join(ROOT, "profiles", f"{PROFILE_TAG}_pmc_sq_b128.json")
 KSUM_FILE = os.path.join(ROOT, "profiles", f"{PROFILE_TAG}_kernel_summary_3provers.json")
 KSUM1_FILE = os.path.join(ROOT, "profiles", f"{PROFILE_TAG}_kernel_summary_1prover.json")
+# measured issue ceiling of k_leaf_hash's instruction mix (tools/issue_ceiling.py:
+# per-class wall-time costs from a counter pass over saturated single-instruction
+# kernels, weighted by the kernel's static mix)
+CEIL_FILE = os.path.join(ROOT, "profiles", f"{PROFILE_TAG}_issue_ceiling.json")
 
 
 def load_json(path):
@@ -448,7 +449,7 @@ def main():
                                             "note": "isolated pass, as roofline.achieved; HBM bytes: PMC file"})
         vk = rec["valu_kernels"]
         ipp = perm_valu_instr()
-        ksum, ksum1 = load_json(KSUM_FILE), load_json(KSUM1_FILE)
+        ksum, ksum1, ceil = load_json(KSUM_FILE), load_json(KSUM1_FILE), load_json(CEIL_FILE)
         if vk.get("leaf_hash_wires_perms_per_s") and ipp:
             ach = vk["leaf_hash_wires_perms_per_s"] / 64 * ipp
             rec["dominant_kernel"] = {
@@ -457,12 +458,16 @@ def main():
                 "share_of_kernel_time": ksum1["leaf_hash_share"] if ksum1 else None,
                 "achieved": ach, "peak": VALU_PEAK_WAVE_INSTR_S, "unit": "wave-instructions/s",
                 "frac": ach / VALU_PEAK_WAVE_INSTR_S, "instr_per_perm": ipp,
-                "frac_of_isa_microbench_ceiling": ach / VALU_ISA_CEILING_WAVE_INSTR_S,
+                "mix_ceiling": ceil["ceiling_wave_instr_per_s"] if ceil else None,
+                "frac_of_mix_ceiling": ach / ceil["ceiling_wave_instr_per_s"] if ceil else None,
                 "sources": {"instr_per_perm": os.path.relpath(PMC_SQ_FILE, ROOT),
+                            "mix_ceiling": os.path.relpath(CEIL_FILE, ROOT) if ceil else None,
                             "share": os.path.relpath(KSUM1_FILE, ROOT) if ksum1 else None,
                             "perms_per_s": "this run (HIP events, isolated pass)"},
                 "note": "issue-bound 64-bit integer work (no MFMA path); peak = the guide's wave64 issue "
-                        "(1 VALU instruction / 2 cycles / SIMD)"}
+                        "(1 VALU instruction / 2 cycles / SIMD), which v_mad_u64_u32 (59% of the kernel's "
+                        "VALU) does not reach: mix_ceiling = the kernel's instruction mix at the measured "
+                        "saturated rate of each instruction class"}
         if ksum:
             rec["gpu_busy_frac"] = {"value": ksum["gpu_busy_frac"], "source": os.path.relpath(KSUM_FILE, ROOT),
                                     "scope": ksum.get("scope"),

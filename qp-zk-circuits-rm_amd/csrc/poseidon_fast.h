@@ -778,11 +778,21 @@ __device__ __forceinline__ void partial_group(uint64_t s[12], const HK &hook = H
 // only those rows; digests need lanes 0..3, the PoW lane 7)
 template <int M, int R, uint32_t OUT = 0xFFFu>
 __device__ __forceinline__ void rounds(uint64_t s[12]) {
-  if constexpr (QP_POSEIDON_SPARSE && M == 3 && R == 3) {
+  if constexpr (M == 10 && R == 0) {
+    // mode 10: mode 3 with the full rounds 0-2 and 26-28 rolled (a third of
+    // the code; round constants from memory)
+#pragma unroll 1
+    for (int r = 0; r < 3; r++) full_round_dyn(s, ps::RC_DEV + (r + 1) * 12);
+    rounds<M, 3, OUT>(s);
+  } else if constexpr (M == 10 && R == 26) {
+#pragma unroll 1
+    for (int r = 26; r < 29; r++) full_round_dyn(s, ps::RC_DEV + (r + 1) * 12);
+    rounds<3, 29, OUT>(s);
+  } else if constexpr (QP_POSEIDON_SPARSE && (M == 3 || M == 10) && R == 3) {
     sbox12(s);
     mds_init_sparse(s);
     rounds<M, 4, OUT>(s);
-  } else if constexpr (QP_POSEIDON_SPARSE && M == 3 && R >= 4 && R < 26) {
+  } else if constexpr (QP_POSEIDON_SPARSE && (M == 3 || M == 10) && R >= 4 && R < 26) {
     constexpr int T0 = R - 4, G = (22 - T0) < QP_PF_GROUP ? (22 - T0) : QP_PF_GROUP;
     if constexpr (G > 1) partial_group<T0, G>(s);
     else partial_sparse<T0>(s);

@@ -53,10 +53,34 @@ NOPS = [
     ("addco e32,cndmask e32", 32, "v_add_co_u32_e32 %0, vcc, %0, %1\\n\\tv_cndmask_b32_e32 %0, %0, %1, vcc", 2),
     ("addco,2nop,addc", 32, "v_add_co_u32_e64 %0, s[40:41], %0, %1\\n\\ts_nop 0\\n\\ts_nop 0\\n\\tv_addc_co_u32_e64 %0, s[42:43], %0, %1, s[40:41]", 2),
 ]
+# dependency distance: the 8 statements per iteration cycle over CH chains,
+# so each instruction depends on the one CH statements earlier (CH = 8: the
+# throughput tables above; CH = 1: a single dependent chain per wave)
+CHAINS = [
+    ("mad CH1", 64, "v_mad_u64_u32 %0, s[40:41], %1, 13, %0", 1, 1),
+    ("mad CH2", 64, "v_mad_u64_u32 %0, s[40:41], %1, 13, %0", 1, 2),
+    ("mad CH4", 64, "v_mad_u64_u32 %0, s[40:41], %1, 13, %0", 1, 4),
+    ("mad CH8", 64, "v_mad_u64_u32 %0, s[40:41], %1, 13, %0", 1, 8),
+    ("add_u32 CH1", 32, "v_add_u32_e32 %0, %0, %1", 1, 1),
+    ("add_u32 CH2", 32, "v_add_u32_e32 %0, %0, %1", 1, 2),
+    ("cndmask CH1", 32, "v_cndmask_b32_e64 %0, %0, %1, s[40:41]", 1, 1),
+    ("cndmask CH2", 32, "v_cndmask_b32_e64 %0, %0, %1, s[40:41]", 1, 2),
+]
+# one asm statement holding the 8 chains' instructions (no compiler hazard pad
+# between them: inline asm that writes an SGPR gets an s_nop after it); the
+# clean per-class costs for tools/issue_ceiling.py
+BLOCKS = [
+    ("mad blk", 64, "v_mad_u64_u32 %0, s[40:41], %1, 13, %0", 1, -1),
+    ("mad+nop blk", 64, "v_mad_u64_u32 %0, s[40:41], %1, 13, %0\\n\\ts_nop 0", 1, -1),
+    ("add_u32 blk", 32, "v_add_u32_e32 %0, %0, %1", 1, -1),
+    ("mov_b32 blk", 32, "v_mov_b32_e32 %0, %1", 1, -1),
+    ("cndmask blk", 32, "v_cndmask_b32_e64 %0, %0, %1, s[40:41]", 1, -1),
+    ("sub_co blk", 32, "v_sub_co_u32_e64 %0, s[42:43], %0, %1", 1, -1),
+]
 ITERS = 65536
 
 
-def kernel(i, name, kind, asm, nvalu=1):
+def kernel(i, name, kind, asm, nvalu=1, ch=8):
     lines = []
     if kind == 64:
         decl = "uint64_t c[8]; for (int i = 0; i < 8; i++) c[i] = seed + i + threadIdx.x;"
@@ -67,7 +91,13 @@ def kernel(i, name, kind, asm, nvalu=1):
     else:
         decl = "uint32_t c[8]; for (int i = 0; i < 8; i++) c[i] = seed + i + threadIdx.x;"
         cons = '"+v"(c[{k}]) : "v"(x) : "s40","s41","s42","s43","vcc"'
-    body = "\n".join(f'    asm volatile("{asm}" : {cons.format(k=k)});' for k in range(8))
+    if ch < 0:  # block: chains %0..%7, x = %8, z = %9
+        ins = "\\n\\t".join(asm.replace("%1", "%8").replace("%2", "%9").replace("%0", f"%{k}") for k in range(8))
+        outs = ", ".join(f'"+v"(c[{k}])' for k in range(8))
+        ins_c = '"v"(x), "v"(z)' if kind != 0 else '"v"(g), "v"(g)'
+        body = f'    asm volatile("{ins}" : {outs} : {ins_c} : "s40","s41","s42","s43","vcc");'
+    else:
+        body = "\n".join(f'    asm volatile("{asm}" : {cons.format(k=k % ch)});' for k in range(8))
     lines.append(f"""__global__ void k{i}(uint64_t *out, uint64_t *ticks, uint32_t seed) {{
   // {name}
   {decl}
@@ -92,12 +122,15 @@ def main():
         INSTRS = NOPS
     elif len(sys.argv) > 1 and sys.argv[1] == "all":
         INSTRS = INSTRS + NOPS
-    INSTRS = [t if len(t) == 4 else t + (1,) for t in INSTRS]
+    elif len(sys.argv) > 1 and sys.argv[1] == "chains":
+        INSTRS = CHAINS + BLOCKS
+    INSTRS = [t if len(t) >= 4 else t + (1,) for t in INSTRS]
+    INSTRS = [t if len(t) == 5 else t + (8,) for t in INSTRS]
     print("// isa_rates.hip -- GENERATED by tools/gen_isa_rates.py; see that file.")
     print("#include <hip/hip_runtime.h>\n#include <stdint.h>\n#include <stdio.h>\n#include <vector>")
     print(f"#define ITERS {ITERS}")
-    for i, (name, kind, asm, nv) in enumerate(INSTRS):
-        print(kernel(i, name, kind, asm, nv))
+    for i, (name, kind, asm, nv, ch) in enumerate(INSTRS):
+        print(kernel(i, name, kind, asm, nv, ch))
     nvs = ", ".join(str(t[3]) for t in INSTRS)
     names = ", ".join(f'"{t[0]}"' for t in INSTRS)
     ptrs = ", ".join(f"k{i}" for i in range(len(INSTRS)))
