@@ -165,6 +165,7 @@ def test_quotient_rejects_bad_shapes(ctx, circuit):
 # (nonzero coefficients log, buffer log, values log, shift, arity bits, cap height)
 FRI_CASES = [
     (13, 16, 16, G, 4, 4),            # wormhole layer 0: degree < n, zero tail to N (arity 16)
+    (14, 17, 17, G, 4, 4),            # aggregation-circuit layer 0 (degree 2^14, rate 3)
     (9, 12, 12, gpow(G, 16), 4, 4),    # wormhole layer 1
     (13, 13, 16, G, 2, 4),            # arity 4, unpadded buffer
     (9, 9, 12, gpow(G, 16), 3, 2),
@@ -200,8 +201,8 @@ def test_fri_layer_matches_oracle(ctx, lnz, lbuf, lv, shift, ab, cap_h):
 def test_fri_layer_errors(ctx):
     import qp_wormhole
     rng = np.random.default_rng(5)
-    with pytest.raises(qp_wormhole.QpError, match="nonzero coefficients"):
-        qp_wormhole.FriLayer(ctx, rand_felts(rng, 2, 1 << 14), 16, G, 2, 4)
+    with pytest.raises(qp_wormhole.QpError, match="more than 2\\^14 nonzero coefficients"):
+        qp_wormhole.FriLayer(ctx, rand_felts(rng, 2, 1 << 15), 17, G, 2, 4)
     with pytest.raises(qp_wormhole.QpError, match="QP_ERR_ARG"):
         qp_wormhole.FriLayer(ctx, rand_felts(rng, 2, 1 << 8), 7, G, 2, 4)  # values shorter than coeffs
     layer = qp_wormhole.FriLayer(ctx, rand_felts(rng, 2, 1 << 8), 10, G, 2, 4)
