@@ -212,14 +212,36 @@ __global__ void __launch_bounds__(1024) k_z_scan(const uint64_t *__restrict__ pr
 
 #define WV(j) wl[(uint64_t)(j) * N]
 
+// two independent products: QP_Q_MULK=1 issues them interleaved (pf::mulk<2>:
+// each carry is read one product later instead of after hazard pads).
+// Measured no change on the quotient (7.25 / 7.41 vs 7.31 / 7.24 ms per
+// 86-proof launch, profiles/r03_ab_quotient_mulk.log), so off.
+#ifndef QP_Q_MULK
+#define QP_Q_MULK 0
+#endif
+__device__ __forceinline__ void mul2(uint64_t a0, uint64_t b0, uint64_t a1, uint64_t b1, uint64_t &r0, uint64_t &r1) {
+  if constexpr (QP_Q_MULK) {
+    const uint64_t a[2] = {a0, a1}, b[2] = {b0, b1};
+    uint64_t r[2];
+    pf::mulk<2>(a, b, r);
+    r0 = r[0];
+    r1 = r[1];
+  } else {
+    r0 = gfn::mul(a0, b0);
+    r1 = gfn::mul(a1, b1);
+  }
+}
+
 struct TermAcc {
   const uint64_t *__restrict__ p0;  // alpha_0^i
   const uint64_t *__restrict__ p1;  // alpha_1^i
   uint64_t s0, s1;
   uint32_t i;
   __device__ __forceinline__ void emit(uint64_t t) {
-    s0 = gfn::add(s0, gfn::mul(t, p0[i]));
-    s1 = gfn::add(s1, gfn::mul(t, p1[i]));
+    uint64_t m0, m1;
+    mul2(t, p0[i], t, p1[i], m0, m1);
+    s0 = gfn::add(s0, m0);
+    s1 = gfn::add(s1, m1);
     i++;
   }
 };
@@ -652,8 +674,10 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(QP_QGE
 // and per gate: 3.0x the algorithmic HBM bytes, profiles/r01_v5_pmc_hbm_b128.json).
 __device__ __forceinline__ void emit_at(const uint64_t *__restrict__ p0, const uint64_t *__restrict__ p1, uint32_t i,
                                         uint64_t t, uint64_t &s0, uint64_t &s1) {
-  s0 = gfn::add(s0, gfn::mul(t, p0[i]));
-  s1 = gfn::add(s1, gfn::mul(t, p1[i]));
+  uint64_t m0, m1;
+  mul2(t, p0[i], t, p1[i], m0, m1);
+  s0 = gfn::add(s0, m0);
+  s1 = gfn::add(s1, m1);
 }
 
 // x * 2^e, 0 <= e < 64, x in [0, 2^64) -> [0, 2^64)
@@ -753,12 +777,14 @@ k_quotient_1r(QuotientArgs a) {
     }
     if (jj < nst) stash[jj * blockDim.x + threadIdx.x] = w;
     // permutation argument, both challenges (k_j = g^j folded into bkx)
-    num0 = gfn::mul(num0, gfn::add(gfn::add_c(w, gamma0), bkx0));
-    den0 = gfn::mul(den0, gfn::add(gfn::add_c(w, gamma0), gfn::mul(beta0, sg)));
-    num1 = gfn::mul(num1, gfn::add(gfn::add_c(w, gamma1), bkx1));
-    den1 = gfn::mul(den1, gfn::add(gfn::add_c(w, gamma1), gfn::mul(beta1, sg)));
-    bkx0 = gfn::mul(bkx0, gl::GEN);
-    bkx1 = gfn::mul(bkx1, gl::GEN);
+    {
+      uint64_t bs0, bs1;
+      mul2(beta0, sg, beta1, sg, bs0, bs1);
+      const uint64_t wg0 = gfn::add_c(w, gamma0), wg1 = gfn::add_c(w, gamma1);
+      mul2(num0, gfn::add(wg0, bkx0), den0, gfn::add(wg0, bs0), num0, den0);
+      mul2(num1, gfn::add(wg1, bkx1), den1, gfn::add(wg1, bs1), num1, den1);
+      mul2(bkx0, gl::GEN, bkx1, gl::GEN, bkx0, bkx1);
+    }
     if ((jj + 1) % qdf == 0 || jj + 1 == R) {
       const uint32_t k = jj / qdf;
       for (uint32_t c = 0; c < 2; c++) {
