@@ -35,8 +35,29 @@ constexpr uint64_t EPS = 0xFFFFFFFFull;
 #ifndef QP_NTT_CARRY
 #define QP_NTT_CARRY 1
 #endif
+// QP_NTT_ADD_MAD=1: the wrap corrections as v_mad_u64_u32 with carry-out
+// (s + e, e = eps on a wrap): 6 instructions instead of the 8-step carry chain
+#ifndef QP_NTT_ADD_MAD
+#define QP_NTT_ADD_MAD 0
+#endif
+__device__ __forceinline__ uint64_t add_mad(uint64_t a, uint64_t b) {
+  uint32_t c0, c1;
+  const uint32_t lo = __builtin_addc((uint32_t)a, (uint32_t)b, 0u, &c0);
+  const uint32_t hi = __builtin_addc((uint32_t)(a >> 32), (uint32_t)(b >> 32), c0, &c1);
+  const uint64_t s = ((uint64_t)hi << 32) | lo;
+  const uint32_t e = 0u - c1;  // a + b wrapped: 2^64 = eps
+  uint64_t s2, c2, s3, cd;
+  uint32_t e2;
+  asm("v_mad_u64_u32 %0, %1, %2, 1, %3" : "=v"(s2), "=s"(c2) : "v"(e), "v"(s));
+  // wrapped again (both inputs in [p, 2^64)): s2 < eps, + eps cannot wrap
+  asm(QP_CWAIT "v_cndmask_b32_e64 %0, 0, -1, %1" : "=v"(e2) : "s"(c2));
+  asm("v_mad_u64_u32 %0, %1, %2, 1, %3" : "=v"(s3), "=s"(cd) : "v"(e2), "v"(s2));
+  return s3;
+}
+
 __device__ __forceinline__ uint64_t add(uint64_t a, uint64_t b) {
 #if QP_NTT_CARRY
+  if constexpr (QP_NTT_ADD_MAD) return add_mad(a, b);
   return gfn::add(a, b);
 #else
   uint64_t s = a + b;
