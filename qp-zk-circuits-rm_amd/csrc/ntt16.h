@@ -35,10 +35,11 @@ constexpr uint64_t EPS = 0xFFFFFFFFull;
 #ifndef QP_NTT_CARRY
 #define QP_NTT_CARRY 1
 #endif
-// QP_NTT_ADD_MAD=1: the wrap corrections as v_mad_u64_u32 with carry-out
-// (s + e, e = eps on a wrap): 6 instructions instead of the 8-step carry chain
+// QP_NTT_ADD_MAD=1 (default): the wrap corrections as v_mad_u64_u32 with
+// carry-out (s + e, e = eps on a wrap): 6 instructions instead of the 8-step
+// carry chain.  LDE -4.4 %, iNTT -8 % (profiles/r03_ab_ntt_add_mad.log)
 #ifndef QP_NTT_ADD_MAD
-#define QP_NTT_ADD_MAD 0
+#define QP_NTT_ADD_MAD 1
 #endif
 __device__ __forceinline__ uint64_t add_mad(uint64_t a, uint64_t b) {
   uint32_t c0, c1;
