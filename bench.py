@@ -107,9 +107,9 @@ def parse():
                          "cores (OMP_NUM_THREADS, else min(cores, 16)) between the provers")
     ap.add_argument("--agg-leaves", type=int, default=64,
                     help="leaf proofs aggregated (one level, pairs) after the timed region (0 = skip)")
-    ap.add_argument("--subtree", type=int, default=1,
-                    help="after the timed region, aggregate the GPU's batch of leaf proofs (largest power of two) "
-                         "into one subtree root and time it (configs[3]'s per-GPU share; 0 = skip)")
+    ap.add_argument("--configs3", type=int, default=1,
+                    help="after the headline, time BASELINE configs[3] as one pipeline (every rank: its batch of "
+                         "leaves -> its subtree root; roots gathered over RCCL; rank 0: the tree root); 0 = skip")
     ap.add_argument("--cpu-sample", type=int, default=2, help="min proofs in the CPU baseline sample (0 = skip)")
     ap.add_argument("--cpu-seconds", type=float, default=10.0, help="min seconds of CPU baseline proving")
     return ap.parse_args()
@@ -196,6 +196,73 @@ def reference_parity(qp_wormhole, device):
     out["note"] = ("GPU proof bytes == the reference's own proof of test_inputs() given its PI-row random cells "
                    "and PoW witness (its find_any witness is nondeterministic); after the timed region")
     return out
+
+
+def configs3(args, circuit, prover, provers, cin, per, NP, B, dist, world, rank, local, torch):
+    """BASELINE configs[3] ("Batch 2048 proofs sharded 8xMI355X, RCCL-gather leaves
+    into recursive aggregator"; aggregator.rs:74-92, tree.rs:55-103) timed as one
+    pipeline (qp_wormhole.distributed.pipeline_aggregate_step): every rank proves
+    its batch of leaves end to end (CircuitInputs -> proofs, its provers in
+    parallel), aggregates them (branching 2) into its subtree root on its own GPU
+    with device witness generation, the roots are gathered to rank 0 over RCCL,
+    and rank 0 aggregates them into the tree root.  One untimed pass builds and
+    caches every level's circuit; the timed pass is bracketed by barriers and
+    device syncs, max over ranks."""
+    import threading
+    from qp_wormhole.distributed import pipeline_aggregate_step
+    ns = 1 << (B.bit_length() - 1)  # leaves per rank: the largest power of two <= B
+    vd = prover.verifier_data()
+    cb = circuit.common_data()
+    vo = vd[:len(vd) - len(cb)]
+
+    def prove_leaves():
+        outs = [None] * NP
+
+        def run(i):
+            outs[i] = provers[i].prove_inputs_array(cin[i], per[i])
+        th = [threading.Thread(target=run, args=(i,)) for i in range(NP)]
+        for t in th:
+            t.start()
+        for t in th:
+            t.join()
+        if any(o is None for o in outs):
+            raise RuntimeError("a leaf prover thread failed")
+        return [p for o in outs for p in o][:ns]
+
+    dev = f"cuda:{local}"
+
+    def step():
+        return pipeline_aggregate_step(prove_leaves, cb, vo, 2, dist, device=dev, gpu=local)
+
+    step()  # untimed: builds and caches every level's circuit and device preprocessing
+    if dist is not None:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    root, tm = step()
+    torch.cuda.synchronize()
+    if dist is not None:
+        dist.barrier()
+    dt = time.perf_counter() - t0
+    if dist is not None:
+        tt = torch.tensor([dt], dtype=torch.float64, device=dev)
+        dist.all_reduce(tt, op=dist.ReduceOp.MAX)
+        dt = float(tt.item())
+    if rank != 0:
+        return None
+    from oracle_lib import lib as olib
+    rvd, rp = root.circuit_data.verifier_data(), root.proof.to_bytes()
+    leaves = world * ns
+    return {"workload": f"{leaves}_leaves_as_{world}x{ns}_per_gpu_subtrees_branching2",
+            "value": leaves / dt, "unit": "leaf proofs/s (proved and aggregated into one root)",
+            "seconds": dt, "leaves": leaves, "aggregation_proofs": leaves - 1,
+            "stages_rank0_s": tm,
+            "root_verified": olib().ora_verify(rvd, len(rvd), rp, len(rp)) == 0,
+            "root_public_inputs": len(root.proof.public_inputs),
+            "note": "one timed pass after an untimed one that builds the level circuits; leaves e2e from "
+                    "CircuitInputs, per-GPU subtree (device witness generation, batched levels), roots gathered "
+                    "over RCCL (world > 1), top levels on rank 0; root verified by the oracle verifier after the "
+                    "timed region"}
 
 
 def main():
@@ -327,29 +394,20 @@ def main():
         t1 = time.perf_counter()
         root = aggregate_to_tree(proofs[:8], cb, vo)
         tree_ms = (time.perf_counter() - t1) * 1e3
-        # configs[3]'s per-GPU share: this GPU's whole batch of leaf proofs ->
-        # one subtree root (the levels of tree.rs:92-103; only the roots of the
-        # GPUs' subtrees would cross xGMI), timed end to end
-        sub = None
-        if args.subtree:
-            ns = 1 << (min(len(proofs), B).bit_length() - 1)
-            aggregate_to_tree(proofs[:ns], cb, vo, TreeAggregationConfig.new(2, ns.bit_length() - 1))  # warm caches
-            t1 = time.perf_counter()
-            sroot = aggregate_to_tree(proofs[:ns], cb, vo, TreeAggregationConfig.new(2, ns.bit_length() - 1))
-            sub_s = time.perf_counter() - t1
-            srvd, srp = sroot.circuit_data.verifier_data(), sroot.proof.to_bytes()
-            sub = {"leaves": ns, "aggregation_proofs": ns - 1, "seconds": sub_s,
-                   "aggregation_proofs_per_s": (ns - 1) / sub_s,
-                   "root_verified": olib().ora_verify(srvd, len(srvd), srp, len(srp)) == 0}
         rvd = root.circuit_data.verifier_data()
         rp = root.proof.to_bytes()
         agg = {"level_leaves": nl, "level_aggregation_proofs": len(level),
                "aggregation_proofs_per_s": len(level) / lvl_s, "leaves_per_s_through_one_level": nl / lvl_s,
                "tree8_root_ms": tree_ms, "root_verified": olib().ora_verify(rvd, len(rvd), rp, len(rp)) == 0,
                "aggregation_circuit_degree_bits": _common_degree_bits(root.circuit_data.common),
-               "proof_bytes": len(rp), "subtree_to_root": sub,
-               "note": "aggregate_chunk circuits (native recursive verifier of 2 proofs, degree 2^14), host "
+               "proof_bytes": len(rp),
+               "note": "aggregate_chunk circuits (native recursive verifier of 2 proofs, degree 2^14), device "
                        "witness generation + batched GPU prove; one level = nl/2 chunks; tree = 4+2+1 proofs"}
+    # BASELINE configs[3] as one measured pipeline (every rank, after the headline):
+    # leaves -> per-GPU subtree root -> RCCL gather of the roots -> tree root on rank 0
+    c3 = None
+    if not voting and args.configs3 and args.mode == "e2e":
+        c3 = configs3(args, circuit, prover, provers, cin, per, NP, B, dist, world, rank, local, torch)
     # standard_recursion_zk_config (the reference's cargo-bench and aggregator config):
     # under no_random it proves the same circuit without salts, one prover, one batch
     zk = None
@@ -423,6 +481,7 @@ def main():
             "latency_1proof_ms": lat,
             "zk_config": zk,
             "aggregation": agg,
+            "configs3": c3,
             "prove_only_1prover_proofs_per_s": prove_only,
             "warmup_proof_verified": verified,
             "reference_proof_bytes_equal": ref_parity,

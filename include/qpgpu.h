@@ -142,12 +142,17 @@ typedef struct {
 int qp_wormhole_circuit_new(int zero_knowledge, qp_circuit **out);
 void qp_circuit_free(qp_circuit *c);
 /* info[0..6] = degree_bits, num_wires, num_routed_wires, num_constants,
- *              num_public_inputs, gates used (before padding), num_gate_constraints */
+ *              num_public_inputs, gates used (before padding), num_gate_constraints
+ * info[7..8] = witness generators, dependency levels of the device schedule
+ * (info must hold 9 words)                                                  */
 int qp_circuit_info(const qp_circuit *c, uint32_t *info);
 /* CommonCircuitData::to_bytes (plonky2 util/serialization.rs) */
 int qp_circuit_common_data(const qp_circuit *c, uint8_t *out, size_t cap, size_t *len);
 /* preprocessed constants||sigmas values over H, [num_constants+num_routed][n] */
 int qp_circuit_constants_sigmas(const qp_circuit *c, uint64_t *out);
+/* their coefficients (PolynomialValues::ifft per column, host), the polynomials
+ * of ProverOnlyCircuitData.constants_sigmas_commitment                     */
+int qp_circuit_constants_sigmas_coeffs(const qp_circuit *c, uint64_t *out);
 /* WormholeProver::commit (lib.rs:209-225) + witness generation.  On a witness
  * conflict returns QP_ERR_WITNESS with the reference's message in err.     */
 int qp_wormhole_commit(const qp_circuit *c, const qp_wormhole_inputs *in, qp_witness **out, char *err,
@@ -181,15 +186,27 @@ int qp_voting_commit(const qp_circuit *c, const qp_voting_inputs *in, qp_witness
  * FRI with Merkle paths to the caps, coset interpolation, PoW) of nproofs
  * proofs of the circuit whose CommonCircuitData bytes are inner_common (this
  * library's leaf or aggregation circuits), their public inputs registered in
- * order.  The circuit's witness generators run on the host (commit below);
- * prove it with qp_prover_new / qp_prover_prove like any other circuit.    */
+ * order.  Prove it from chunks with qp_prover_prove_aggregation (witness
+ * generation on the device) or from host witnesses (qp_aggregation_commit +
+ * qp_prover_prove).                                                        */
 int qp_aggregation_circuit_new(const uint8_t *inner_common, size_t len, uint32_t nproofs, qp_circuit **out);
-/* aggregate_chunk's witness (tree.rs:129-134): verifier_only =
+/* one aggregate_chunk call's inputs (tree.rs:129-134): verifier_only =
  * VerifierOnlyCircuitData bytes of the inner circuit (cap height u64, cap,
- * circuit digest), proofs = nproofs serialized ProofWithPublicInputs.  An
- * invalid inner proof fails witness generation (QP_ERR_WITNESS), as plonky2's
- * prove() of the aggregation circuit fails.  zk_randomness: as in
- * qp_wormhole_inputs (NULL: derived from the inner proofs).                 */
+ * circuit digest), proofs = nproofs serialized ProofWithPublicInputs,
+ * zk_randomness = the PublicInputGate row's num_wires - 4 random cells (NULL:
+ * OS randomness under the zk config, zeros otherwise).                      */
+typedef struct {
+    const uint8_t *verifier_only;
+    size_t vlen;
+    const uint8_t *const *proofs;
+    const size_t *lens;
+    uint32_t nproofs;
+    const uint64_t *zk_randomness;
+} qp_aggregation_chunk;
+/* aggregate_chunk's witness on the host (set_verifier_data_target +
+ * set_proof_with_pis_target + generate_partial_witness).  An invalid inner
+ * proof fails witness generation (QP_ERR_WITNESS), as plonky2's prove() of the
+ * aggregation circuit fails.  zk_randomness: as in qp_aggregation_chunk.    */
 int qp_aggregation_commit(const qp_circuit *c, const uint8_t *verifier_only, size_t vlen,
                           const uint8_t *const *proofs, const size_t *lens, uint32_t nproofs,
                           const uint64_t *zk_randomness, qp_witness **out, char *err, size_t errcap);
@@ -233,6 +250,14 @@ int qp_prover_prove_wormhole_inputs(qp_prover *p, const qp_wormhole_inputs *in, 
  * (voting/src/lib.rs:199-261, :346-357)                                     */
 int qp_prover_prove_voting_inputs(qp_prover *p, const qp_voting_inputs *in, uint32_t nproofs, uint8_t *out,
                                   size_t stride, size_t *lens);
+/* the same for aggregation circuits: nchunks aggregate_chunk calls
+ * (tree.rs:106-143) proven as one batch — the chunks' proof bytes are
+ * deserialized into the circuit's input targets on the host pool, the
+ * recursive verifier's generators (Poseidon, arithmetic, BaseSum, wire split,
+ * extension division, RandomAccess, ...) run on the device; an invalid inner
+ * proof returns QP_ERR_WITNESS naming the chunk.                            */
+int qp_prover_prove_aggregation(qp_prover *p, const qp_aggregation_chunk *chunks, uint32_t nchunks, uint8_t *out,
+                                size_t stride, size_t *lens);
 /* same, with the wire matrices already resident on the device:
  * d_wires = device pointer [nproofs][num_wires][n]; pis on the host          */
 int qp_prover_prove_wires_dev(qp_prover *p, const uint64_t *d_wires, const uint64_t *pis, uint32_t nproofs,
@@ -249,6 +274,11 @@ int qp_prover_set_timing(qp_prover *p, int enable);
  * witness without the required leading zeros gives a proof that fails
  * verification.                                                            */
 int qp_prover_debug_force_pow(qp_prover *p, uint64_t witness, int enable);
+/* TEST-ONLY: release one of the prover's device tables ("wg_wslot_cm",
+ * "wg_gens" or "qtab") to check that a launch whose table is missing returns
+ * QP_ERR_STATE naming it instead of faulting (every prove entry point checks
+ * the tables its kernels read before launching them).                      */
+int qp_prover_debug_drop_table(qp_prover *p, const char *name);
 /* host threads (the caller included) of the prover's pool for commit() and the
  * per-proof host stages; default min(hardware threads, 16).  Several provers in
  * one process should split the host cores (cores / provers each).           */

@@ -621,10 +621,8 @@ CircuitData CircuitBuilder::build() {
     for (Target t : public_inputs_) cd.pi_slots.push_back(sid[pt(t)]);
     for (Target t : zk_cells) cd.zk_slots.push_back(sid[pt(t)]);
     // device schedule: a generator runs at the first level where all its
-    // inputs exist; its outputs exist from the next level on (circuits with
-    // host-only generators, e.g. the recursive verifier, have none)
-    for (const Gen &g : cd.schedule)
-      if (g.kind == GEN_WIRE_SPLIT || g.kind == GEN_EXT_DIV || g.kind == GEN_RANDOM_ACCESS) cd.device_witness = false;
+    // inputs exist; its outputs exist from the next level on.  Every generator
+    // kind has a device form (witness.hip), the recursive verifier's included.
     if (cd.device_witness) {
       std::vector<uint8_t> is_in(nslots, 0);
       for (Target t : inputs_) {
@@ -658,6 +656,20 @@ CircuitData CircuitBuilder::build() {
             for (uint32_t j = 12; j < W; j++)
               if (j != 24) wr.push_back(cd.wire_slot[(size_t)g.row * W + j]);
             break;
+          case GEN_WIRE_SPLIT:
+            rd = {g.s[0]};
+            for (uint32_t j = 0; j < g.op; j++) wr.push_back(cd.wire_slot[(size_t)(g.row + j) * W]);
+            break;
+          case GEN_EXT_DIV:
+            rd = {g.s[0], g.s[1], g.s[2], g.s[3]};
+            wr = {g.s[4], g.s[5]};
+            break;
+          case GEN_RANDOM_ACCESS:
+            rd.push_back(cd.wire_slot[(size_t)g.row * W + ra_wire_index(g.op)]);
+            for (uint32_t i = 0; i < RA_VEC; i++) rd.push_back(cd.wire_slot[(size_t)g.row * W + ra_wire_item(i, g.op)]);
+            wr.push_back(cd.wire_slot[(size_t)g.row * W + ra_wire_claimed(g.op)]);
+            for (uint32_t i = 0; i < RA_BITS; i++) wr.push_back(cd.wire_slot[(size_t)g.row * W + ra_wire_bit(i, g.op)]);
+            break;
         }
         uint32_t l = 0;
         for (uint32_t s : rd) {
@@ -682,6 +694,13 @@ CircuitData CircuitBuilder::build() {
         for (int j = 0; j < 4; j++) d.s[j] = g.s[j];
         d.k0 = g.k0;
         d.k1 = g.k1;
+        if (g.kind == GEN_WIRE_SPLIT) {
+          d.s[1] = g.op;  // number of BaseSum gates from `row`
+        } else if (g.kind == GEN_EXT_DIV) {
+          d.k0 = g.s[4] | (uint64_t)g.s[5] << 32;  // quotient slots
+        } else if (g.kind == GEN_RANDOM_ACCESS) {
+          d.s[0] = g.op;  // copy
+        }
       }
     }
   }

@@ -86,9 +86,9 @@ struct GateInst {
   F c0 = 0, c1 = 0;
 };
 
-// generator record: run by witness generation in schedule order
-// (the last three: host witness generation only -- circuits using them, e.g. the
-// recursive verifier, are not device-generated; CircuitData::device_witness)
+// generator record: run by witness generation in schedule order (host) or
+// level by level (device, witness.hip); the last three are the recursive
+// verifier's (aggregation circuits)
 enum GenKind : uint8_t {
   GEN_CONSTANT = 0, GEN_ARITH, GEN_POSEIDON, GEN_BASE_SPLIT, GEN_EQUALITY,
   GEN_WIRE_SPLIT,     // WireSplitGenerator: integer -> the sums of `op` consecutive BaseSum gates from `row`
@@ -109,7 +109,9 @@ struct Gen {
 // Device witness generation (plonky2 iop/generator.rs generate_partial_witness
 // on the GPU): one record per generator, grouped into dependency levels so a
 // workgroup can run one proof's generators level by level (same layout as the
-// device struct in witness.hip).
+// device struct in witness.hip).  Kind-specific packing: WIRE_SPLIT s[1] = gate
+// count; EXT_DIV k0 = the two quotient slots (lo | hi << 32); RANDOM_ACCESS
+// s[0] = copy.
 struct DevGen {
   uint32_t kind, row;
   uint32_t s[4];

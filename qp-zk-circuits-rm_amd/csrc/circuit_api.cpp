@@ -3,6 +3,7 @@
 // side of a circuit (constants/sigmas commitment) lives in prover.cpp.
 #include <string.h>
 #include <exception>
+#include <random>
 #include <memory>
 #include <new>
 #include "../../include/qpgpu.h"
@@ -17,8 +18,11 @@
 // hash_n_to_m_no_pad(domain tag || private felts), a deterministic nonce that
 // hides like fresh randomness while the private inputs stay secret, so the
 // proof remains a pure function of the inputs.
+// os_random: under the zk config with no values given, draw them from the OS
+// (the aggregation circuits: their only witness inputs are public proofs, so a
+// nonce derived from them would not hide anything).
 static std::string zk_fill(const qc::CircuitData &cd, const uint64_t *given, const std::vector<uint64_t> &priv,
-                           qc::Witness &w, int *code) {
+                           qc::Witness &w, int *code, bool os_random = false) {
   *code = QP_ERR_ARG;
   const size_t m = cd.zk_slots.size();
   if (!m) return "";
@@ -27,6 +31,17 @@ static std::string zk_fill(const qc::CircuitData &cd, const uint64_t *given, con
     for (size_t i = 0; i < m; i++) {
       if (given[i] >= gl::P) return "zk randomness value " + std::to_string(i) + " is not a canonical field element";
       v[i] = given[i];
+    }
+  } else if (cd.config.zero_knowledge && os_random) {
+    // RandomValueGenerator: uniform field elements (rejection of the 2^32 - 1
+    // values >= p), from the kernel's CSPRNG
+    std::random_device rd("/dev/urandom");
+    for (size_t i = 0; i < m; i++) {
+      uint64_t x;
+      do {
+        x = (uint64_t)rd() << 32 | rd();
+      } while (x >= gl::P);
+      v[i] = x;
     }
   } else if (cd.config.zero_knowledge) {
     std::vector<uint64_t> in = {0x6b7a2d626c696e64ull % gl::P /* "zk-blind" */, (uint64_t)m};
@@ -112,6 +127,22 @@ std::string voting_fill(const qp_circuit *c, const void *vin, qc::Witness &w, in
   return zk_fill(c->cd, in->zk_randomness, priv, w, code);
 }
 
+// aggregate_chunk's set_verifier_data_target + set_proof_with_pis_target
+// (tree.rs:129-134) and the PublicInputGate row's random cells (zk config:
+// given, else OS randomness; the non-zk config: given, else zeros)
+std::string aggregation_fill(const qp_circuit *c, const void *vin, qc::Witness &w, int *code) {
+  const qp_aggregation_chunk *in = (const qp_aggregation_chunk *)vin;
+  *code = QP_ERR_ARG;
+  if (!c || !in || c->kind != qp_circuit::AGGREGATION) return "not an aggregation circuit / null chunk";
+  if (!in->verifier_only || !in->proofs || !in->lens) return "null verifier data / proof arrays";
+  std::string e = qr::fill_aggregation(c->aggregation, in->verifier_only, in->vlen, in->proofs, in->lens, in->nproofs, w);
+  if (!e.empty()) {
+    *code = e.find("set twice") != std::string::npos ? QP_ERR_WITNESS : QP_ERR_ARG;
+    return e;
+  }
+  return zk_fill(c->cd, in->zk_randomness, {}, w, code, true);
+}
+
 extern "C" {
 
 int qp_wormhole_circuit_new(int zk, qp_circuit **out) {
@@ -195,6 +226,8 @@ int qp_circuit_info(const qp_circuit *c, uint32_t *info) {
   info[4] = c->cd.num_public_inputs;
   info[5] = c->gates_used;
   info[6] = c->cd.num_gate_constraints;
+  info[7] = (uint32_t)c->cd.schedule.size();
+  info[8] = c->cd.level_off.empty() ? 0 : (uint32_t)c->cd.level_off.size() - 1;
   return QP_OK;
 }
 
@@ -212,6 +245,35 @@ int qp_circuit_common_data(const qp_circuit *c, uint8_t *out, size_t cap, size_t
 int qp_circuit_constants_sigmas(const qp_circuit *c, uint64_t *out) {
   if (!c || !out) return QP_ERR_ARG;
   memcpy(out, c->cd.constants_sigmas.data(), c->cd.constants_sigmas.size() * 8);
+  return QP_OK;
+}
+
+// PolynomialValues::ifft of every constants||sigmas column on the host (the
+// coefficients plonky2 keeps in ProverOnlyCircuitData.constants_sigmas_commitment):
+// radix-2 DIT on bit-reversed input, scaled by 1/n
+int qp_circuit_constants_sigmas_coeffs(const qp_circuit *c, uint64_t *out) {
+  if (!c || !out) return QP_ERR_ARG;
+  const uint32_t n = c->cd.n, lg = c->cd.degree_bits;
+  const size_t ncols = c->cd.constants_sigmas.size() / n;
+  std::vector<uint64_t> wi(n / 2);
+  const uint64_t w = gl::inv(gl::root_of_unity(lg));
+  for (uint32_t k = 0; k < n / 2; k++) wi[k] = k ? gl::mul(wi[k - 1], w) : 1;
+  const uint64_t n_inv = gl::inv(n);
+  for (size_t col = 0; col < ncols; col++) {
+    const uint64_t *src = c->cd.constants_sigmas.data() + col * n;
+    uint64_t *a = out + col * n;
+    for (uint32_t i = 0; i < n; i++) a[gl::rev_bits(i, lg)] = src[i];
+    for (uint32_t len = 2; len <= n; len <<= 1) {
+      const uint32_t step = n / len;
+      for (uint32_t i = 0; i < n; i += len)
+        for (uint32_t j = 0; j < len / 2; j++) {
+          const uint64_t u = a[i + j], v = gl::mul(a[i + j + len / 2], wi[j * step]);
+          a[i + j] = gl::add(u, v);
+          a[i + j + len / 2] = gl::sub(u, v);
+        }
+    }
+    for (uint32_t i = 0; i < n; i++) a[i] = gl::mul(a[i], n_inv);
+  }
   return QP_OK;
 }
 
@@ -270,20 +332,9 @@ int qp_aggregation_commit(const qp_circuit *c, const uint8_t *verifier_only, siz
   *out = nullptr;
   try {
     auto w = std::make_unique<qp_witness>(c);
-    std::string e = qr::fill_aggregation(c->aggregation, verifier_only, vlen, proofs, lens, nproofs, w->w);
-    int code = e.empty() ? QP_OK : e.find("set twice") != std::string::npos ? QP_ERR_WITNESS : QP_ERR_ARG;
-    if (e.empty()) {
-      // zk: the PublicInputGate row's random cells; default: a Poseidon nonce
-      // of the inner proofs' wires caps
-      std::vector<uint64_t> priv;
-      for (uint32_t i = 0; i < nproofs; i++)
-        for (size_t k = 0; k < 64 && (k + 1) * 8 <= lens[i]; k++) {
-          uint64_t v;
-          memcpy(&v, proofs[i] + 8 * k, 8);
-          priv.push_back(v);
-        }
-      e = zk_fill(c->cd, zk_randomness, priv, w->w, &code);
-    }
+    qp_aggregation_chunk ch{verifier_only, vlen, proofs, lens, nproofs, zk_randomness};
+    int code = QP_OK;
+    std::string e = aggregation_fill(c, &ch, w->w, &code);
     if (e.empty() && !w->w.generate(e)) code = QP_ERR_WITNESS;
     if (!e.empty()) {
       put_err(err, errcap, e);

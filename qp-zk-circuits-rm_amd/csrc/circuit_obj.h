@@ -19,6 +19,8 @@ struct qp_circuit {
 // else the reference's message; *code receives the qp_status to return
 std::string wormhole_fill(const qp_circuit *c, const void *in /* qp_wormhole_inputs */, qc::Witness &w, int *code);
 std::string voting_fill(const qp_circuit *c, const void *in /* qp_voting_inputs */, qc::Witness &w, int *code);
+std::string aggregation_fill(const qp_circuit *c, const void *in /* qp_aggregation_chunk */, qc::Witness &w,
+                             int *code);
 
 struct qp_witness {
   explicit qp_witness(const qp_circuit *c) : circuit(c), w(c->cd) {}

@@ -31,8 +31,11 @@ __host__ __device__ constexpr uint32_t ntt_lds_words(uint32_t n) { return n + (n
 constexpr unsigned LDE_MAX_RATE = 4;  // coset-fused LDE kernel: up to 16 cosets
 
 struct Twiddles {
-  uint64_t *fwd = nullptr;  // fwd[j] = w_{2^TW_LOG}^j,   j < 2^(TW_LOG-1)
-  uint64_t *inv = nullptr;  // inv[j] = w_{2^TW_LOG}^-j
+  // power tables of w = w_{2^TW_LOG} (fwd) and w^-1 (inv), 2^(TW_LOG-1) words
+  // each in the even/odd layout above: read them only through tw_get / tw_pow
+  // (a direct index tw[E] is NOT w^E)
+  uint64_t *fwd = nullptr;
+  uint64_t *inv = nullptr;
   // coset pre-twists of the fused LDE: for rate r (1..LDE_MAX_RATE), at
   // offset 16*(2^r - 2): ptw[16 s + m] = w_{16*2^r}^(s*m), s < 2^r, m < 16
   uint64_t *ptw = nullptr;
@@ -44,8 +47,15 @@ struct Twiddles {
   uint64_t *pt_fwd = nullptr, *pt_inv = nullptr;
   // merged first-pass twiddles of k_lde_cosets per (log_n, r), n = 16 T,
   // N = n 2^r: at mtw_off[log_n][r], mtw[(16 s + m) T + t] = w_N^(t (s + 2^r brev4(m)))
+  // (QPGPU_LDE_MTW=1 only: N words per (log_n, r) re-read by every column's
+  // workgroup, which missed L2 -- round-3 PMC: LDE reads 4.8x algorithmic)
   uint64_t *mtw = nullptr;
   uint64_t mtw_off[TW_LOG + 1][LDE_MAX_RATE + 1] = {};
+  // coset steps of k_lde_cosets per (log_n, r): at utw_off[log_n][r],
+  // utw[k] = w_N^k, k < n (n words; with the pass table pt for S = n the
+  // first-pass twiddles factor into coset-independent tables that stay in L2)
+  uint64_t *utw = nullptr;
+  uint64_t utw_off[TW_LOG + 1][LDE_MAX_RATE + 1] = {};
 };
 __host__ __device__ constexpr uint32_t pt_offset(uint32_t log_S) { return (1u << log_S) - 16u; }
 constexpr uint32_t LDE_COSETS_MIN_LOG = 10, LDE_COSETS_MAX_LOG = 14;  // k_lde_cosets sizes

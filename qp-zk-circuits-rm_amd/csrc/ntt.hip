@@ -65,6 +65,12 @@ __global__ void k_merged_twiddles(uint64_t *mtw, const uint64_t *__restrict__ tw
   mtw[i] = nt::tw_pow(tw, t * (s + (nt::brev4(m) << rate_bits)), logN);
 }
 
+// coset steps of k_lde_cosets for one (log_n, rate): utw[k] = w_N^k, k < n
+__global__ void k_coset_steps(uint64_t *utw, const uint64_t *__restrict__ tw, uint32_t log_n, uint32_t rate_bits) {
+  const uint32_t k = blockIdx.x * blockDim.x + threadIdx.x;
+  if (k < (1u << log_n)) utw[k] = nt::tw_pow(tw, k, log_n + rate_bits);
+}
+
 hipError_t twiddles_init(Twiddles &t, hipStream_t s) {
   uint32_t half = 1u << (TW_LOG - 1);
   hipError_t e = hipMalloc(&t.fwd, half * 8ull);
@@ -110,6 +116,16 @@ hipError_t twiddles_init(Twiddles &t, hipStream_t s) {
   for (uint32_t ln = LDE_COSETS_MIN_LOG; ln <= LDE_COSETS_MAX_LOG; ln++)
     for (uint32_t r = 1; r <= LDE_MAX_RATE && ln + r <= TW_LOG; r++)
       k_merged_twiddles<<<((1u << (ln + r)) + 255) / 256, 256, 0, s>>>(t.mtw + t.mtw_off[ln][r], t.fwd, ln, r);
+  uint64_t nu = 0;
+  for (uint32_t ln = LDE_COSETS_MIN_LOG; ln <= LDE_COSETS_MAX_LOG; ln++)
+    for (uint32_t r = 1; r <= LDE_MAX_RATE && ln + r <= TW_LOG; r++) {
+      t.utw_off[ln][r] = nu;
+      nu += 1ull << ln;
+    }
+  if ((e = hipMalloc(&t.utw, nu * 8))) return e;
+  for (uint32_t ln = LDE_COSETS_MIN_LOG; ln <= LDE_COSETS_MAX_LOG; ln++)
+    for (uint32_t r = 1; r <= LDE_MAX_RATE && ln + r <= TW_LOG; r++)
+      k_coset_steps<<<((1u << ln) + 255) / 256, 256, 0, s>>>(t.utw + t.utw_off[ln][r], t.fwd, ln, r);
   if ((e = hipGetLastError())) return e;
   return hipStreamSynchronize(s);
 }
@@ -122,7 +138,8 @@ void twiddles_free(Twiddles &t) {
   if (t.pt_fwd) (void)hipFree(t.pt_fwd);
   if (t.pt_inv) (void)hipFree(t.pt_inv);
   if (t.mtw) (void)hipFree(t.mtw);
-  t.fwd = t.inv = t.ptw = t.ptw8 = t.pt_fwd = t.pt_inv = t.mtw = nullptr;
+  if (t.utw) (void)hipFree(t.utw);
+  t.fwd = t.inv = t.ptw = t.ptw8 = t.pt_fwd = t.pt_inv = t.mtw = t.utw = nullptr;
 }
 
 __global__ void __launch_bounds__(512) QP_NTT_OCC k_intt(const uint64_t *__restrict__ in, uint64_t in_stride,
@@ -169,12 +186,16 @@ __global__ void __launch_bounds__(512) QP_NTT_OCC k_lde(const uint64_t *__restri
 // them B times) and scaled by shift^k once.  n = 16 T (T = 2^LOG_T threads):
 // thread t holds a_m = c_{t+Tm} shift^{t+Tm}, m < 16, in registers — exactly
 // the inputs of its first radix-16 DIF butterfly.  For coset s the inputs are
-// a_m w_N^{s(t+Tm)} = w_N^{st} * (a_m w_{16B}^{sm}); the common factor w_N^{st}
-// commutes with the 16-point DFT and merges with the pass's own twiddle
-// w_n^{t brev4(j)} into one lookup w_N^{t(s + B brev4(j))}, so each coset costs
-// one pre-twist product per element instead of a scale and a power update.
+// a_m w_N^{s(t+Tm)}: the registers step from coset s-1 to s by one product
+// with w_N^{t+Tm} (utw, n words per (log_n, r)), and after the 16-point DFT
+// the pass's own twiddle w_n^{t brev4(m)} (pt for S = n) applies unchanged to
+// every coset.  Both tables are coset-independent and together n + n words
+// (128 KiB at n = 2^13), so they stay in L2 across the columns; the same 31
+// products per 16 elements as the MTW form, which multiplies by w_{16B}^{sm}
+// before and by the merged w_N^{t(s + B brev4(m))} (N words, 512 KiB at
+// n = 2^13, evicted by the streaming output) after the DFT.
 // The remaining levels run in LDS (ntt_lds_from); output rows in leaf order.
-template <int LOG_T>
+template <int LOG_T, bool MTW>
 __global__ void __launch_bounds__(1 << LOG_T) QP_NTT_OCC k_lde_cosets(const uint64_t *__restrict__ coeffs, uint64_t c_stride,
                                                           uint64_t c_bstride, uint64_t *__restrict__ out,
                                                           uint64_t o_stride, uint64_t o_bstride, uint32_t rate_bits,
@@ -200,17 +221,32 @@ __global__ void __launch_bounds__(1 << LOG_T) QP_NTT_OCC k_lde_cosets(const uint
   }
   const uint32_t B = 1u << rate_bits;
   const uint64_t *pw = ptw + ptw_offset(rate_bits);
+  // MTW = false: utw = the coset steps w_N^{t+Tm} (mtw argument), p1 = the
+  // first pass's twiddles w_n^{t brev4(m)}
+  const uint64_t *ut = mtw + t, *p1 = pt + pt_offset(LOG_N) + t;
   for (uint32_t s = 0; s < B; s++) {
     uint64_t r[16];
+    if constexpr (MTW) {
 #pragma unroll
-    for (int m = 0; m < 16; m++) r[m] = a[m];
-    nt::mul_rows(r, [&](int m) { return pw[16 * s + m]; });
-    nt::dft16<false>(r);
-    // merged twiddles w_N^{t(s + B brev4(m))}: row (s, m) of the table, lane t
-    // (a product by w^0 = 1 returns its input unchanged)
-    const uint64_t *ms = mtw + (uint64_t)16 * T * s + t;
-    if (s) r[0] = nt::mul(r[0], ms[0]);
-    nt::mul_rows(r, [&](int m) { return ms[T * m]; });
+      for (int m = 0; m < 16; m++) r[m] = a[m];
+      nt::mul_rows(r, [&](int m) { return pw[16 * s + m]; });
+      nt::dft16<false>(r);
+      // merged twiddles w_N^{t(s + B brev4(m))}: row (s, m) of the table, lane t
+      // (a product by w^0 = 1 returns its input unchanged)
+      const uint64_t *ms = mtw + (uint64_t)16 * T * s + t;
+      if (s) r[0] = nt::mul(r[0], ms[0]);
+      nt::mul_rows(r, [&](int m) { return ms[T * m]; });
+    } else {
+      if (s) {
+        // a_m w_N^{s(t+Tm)} from coset s - 1's registers
+        a[0] = nt::mul(a[0], ut[0]);
+        nt::mul_rows(a, [&](int m) { return ut[T * m]; });
+      }
+#pragma unroll
+      for (int m = 0; m < 16; m++) r[m] = a[m];
+      nt::dft16<false>(r);
+      if (t) nt::mul_rows(r, [&](int m) { return p1[T * m]; });
+    }
 #pragma unroll
     for (int m = 0; m < 16; m++) lds[nt::lp(t) + nt::lp(T * m)] = r[m];
     __syncthreads();
@@ -218,6 +254,9 @@ __global__ void __launch_bounds__(1 << LOG_T) QP_NTT_OCC k_lde_cosets(const uint
     // thread takes 16 / 2^g groups of 2^g contiguous values, transforms them in
     // registers and stores them contiguously (leaf order = DIF order)
     constexpr uint32_t G = LOG_N % 4;
+    // the LDS passes (launched with T threads) leave exactly the G levels the
+    // store loop runs
+    static_assert(nt::lds_levels_left(LOG_N, LOG_T, T) == G, "LDS passes and the store loop disagree");
     nt::ntt_lds_from<false, false>(lds, LOG_N, LOG_T, pt);
     uint64_t *dst = dst0 + ((uint64_t)gl::rev_bits(s, rate_bits) << LOG_N);
     if constexpr (G == 0) {
@@ -329,9 +368,17 @@ void lde(const Twiddles &t, const uint64_t *coeffs, uint64_t c_stride, uint64_t 
     }
     const uint32_t T = 1u << (log_n - 4);
     const uint64_t shift_T = gl::pow(shift, T);
-#define QP_LDE_COSETS(LT)                                                                                      \
-  k_lde_cosets<LT><<<g, 1u << LT, lds_bytes, s>>>(coeffs, c_stride, c_bstride, out, o_stride, o_bstride, rate_bits, \
-                                                  shift, shift_T, t.mtw + t.mtw_off[log_n][rate_bits], t.pt_fwd, t.ptw)
+    // QPGPU_LDE_MTW=1: the merged-table form (A/B)
+    static const bool use_mtw = getenv_flag("QPGPU_LDE_MTW");
+#define QP_LDE_COSETS(LT)                                                                                          \
+  if (use_mtw)                                                                                                     \
+    k_lde_cosets<LT, true><<<g, 1u << LT, lds_bytes, s>>>(coeffs, c_stride, c_bstride, out, o_stride, o_bstride,   \
+                                                          rate_bits, shift, shift_T,                               \
+                                                          t.mtw + t.mtw_off[log_n][rate_bits], t.pt_fwd, t.ptw);   \
+  else                                                                                                             \
+    k_lde_cosets<LT, false><<<g, 1u << LT, lds_bytes, s>>>(coeffs, c_stride, c_bstride, out, o_stride, o_bstride,  \
+                                                           rate_bits, shift, shift_T,                              \
+                                                           t.utw + t.utw_off[log_n][rate_bits], t.pt_fwd, t.ptw)
     switch (log_n) {
       case 10: QP_LDE_COSETS(6); break;
       case 11: QP_LDE_COSETS(7); break;

@@ -234,7 +234,7 @@ __device__ __forceinline__ void dft16(uint64_t a[16]) {
   stage16<INV, 1>(a);
 }
 
-// w_S^e via the half table of w_{2^TW_LOG} (tw[j] = w^j, j < 2^(TW_LOG-1))
+// w_S^e from the power table of w_{2^TW_LOG} (even/odd layout: kernels.h tw_get)
 __device__ __forceinline__ uint64_t tw_pow(const uint64_t *__restrict__ tw, uint32_t e, uint32_t log_S) {
   return qpk::tw_get(tw, e << (qpk::TW_LOG - log_S));
 }
@@ -338,13 +338,21 @@ __device__ __forceinline__ void pass32(uint64_t *a, uint32_t n) {
 // TAIL = false: stop before the last radix-2^log_S (log_S < 4) levels and
 // return log_S (after the barrier of the last pass), for callers that fold
 // those levels into their output loop (tail_group)
+__host__ __device__ constexpr bool use_pass32(uint32_t log_S, uint32_t n, uint32_t T) {
+  return QP_PASS32 && log_S == 5 && (n >> 4) % 128 == 0 && T % 64 == 0;
+}
+// the log_S ntt_lds_from<.., false> returns for a block of T threads
+__host__ __device__ constexpr uint32_t lds_levels_left(uint32_t log_n, uint32_t log_S, uint32_t T) {
+  while (log_S >= 4) log_S = use_pass32(log_S, 1u << log_n, T) ? 1 : log_S - 4;
+  return log_S;
+}
 template <bool INV, bool TAIL = true>
 __device__ __forceinline__ uint32_t ntt_lds_from(uint64_t *a, uint32_t log_n, uint32_t log_S, const uint64_t *__restrict__ pt) {
   const uint32_t n = 1u << log_n;
   const uint32_t T = blockDim.x;
   // radix-16 passes
   while (log_S >= 4) {
-    if (QP_PASS32 && log_S == 5 && (n >> 4) % 128 == 0 && T % 64 == 0) {
+    if (use_pass32(log_S, n, T)) {
       pass32<INV>(a, n);
       log_S = 1;
       continue;

@@ -129,6 +129,7 @@ struct qp_prover {
   bool quotient_rereads = false;
   bool quotient_fused = false;  // A/B: QPGPU_QUOTIENT=fused selects k_quotient_fused where it applies
   bool has_poseidon_gate = false;
+  bool has_random_access = false;
   bool generic_quotient = false;  // a gate outside k_quotient_1r's set (the recursive verifier's RandomAccess)
   bool pp_generic = false;  // QPGPU_PP_GENERIC=1: the runtime-shape k_pp_rows (A/B)
   uint64_t *h_in = nullptr;  // pinned [max_batch][wg_nin] commit() values
@@ -272,7 +273,9 @@ int setup(qp_prover *P) {
         break;
       case qc::G_RANDOM_ACCESS:
         g.kind[i] = qpk::GK_RANDOM_ACCESS;
-        P->generic_quotient = true;  // k_quotient_1r covers the leaf circuits' six gates only
+        P->has_random_access = true;
+        // k_quotient_1r evaluates the RandomAccessGate of the recursive verifier's width
+        if (cd.gate_params[i] != qpk::RA_QBITS) P->generic_quotient = true;
         break;
       default:
         c->err = "unsupported gate kind for the GPU prover";
@@ -474,6 +477,51 @@ int push_chal(qp_prover *P, uint32_t nb) {
   return QP_OK;
 }
 
+// Every device table a launch sequence reads must exist for this circuit: a
+// missing one becomes QP_ERR_STATE naming it instead of a kernel fault (the
+// class of 0d3293f: the slot -> wire expansion tables were once skipped for
+// host-witness circuits).  which: 0 = prove_batch (d_wires given or not),
+// 1 = device witness generation.
+int check_tables(qp_prover *P, int which, bool wires_on_device) {
+  struct T {
+    const char *name;
+    const void *p;
+  };
+  std::vector<T> need;
+  if (which == 0) {
+    need = {{"tw.fwd", P->ctx->tw.fwd}, {"tw.pt_inv", P->ctx->tw.pt_inv}, {"cs.lde", P->cs.lde.p},
+            {"cs.coeffs", P->cs.coeffs.p}, {"sigmas", P->sigmas.p}, {"kis", P->kis.p},
+            {"wires.coeffs", P->wires.coeffs.p}, {"wires.lde", P->wires.lde.p}, {"wires.dig", P->wires.dig.p},
+            {"zs.vals", P->zs.vals.p}, {"zs.coeffs", P->zs.coeffs.p}, {"zs.lde", P->zs.lde.p},
+            {"zs.dig", P->zs.dig.p}, {"quot.coeffs", P->quot.coeffs.p}, {"quot.lde", P->quot.lde.p},
+            {"quot.dig", P->quot.dig.p}, {"chal", P->chal.p}, {"apow", P->apow.p}, {"prods", P->prods.p},
+            {"qvals", P->qvals.p}, {"cbuf", P->cbuf.p}, {"openings", P->openings.p}, {"comp", P->comp.p},
+            {"fin", P->fin.p}, {"pow_state", P->pow_state.p}, {"pow_found", P->pow_found.p},
+            {"qidx", P->qidx.p}, {"qout", P->qout.p}, {"qtab", P->qtab.p}};
+    if (!wires_on_device) need.push_back({"wires.vals", P->wires.vals.p});
+    for (size_t l = 0; l < P->arity.size(); l++) {
+      need.push_back({"fri.vals", l < P->fvals.size() ? P->fvals[l].p : nullptr});
+      need.push_back({"fri.dig", l < P->fdig.size() ? P->fdig[l].p : nullptr});
+      need.push_back({"fri.coeffs", l < P->fcoef.size() ? P->fcoef[l].p : nullptr});
+    }
+  } else {
+    need = {{"wg_gens", P->wg_gens.p}, {"wg_lvl", P->wg_lvl.p}, {"wg_wslot", P->wg_wslot.p},
+            {"wg_wslot_cm", P->wg_wslot_cm.p}, {"wg_pi_slots", P->wg_pi_slots.p}, {"wg_vals", P->wg_vals.p},
+            {"wg_pis", P->wg_pis.p}, {"wg_err", P->wg_err.p}, {"h_in", P->h_in}};
+    if (P->wg_nin) {
+      need.push_back({"wg_in_slots", P->wg_in_slots.p});
+      need.push_back({"wg_in", P->wg_in.p});
+    }
+  }
+  for (const T &t : need)
+    if (!t.p) {
+      P->ctx->err = std::string("device table '") + t.name + "' is missing for this circuit (" +
+                    (which ? "device witness generation" : "prove") + ")";
+      return QP_ERR_STATE;
+    }
+  return QP_OK;
+}
+
 struct ProofState {
   qh::Challenger t;
   uint64_t pih[4];
@@ -504,6 +552,7 @@ int prove_batch(qp_prover *P, const uint64_t *d_wires, const uint64_t *const *wi
   };
   TRY(hipSetDevice(c->device));
   int rc;
+  if ((rc = check_tables(P, 0, d_wires != nullptr))) return rc;
 
   // ---- 1. wires commitment
   const uint64_t *wv = d_wires;
@@ -607,7 +656,7 @@ int prove_batch(qp_prover *P, const uint64_t *d_wires, const uint64_t *const *wi
     kt_begin(P, 3);
     if (P->quotient_rereads || P->generic_quotient)  // generic gate list (or A/B: QPGPU_QUOTIENT=rereads)
       qpk::k_quotient<2><<<dim3(cdiv(N, 256), nb), 256, 0, s>>>(a);
-    else if (P->R == 80 && P->qdf == 8 && P->has_poseidon_gate && P->quotient_fused)
+    else if (P->R == 80 && P->qdf == 8 && P->has_poseidon_gate && P->quotient_fused && !P->has_random_access)
       qpk::k_quotient_fused<<<dim3(cdiv(N, 256), nb), 256, 0, s>>>(a);
     else
       qpk::k_quotient_1r<<<dim3(cdiv(N, 256), nb), 256, 0, s>>>(a);
@@ -932,6 +981,7 @@ int gen_witness_batch(qp_prover *P, uint32_t nb) {
   qp_ctx *c = P->ctx;
   hipStream_t s = c->stream;
   const uint64_t nw = (uint64_t)P->W << P->log_n;
+  if (int rc = check_tables(P, 1, true)) return rc;
   if (P->wg_nin)
     TRY(hipMemcpyAsync(P->wg_in.p, P->h_in, (size_t)nb * P->wg_nin * 8, hipMemcpyHostToDevice, s));
   qpk::k_witness_init<<<dim3(std::min<unsigned>(cdiv(P->wg_nslots, 256), 256), nb), 256, 0, s>>>(
@@ -1139,6 +1189,15 @@ int qp_prover_prove(qp_prover *P, const qp_witness *const *w, uint32_t nproofs, 
     }
   hipStream_t s = P->ctx->stream;
   const uint64_t nw = (uint64_t)P->W << P->log_n;
+  for (const char *t : {"wg_vals", "wg_wslot_cm", "wg_pi_slots", "wg_pis", "wires.vals"}) {
+    const void *p = !strcmp(t, "wg_vals") ? (const void *)P->wg_vals.p : !strcmp(t, "wg_wslot_cm") ? P->wg_wslot_cm.p
+                  : !strcmp(t, "wg_pi_slots") ? P->wg_pi_slots.p : !strcmp(t, "wg_pis") ? P->wg_pis.p
+                  : P->wires.vals.p;
+    if (!p) {
+      P->ctx->err = std::string("device table '") + t + "' is missing for this circuit (host-witness expansion)";
+      return QP_ERR_STATE;
+    }
+  }
   for (uint32_t done = 0; done < nproofs;) {
     const uint32_t nb = std::min(P->max_batch, nproofs - done);
     std::vector<uint64_t> pis((size_t)nb * P->npis);
@@ -1205,6 +1264,38 @@ int qp_prover_prove_voting_inputs(qp_prover *P, const qp_voting_inputs *in, uint
   } catch (const std::bad_alloc &) {
     return QP_ERR_OOM;
   }
+}
+
+int qp_prover_prove_aggregation(qp_prover *P, const qp_aggregation_chunk *chunks, uint32_t nchunks, uint8_t *out,
+                                size_t stride, size_t *lens) {
+  if (!P || !chunks || !out || !nchunks) return QP_ERR_ARG;
+  if (P->circuit->kind != qp_circuit::AGGREGATION) {
+    P->ctx->err = "prover circuit is not an aggregation circuit";
+    return QP_ERR_ARG;
+  }
+  if (stride < P->proof_len) {
+    P->ctx->err = "output stride smaller than the proof size";
+    return QP_ERR_ARG;
+  }
+  TRY(hipSetDevice(P->ctx->device));
+  try {
+    return prove_inputs(P, aggregation_fill, (const uint8_t *)chunks, sizeof(qp_aggregation_chunk), nchunks, out,
+                        stride, lens);
+  } catch (const std::bad_alloc &) {
+    return QP_ERR_OOM;
+  }
+}
+
+int qp_prover_debug_drop_table(qp_prover *P, const char *name) {
+  if (!P || !name) return QP_ERR_ARG;
+  (void)hipSetDevice(P->ctx->device);
+  (void)hipStreamSynchronize(P->ctx->stream);
+  DevBuf *d = !strcmp(name, "wg_wslot_cm") ? &P->wg_wslot_cm : !strcmp(name, "wg_gens") ? &P->wg_gens
+            : !strcmp(name, "qtab") ? &P->qtab : nullptr;
+  if (!d) return QP_ERR_ARG;
+  if (d->p) (void)hipFree(d->p);
+  d->p = nullptr;
+  return QP_OK;
 }
 
 int qp_prover_debug_force_pow(qp_prover *P, uint64_t witness, int enable) {

@@ -27,6 +27,9 @@ enum GateKindDev : uint32_t {
   GK_ARITH_EXT, GK_MUL_EXT, GK_RANDOM_ACCESS, GK_EXPONENTIATION, GK_REDUCING, GK_REDUCING_EXT, GK_POSEIDON_MDS,
   GK_COSET_INTERP, GK_COUNT
 };
+// RandomAccessGate width k_quotient_1r evaluates (the recursive verifier's
+// RandomAccessGate::new_from_config shape); other widths take k_quotient<2>
+constexpr uint32_t RA_QBITS = 4;
 constexpr uint32_t MAX_GATES_DEV = 16;
 
 struct GateDesc {

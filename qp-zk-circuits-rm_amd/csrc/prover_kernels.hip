@@ -712,7 +712,7 @@ k_quotient_1r(QuotientArgs a) {
   const uint32_t nsel = a.g.nsel;
   const uint64_t *gc = cs + (uint64_t)nsel * N;  // gate-constant columns
   // gates of the circuit by kind (kernel arguments: uniform)
-  int g_const = -1, g_pi = -1, g_bs = -1, g_ar = -1, g_pos = -1;
+  int g_const = -1, g_pi = -1, g_bs = -1, g_ar = -1, g_pos = -1, g_ra = -1;
   for (uint32_t gi = 0; gi < a.g.ngates; gi++) {
     switch (a.g.kind[gi]) {
       case GK_CONSTANT: g_const = (int)gi; break;
@@ -720,6 +720,7 @@ k_quotient_1r(QuotientArgs a) {
       case GK_BASE_SUM: g_bs = (int)gi; break;
       case GK_ARITHMETIC: g_ar = (int)gi; break;
       case GK_POSEIDON: g_pos = (int)gi; break;
+      case GK_RANDOM_ACCESS: g_ra = (int)gi; break;
       default: break;
     }
   }
@@ -847,6 +848,47 @@ k_quotient_1r(QuotientArgs a) {
     const uint64_t f = filter(g_ar);
     acc0 = gfn::add(acc0, gfn::mul(f, sa0));
     acc1 = gfn::add(acc1, gfn::mul(f, sa1));
+  }
+  if (g_ra >= 0) {
+    // RandomAccessGate (the aggregation circuits' recursive verifier): per copy
+    // the bits' boolean checks, the index recomposition and the claimed
+    // element against the list folded bit by bit (plonky2 random_access.rs
+    // eval_unfiltered: list[i] <- b (list[2i+1] - list[2i]) + list[2i]; the
+    // same multilinear value the generic kernel forms as sum_i item_i weight_i),
+    // then the extra constants.  Terms in the generic kernel's order.
+    // (bits = RA_QBITS: the host picks this kernel only for that width)
+    constexpr uint32_t q0 = RA_QBITS, vec = 1u << RA_QBITS;
+    const uint32_t q1 = a.g.param2[g_ra], q2 = a.g.param3[g_ra];
+    const uint32_t routed = (2 + vec) * q1 + q2;
+    uint64_t sr0 = 0, sr1 = 0;
+    uint32_t k = pre;
+    for (uint32_t cp = 0; cp < q1; cp++) {
+      const uint32_t base = (2 + vec) * cp, bw = routed + cp * q0;
+      uint64_t bits[q0];
+      uint64_t idx = 0;
+#pragma unroll
+      for (uint32_t i = 0; i < q0; i++) {
+        bits[i] = WV(bw + i);
+        emit_at(p0, p1, k++, gfn::mul(bits[i], gfn::sub(bits[i], 1)), sr0, sr1);
+      }
+#pragma unroll
+      for (int i = q0 - 1; i >= 0; i--) idx = gfn::add(gfn::add(idx, idx), bits[i]);
+      emit_at(p0, p1, k++, gfn::sub(idx, WV(base)), sr0, sr1);
+      uint64_t list[vec];
+#pragma unroll
+      for (uint32_t i = 0; i < vec; i++) list[i] = WV(base + 2 + i);
+#pragma unroll
+      for (uint32_t lb = 0; lb < q0; lb++) {
+#pragma unroll
+        for (uint32_t i = 0; i < (vec >> (lb + 1)); i++)
+          list[i] = gfn::add(gfn::mul(bits[lb], gfn::sub(list[2 * i + 1], list[2 * i])), list[2 * i]);
+      }
+      emit_at(p0, p1, k++, gfn::sub(list[0], WV(base + 1)), sr0, sr1);
+    }
+    for (uint32_t i = 0; i < q2; i++) emit_at(p0, p1, k++, gfn::sub(gc[(uint64_t)i * N], WV(routed - q2 + i)), sr0, sr1);
+    const uint64_t f = filter(g_ra);
+    acc0 = gfn::add(acc0, gfn::mul(f, sr0));
+    acc1 = gfn::add(acc1, gfn::mul(f, sr1));
   }
   if (g_pos >= 0) {
     TermAcc A;

@@ -139,7 +139,7 @@ std::string parse_common(const uint8_t *b, size_t n, InnerCommon &c) {
     c.gates.push_back(g);
   }
   if (r.err || r.pos != n) return "malformed CommonCircuitData bytes";
-  if (c.num_challenges != 2 || c.hiding || c.zero_knowledge && c.hiding) return "unsupported inner config";
+  if (c.num_challenges != 2 || c.hiding) return "unsupported inner config";
   if (c.selector_indices.size() != c.gates.size() || c.k_is.size() != c.num_routed_wires)
     return "inconsistent CommonCircuitData";
   for (auto &g : c.gates)

@@ -28,7 +28,10 @@ struct DevGenD {  // == qc::DevGen
   uint32_t s[4];
   uint64_t k0, k1;
 };
-enum : uint32_t { WG_CONSTANT = 0, WG_ARITH, WG_POSEIDON, WG_BASE_SPLIT, WG_EQUALITY };
+enum : uint32_t { WG_CONSTANT = 0, WG_ARITH, WG_POSEIDON, WG_BASE_SPLIT, WG_EQUALITY,
+                  WG_WIRE_SPLIT, WG_EXT_DIV, WG_RANDOM_ACCESS };
+// RandomAccessGate{bits 4, copies 4, extra constants 2} wire layout (circuit.h ra_wire_*)
+constexpr uint32_t RA_BITS = 4, RA_VEC = 16, RA_COPIES = 4, RA_EXTRA = 2;
 
 __device__ __forceinline__ bool wset(uint64_t *v, uint32_t s, uint64_t x) {
   const unsigned long long old = atomicCAS((unsigned long long *)(v + s), (unsigned long long)UNSET,
@@ -87,6 +90,40 @@ __device__ bool run_gen(const DevGenD &g, uint64_t *v, const uint32_t *wslot, ui
       if (!in_ok) return false;
       const bool eq = x == y;
       return wset(v, g.s[2], eq ? 1 : 0) && wset(v, g.s[3], eq ? 0 : gl::inv(gl::sub(x, y)));
+    }
+    case WG_WIRE_SPLIT: {
+      // WireSplitGenerator (gadgets/split_base.rs): the integer's `limbs`-bit
+      // chunks into the sum wires of s[1] consecutive BaseSum gates
+      uint64_t x = rd(v, g.s[0], in_ok);
+      if (!in_ok) return false;
+      bool ok = true;
+      for (uint32_t j = 0; j < g.s[1]; j++) {
+        const uint64_t sum = limbs < 64 ? (x & ((1ull << limbs) - 1)) : x;
+        x = limbs < 64 ? x >> limbs : 0;
+        ok &= wset(v, wslot[(uint64_t)(g.row + j) * W], sum);
+      }
+      return ok;
+    }
+    case WG_EXT_DIV: {
+      // QuotientGeneratorExtension (gadgets/arithmetic_extension.rs): (a + bX) / (c + dX)
+      const gl::ext num{rd(v, g.s[0], in_ok), rd(v, g.s[1], in_ok)};
+      const gl::ext den{rd(v, g.s[2], in_ok), rd(v, g.s[3], in_ok)};
+      if (!in_ok || (den.c0 == 0 && den.c1 == 0)) return false;
+      const gl::ext q = gl::ext_mul(num, gl::ext_inv(den));
+      return wset(v, (uint32_t)g.k0, q.c0) && wset(v, (uint32_t)(g.k0 >> 32), q.c1);
+    }
+    case WG_RANDOM_ACCESS: {
+      // RandomAccessGenerator (gates/random_access.rs) of copy s[0]
+      const uint32_t c = g.s[0];
+      const uint32_t *ws = wslot + (uint64_t)g.row * W + (2 + RA_VEC) * c;
+      const uint64_t idx = rd(v, ws[0], in_ok);
+      if (!in_ok || idx >= RA_VEC) return false;
+      const uint64_t item = rd(v, ws[2 + idx], in_ok);
+      if (!in_ok) return false;
+      bool ok = wset(v, ws[1], item);
+      const uint32_t *wb = wslot + (uint64_t)g.row * W + (2 + RA_VEC) * RA_COPIES + RA_EXTRA + RA_BITS * c;
+      for (uint32_t i = 0; i < RA_BITS; i++) ok &= wset(v, wb[i], (idx >> i) & 1);
+      return ok;
     }
     case WG_POSEIDON: {
       // PoseidonGenerator (gates/poseidon.rs), wire layout SURVEY.md A.5

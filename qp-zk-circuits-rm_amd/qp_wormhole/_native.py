@@ -109,6 +109,7 @@ def lib():
         "qp_circuit_common_data": (ctypes.c_int, [VP, ctypes.c_char_p, ctypes.c_size_t,
                                                   ctypes.POINTER(ctypes.c_size_t)]),
         "qp_circuit_constants_sigmas": (ctypes.c_int, [VP, U64P]),
+        "qp_circuit_constants_sigmas_coeffs": (ctypes.c_int, [VP, U64P]),
         "qp_wormhole_commit": (ctypes.c_int, [VP, VP, PP, ctypes.c_char_p, ctypes.c_size_t]),
         "qp_voting_circuit_new": (ctypes.c_int, [ctypes.c_int, PP]),
         "qp_voting_commit": (ctypes.c_int, [VP, VP, PP, ctypes.c_char_p, ctypes.c_size_t]),
@@ -134,8 +135,11 @@ def lib():
                                                            ctypes.POINTER(ctypes.c_size_t)]),
         "qp_prover_prove_voting_inputs": (ctypes.c_int, [VP, VP, ctypes.c_uint32, ctypes.c_char_p, ctypes.c_size_t,
                                                          ctypes.POINTER(ctypes.c_size_t)]),
+        "qp_prover_prove_aggregation": (ctypes.c_int, [VP, VP, ctypes.c_uint32, ctypes.c_char_p, ctypes.c_size_t,
+                                                       ctypes.POINTER(ctypes.c_size_t)]),
         "qp_prover_set_timing": (ctypes.c_int, [VP, ctypes.c_int]),
         "qp_prover_debug_force_pow": (ctypes.c_int, [VP, ctypes.c_uint64, ctypes.c_int]),
+        "qp_prover_debug_drop_table": (ctypes.c_int, [VP, ctypes.c_char_p]),
         "qp_prover_set_host_threads": (ctypes.c_int, [VP, ctypes.c_uint32]),
         "qp_prover_kernel_stats": (ctypes.c_int, [VP, ctypes.POINTER(ctypes.c_double), ctypes.POINTER(ctypes.c_double),
                                                   ctypes.POINTER(ctypes.c_uint64), ctypes.c_uint32, ctypes.c_int]),

@@ -84,6 +84,21 @@ class _LevelProver:
         self.lock = threading.Lock()
 
     def prove_chunks(self, chunks, inner_vo: bytes) -> List[AggregatedProof]:
+        if os.environ.get("QP_AGG_WITNESS", "device") == "host":
+            return self._prove_chunks_host(chunks, inner_vo)
+        # device witness generation (qp_prover_prove_aggregation): the host only
+        # deserializes the inner proofs into the circuit's input targets
+        npis = self.circuit.num_public_inputs
+        out = []
+        with self.lock:
+            for i in range(0, len(chunks), self.max_batch):
+                grp = chunks[i:i + self.max_batch]
+                for data in self.prover.prove_aggregation(inner_vo, [[p.to_bytes() for p in ch] for ch in grp]):
+                    pis = struct.unpack_from(f"<{npis}Q", data, len(data) - 8 * npis)
+                    out.append(AggregatedProof(ProofWithPublicInputs(data, pis), self.data))
+        return out
+
+    def _prove_chunks_host(self, chunks, inner_vo: bytes) -> List[AggregatedProof]:
         # aggregate_chunk's witnesses on host threads (the C call releases the GIL;
         # ~50 ms each for two leaves), each max_batch group proven on the GPU as
         # soon as its witnesses exist while the next group's are generated
@@ -152,13 +167,23 @@ def aggregate_level(proofs, common_data: bytes, verifier_only: bytes, config: Tr
     (default: the GPU level prover; tests inject a CPU one)."""
     k = config.tree_branching_factor
     proofs = [_as_proof(p) for p in proofs]
-    if len(proofs) % k:
-        raise ValueError(f"{len(proofs)} proofs do not split into chunks of {k}")
+    if not proofs or k < 1:
+        raise ValueError("aggregate_level: no proofs / branching factor < 1")
     chunks = [proofs[i:i + k] for i in range(0, len(proofs), k)]
-    # up to 32 aggregation proofs per GPU batch (2.7 vs 3.2 ms per proof at 16;
-    # tools/agg_bench.py, profiles/r03_agg_bench.log)
-    lp = (backend or _level_prover)(common_data, k, device, max(1, min(len(chunks), 32)))
-    return lp.prove_chunks(chunks, verifier_only)
+    # proofs.chunks(k) (tree.rs:86-89): a shorter last chunk is aggregated by a
+    # circuit built for its own size (the next level can only take its proof
+    # if it is alone, as in the reference, whose next level uses proofs[0]'s
+    # circuit data for every proof)
+    tail = chunks.pop() if len(chunks[-1]) != k else None
+    make = backend or _level_prover
+    out = []
+    if chunks:
+        # up to 32 aggregation proofs per GPU batch (2.7 vs 3.2 ms per proof at 16;
+        # tools/agg_bench.py, profiles/r03_agg_bench.log)
+        out = make(common_data, k, device, max(1, min(len(chunks), 32))).prove_chunks(chunks, verifier_only)
+    if tail is not None:
+        out += make(common_data, len(tail), device, 1).prove_chunks([tail], verifier_only)
+    return out
 
 
 def aggregate_to_tree(leaf_proofs, common_data: bytes, verifier_only: bytes,

@@ -194,10 +194,10 @@ class Circuit:
     def __init__(self, handle, kind):
         self.h, self.kind = handle, kind
         self.zk = False
-        info = (ctypes.c_uint32 * 8)()
+        info = (ctypes.c_uint32 * 9)()
         lib().qp_circuit_info(self.h, info)
         (self.degree_bits, self.num_wires, self.num_routed_wires, self.num_constants, self.num_public_inputs,
-         self.gates_used, self.num_gate_constraints) = list(info)[:7]
+         self.gates_used, self.num_gate_constraints, self.num_generators, self.witness_levels) = list(info)
         self.n = 1 << self.degree_bits
 
     @classmethod
@@ -267,6 +267,14 @@ class Circuit:
         rc = lib().qp_circuit_constants_sigmas(self.h, out)
         if rc:
             raise QpError(rc, "qp_circuit_constants_sigmas")
+        return out
+
+    def constants_sigmas_coeffs(self):
+        """Coefficients of the constants||sigmas columns (PolynomialValues::ifft, host)."""
+        out = np.zeros((self.num_constants + self.num_routed_wires, self.n), np.uint64)
+        rc = lib().qp_circuit_constants_sigmas_coeffs(self.h, out)
+        if rc:
+            raise QpError(rc, "qp_circuit_constants_sigmas_coeffs")
         return out
 
     def commit(self, inputs) -> Witness:

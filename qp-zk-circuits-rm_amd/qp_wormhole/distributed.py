@@ -131,35 +131,100 @@ def run_steps(prove_share, nprovers, steps, dist=None, slot=0, device="cpu", pip
     return last
 
 
+def log_exact(n: int, base: int):
+    """k with base**k == n (k >= 0), else None."""
+    if n < 1 or base < 2:
+        return None
+    k, p = 0, 1
+    while p < n:
+        p, k = p * base, k + 1
+    return k if p == n else None
+
+
+def check_subtree_shards(n_local: int, branching: int, dist, device="cpu"):
+    """Cross-rank preconditions of per-rank subtree aggregation, checked on every
+    rank through one all_gather of the local leaf counts BEFORE any aggregation
+    or gather: all ranks hold the same number of leaves, a power (>= 1) of the
+    branching factor, and the world size is a power of it.  Every rank raises
+    the same error otherwise (no rank is left waiting in a collective, and no
+    rank aggregates roots of subtrees of different depths)."""
+    import torch
+    world = dist.get_world_size()
+    valid = log_exact(n_local, branching) not in (None, 0)
+    cnt = torch.tensor([n_local if valid else -1], dtype=torch.int64, device=device)
+    counts = [torch.zeros_like(cnt) for _ in range(world)]
+    dist.all_gather(counts, cnt)
+    counts = [int(c.item()) for c in counts]
+    bad = [r for r, c in enumerate(counts) if c < 0]
+    if bad:
+        raise ValueError(f"rank(s) {bad} hold a leaf count that is not a power (>= 1) of the branching factor "
+                         f"{branching} (counts {counts})")
+    if len(set(counts)) != 1:
+        raise ValueError(f"ranks hold different leaf counts {counts}: subtree roots would come from circuits of "
+                         f"different depths")
+    if log_exact(world, branching) is None:
+        raise ValueError(f"world size {world} is not a power of the branching factor {branching}")
+
+
 def aggregate_subtrees(local_proofs, common: bytes, verifier_only: bytes, branching: int, dist,
-                       device="cpu", gpu: int = 0, dst: int = 0, backend=None):
+                       device="cpu", gpu: int = 0, dst: int = 0, backend=None, timings=None):
     """Per-rank subtree aggregation (the levels of tree.rs:92-103
     are independent per chunk): each rank aggregates its own leaf proofs into one
     subtree root (aggregate_to_tree with depth log_branching(local count)); only
     the roots cross the interconnect (one gather of world proofs instead of every
     leaf); rank dst aggregates the roots into the tree root.  Every rank must hold
-    branching**k leaves (equal k) and world must be a power of branching.
-    Returns the root AggregatedProof on dst, None elsewhere."""
+    branching**k leaves (equal k) and world must be a power of branching
+    (check_subtree_shards, before any work).  dist=None: one rank.
+    Returns the root AggregatedProof on dst, None elsewhere; timings (a dict)
+    receives the seconds of the stages: subtree_s, gather_s, top_s."""
+    import time
     from .aggregator import TreeAggregationConfig, aggregate_to_tree
     from .prover import ProofWithPublicInputs
-    world, rank = dist.get_world_size(), dist.get_rank()
-    n, depth = len(local_proofs), 0
-    while branching ** depth < n:
-        depth += 1
-    if branching ** depth != n or n < branching:
-        raise ValueError(f"{n} local proofs are not a power (>= 1) of the branching factor {branching}")
+    world, rank = (dist.get_world_size(), dist.get_rank()) if dist is not None else (1, 0)
+    if dist is not None:
+        check_subtree_shards(len(local_proofs), branching, dist, device)
+    elif log_exact(len(local_proofs), branching) in (None, 0):
+        raise ValueError(f"{len(local_proofs)} local proofs are not a power (>= 1) of the branching factor "
+                         f"{branching}")
+    depth = log_exact(len(local_proofs), branching)
+    wdepth = log_exact(world, branching)
+    tm = timings if timings is not None else {}
+    t0 = time.perf_counter()
     sub = aggregate_to_tree(local_proofs, common, verifier_only, TreeAggregationConfig.new(branching, depth),
                             gpu, backend)
-    roots = gather_proofs([sub.proof.to_bytes()], len(sub.proof.to_bytes()), dist, device=device, dst=dst)
+    t1 = time.perf_counter()
+    tm["subtree_s"] = t1 - t0
+    if dist is not None:
+        roots = gather_proofs([sub.proof.to_bytes()], len(sub.proof.to_bytes()), dist, device=device, dst=dst)
+    else:
+        roots = [sub.proof.to_bytes()]
+    t2 = time.perf_counter()
+    tm["gather_s"] = t2 - t1
+    tm["top_s"] = 0.0
     if rank != dst:
         return None
     if world == 1:
         return sub
-    wdepth = 0
-    while branching ** wdepth < world:
-        wdepth += 1
-    if branching ** wdepth != world:
-        raise ValueError(f"world size {world} is not a power of the branching factor {branching}")
     cd = sub.circuit_data
-    return aggregate_to_tree([ProofWithPublicInputs(r, []) for r in roots], cd.common, cd.verifier_only,
+    root = aggregate_to_tree([ProofWithPublicInputs(r, []) for r in roots], cd.common, cd.verifier_only,
                              TreeAggregationConfig.new(branching, wdepth), gpu, backend)
+    tm["top_s"] = time.perf_counter() - t2
+    return root
+
+
+def pipeline_aggregate_step(prove_leaves, common: bytes, verifier_only: bytes, branching: int, dist=None,
+                            device="cpu", gpu: int = 0, dst: int = 0, backend=None):
+    """BASELINE configs[3] as one step ("Batch 2048 proofs sharded 8xMI355X,
+    RCCL-gather leaves into recursive aggregator"; wormhole/aggregator/src/
+    aggregator.rs:74-92, circuits/tree.rs:55-103): every rank proves its batch
+    of leaves (prove_leaves() -> serialized proofs), aggregates them into its
+    subtree root on its own GPU, the roots are gathered to dst over RCCL, and dst
+    aggregates them into the tree root.  Returns (root on dst / None, stage
+    seconds {leaves_s, subtree_s, gather_s, top_s})."""
+    import time
+    t0 = time.perf_counter()
+    leaves = prove_leaves()
+    tm = {"leaves_s": time.perf_counter() - t0}
+    root = aggregate_subtrees(leaves, common, verifier_only, branching, dist, device=device, gpu=gpu, dst=dst,
+                              backend=backend, timings=tm)
+    return root, tm

@@ -85,6 +85,42 @@ class Prover:
             return []
         return self.prove_inputs_array(self.inputs_array(inputs), len(inputs))
 
+    def prove_aggregation(self, verifier_only: bytes, chunks, zk_randomness=None):
+        """aggregate_chunk (tree.rs:106-143) for every chunk of inner proofs as one
+        batch: the proof bytes are deserialized into the circuit's targets on the
+        host pool, the recursive verifier's witness is generated on the device
+        (qp_prover_prove_aggregation).  zk_randomness: per chunk a list of
+        num_wires - 4 felts, or None (OS randomness under zk, zeros otherwise)."""
+        from .circuits import _zk_ptr
+        nb = len(chunks)
+        if not nb:
+            return []
+
+        class _Chunk(ctypes.Structure):
+            _fields_ = [("verifier_only", ctypes.c_char_p), ("vlen", ctypes.c_size_t),
+                        ("proofs", ctypes.c_void_p), ("lens", ctypes.c_void_p), ("nproofs", ctypes.c_uint32),
+                        ("zk_randomness", ctypes.c_void_p)]
+
+        vo = bytes(verifier_only)
+        arr = (_Chunk * nb)()
+        keep = [vo]
+        for i, ch in enumerate(chunks):
+            ps = [bytes(p) for p in ch]
+            pa = (ctypes.c_char_p * len(ps))(*ps)
+            la = (ctypes.c_size_t * len(ps))(*[len(p) for p in ps])
+            zp, zk = _zk_ptr(zk_randomness[i] if zk_randomness is not None else None)
+            keep += [ps, pa, la, zk]
+            arr[i].verifier_only, arr[i].vlen = vo, len(vo)
+            arr[i].proofs, arr[i].lens, arr[i].nproofs = ctypes.cast(pa, ctypes.c_void_p), \
+                ctypes.cast(la, ctypes.c_void_p), len(ps)
+            arr[i].zk_randomness = ctypes.cast(zp, ctypes.c_void_p) if zp else None
+        out = ctypes.create_string_buffer(self.proof_size * nb)
+        lens = (ctypes.c_size_t * nb)()
+        self.ctx.check(lib().qp_prover_prove_aggregation(self.h, ctypes.cast(arr, ctypes.c_void_p), nb, out,
+                                                         self.proof_size, lens), "qp_prover_prove_aggregation")
+        raw = out.raw
+        return [raw[i * self.proof_size:i * self.proof_size + lens[i]] for i in range(nb)]
+
     def prove_wires(self, wires, pis):
         wires = np.ascontiguousarray(wires, dtype=np.uint64)
         pis = np.ascontiguousarray(pis, dtype=np.uint64)
@@ -177,14 +213,15 @@ CONFIGS = ("standard_recursion_config", "standard_recursion_zk_config")
 # refuses data whose commitment differs.
 #
 # An upstream prover.bin (ProverOnlyCircuitData::to_bytes of the reference's
-# generate_circuit_binaries, circuit-builder/src/lib.rs:54-60) is accepted by
-# its circuit digest: plonky2 writes the digest (HashOut, 4 u64) right before
-# the lookup tables, which are two empty vectors (u64 length 0 each) for a
-# lookup-free circuit such as Wormhole, so the file ends with digest || 0u64 ||
-# 0u64.  The native circuit IS the reference's (same constants||sigmas cap and
-# circuit digest: tests/test_reference_layout.py), so an equal digest means the
-# file describes this circuit's preprocessing; its generators are not needed
-# (witness generation is native).
+# generate_circuit_binaries, circuit-builder/src/lib.rs:54-60; read back by
+# WormholeProver::new_from_bytes, prover/src/lib.rs:105-137) is walked by
+# upstream_prover_layout: the framing is restated from upstream plonky2's
+# write_prover_only_circuit_data (parity unpinned: the reference commits no
+# such file) and the walk checks the CONTENT the preprocessing fixes, so a
+# truncated or foreign blob is refused even if it ends like one.  The native
+# circuit IS the reference's (same constants||sigmas columns, cap and circuit
+# digest: tests/test_reference_layout.py), so a file of the reference's circuit
+# passes; its generators are not needed (witness generation is native).
 PROVER_MAGIC = b"QPGPU-PROVER-ONLY\0"
 PROVER_VERSION = 1
 _KINDS = {"wormhole": 0, "voting": 1}
@@ -227,28 +264,155 @@ def prover_only_bytes(circuit, prover):
     return head + hashlib.sha256(common).digest() + _verifier_only(circuit, prover)
 
 
+# plonky2 Goldilocks POWER_OF_TWO_GENERATOR: w_{2^k} = TWO_ADIC_GEN^(2^(32-k))
+TWO_ADIC_GEN = 7277203076849721926
+
+
+def _goldilocks_powers(w, n):
+    out = np.empty(n, np.uint64)
+    x = 1
+    for i in range(n):
+        out[i] = x
+        x = x * w % 0xFFFFFFFF00000001
+    return out
+
+
+def upstream_prover_layout(data, circuit, cap=None):
+    """Walk an upstream ProverOnlyCircuitData::to_bytes file of `circuit` and
+    return its circuit digest (4 ints), or raise ValueError naming what is
+    missing.  Restated framing (plonky2 util/serialization write_prover_only_
+    circuit_data), in file order:
+      generators.len() u64, the generators (tag u32 + body each),
+      generator_indices_by_watches, then the constants||sigmas PolynomialBatch:
+      polynomials.len() u64 and per polynomial its coefficients as a field vec
+      (u64 length + values), the MerkleTree (leaves, digests, cap: u64 length +
+      16 hashes), degree_log, rate_bits, blinding; sigmas.len() u64 and the
+      sigma value vectors; the subgroup (powers of w_n); public-input targets;
+      representative_map; the fft root table (optional); circuit_digest
+      (4 u64); lookup_rows and lut_to_lookups (empty: two u64 zeros).
+    What is checked is what the preprocessing fixes: this circuit's
+    constants||sigmas coefficients (every column, consecutive), the cap
+    (when given: the caller's device-computed one), the 80 sigma value
+    columns, the subgroup, and the empty lookup tail.  The generator bodies and
+    the Merkle leaves/digests are skipped by search, so only their presence is
+    restated, not their layout."""
+    data = bytes(data)
+    if data[:len(PROVER_MAGIC)] == PROVER_MAGIC:
+        raise ValueError("this backend's prover.bin, not an upstream one")
+    if len(data) < 8 + 48 or data[-16:] != bytes(16):
+        raise ValueError("does not end with the circuit digest and empty lookup tables")
+    (ngen,) = struct.unpack_from("<Q", data, 0)
+    dig = struct.unpack_from("<4Q", data, len(data) - 48)
+    if not 0 < ngen < len(data) // 8 or any(x >= 0xFFFFFFFF00000001 for x in dig):
+        raise ValueError("implausible generator count or non-canonical digest")
+    n = circuit.n
+    N = struct.pack("<Q", n)
+    coeffs = circuit.constants_sigmas_coeffs()
+    vals = circuit.constants_sigmas()
+    ncs = coeffs.shape[0]
+
+    def column(pos, arr, what):
+        blob = N + arr.tobytes()
+        if data[pos:pos + len(blob)] != blob:
+            raise ValueError(f"{what} does not follow at offset {pos}")
+        return pos + len(blob)
+
+    # the PolynomialBatch's coefficient columns: located by column 0, then every
+    # column must follow at the same gap (0 or 8 extra bytes per polynomial)
+    p0 = data.find(N + coeffs[0].tobytes(), 8 + 8 * ngen)
+    if p0 < 0:
+        raise ValueError("constants||sigmas coefficients of this circuit not found")
+    if struct.pack("<Q", ncs) not in data[max(0, p0 - 16):p0]:
+        raise ValueError("polynomial count missing before the coefficients")
+    e = p0 + 8 + 8 * n
+    gap = None
+    for g in (0, 8):
+        if data[e + g:e + g + 8 + 8 * n] == N + coeffs[1].tobytes():
+            gap = g
+            break
+    if gap is None:
+        raise ValueError("constants||sigmas coefficient column 1 does not follow column 0")
+    for c in range(1, ncs):
+        e = column(e + gap, coeffs[c], f"coefficient column {c}")
+    # the Merkle tree's cap (the leaves and digests precede it)
+    pos = e
+    if cap is not None:
+        cb = struct.pack("<Q", len(cap) // 4) + np.ascontiguousarray(cap, dtype=np.uint64).tobytes()
+        pc = data.find(cb, e)
+        if pc < 0:
+            raise ValueError("constants||sigmas Merkle cap differs from this circuit's")
+        pos = pc + len(cb)
+    # sigmas: count, then the value vectors
+    nsig = ncs - circuit.num_constants
+    ps = data.find(struct.pack("<Q", nsig) + N + vals[circuit.num_constants].tobytes(), pos)
+    if ps < 0:
+        raise ValueError("sigma columns of this circuit not found")
+    e = ps + 8
+    for j in range(nsig):
+        e = column(e, vals[circuit.num_constants + j], f"sigma column {j}")
+    # subgroup: powers of w_n
+    w = pow(TWO_ADIC_GEN, 1 << (32 - circuit.degree_bits), 0xFFFFFFFF00000001)
+    e = column(e, _goldilocks_powers(w, n), "subgroup")
+    # public_inputs: target vec (write_target: bool Wire? + row, column | index)
+    end = len(data) - 48
+    try:
+        (npi,) = struct.unpack_from("<Q", data, e)
+        if npi != circuit.num_public_inputs:
+            raise ValueError(f"{npi} public-input targets, the circuit has {circuit.num_public_inputs}")
+        e += 8
+        for _ in range(npi):
+            e += 17 if data[e] == 1 else 9 if data[e] == 0 else 1 << 62
+        # representative_map: one entry per wire target and virtual target
+        (nrep,) = struct.unpack_from("<Q", data, e)
+        if nrep < n * circuit.num_wires:
+            raise ValueError(f"representative_map of {nrep} entries for {n} x {circuit.num_wires} wires")
+        e += 8 + 8 * nrep
+        # fft_root_table: Option<Vec<Vec<F>>>
+        if data[e] == 1:
+            (k,) = struct.unpack_from("<Q", data, e + 1)
+            e += 9
+            for _ in range(k):
+                (m,) = struct.unpack_from("<Q", data, e)
+                e += 8 + 8 * m
+        elif data[e] == 0:
+            e += 1
+        else:
+            raise ValueError("malformed fft_root_table")
+    except (struct.error, IndexError):
+        raise ValueError("truncated after the subgroup") from None
+    if e != end:
+        raise ValueError(f"{end - e} bytes between the fft root table and the circuit digest")
+    return dig
+
+
 def upstream_prover_digest(data):
-    """Circuit digest (4 u64) of an upstream ProverOnlyCircuitData::to_bytes file of a
-    lookup-free circuit, or None when `data` does not end like one."""
+    """Circuit digest of a blob that ENDS like an upstream prover.bin (no
+    structural walk; upstream_prover_layout does that), or None."""
     data = bytes(data)
     if data[:len(PROVER_MAGIC)] == PROVER_MAGIC or len(data) < 8 + 48 or data[-16:] != bytes(16):
         return None
-    (ngen,) = struct.unpack_from("<Q", data, 0)   # generators.len() opens the file
+    (ngen,) = struct.unpack_from("<Q", data, 0)
     dig = struct.unpack_from("<4Q", data, len(data) - 48)
     if not 0 < ngen < len(data) or any(x >= 0xFFFFFFFF00000001 for x in dig):
         return None
     return dig
 
 
-def _parse_prover_only(data, common_bytes):
+def _parse_prover_only(data, common_bytes, circuit=None, vo=None):
     """-> (zk, degree_bits, VerifierOnlyCircuitData bytes) for this backend's
-    prover.bin, or (None, None, circuit digest) for an upstream one."""
+    prover.bin, or (None, None, circuit digest) for an upstream one, which is
+    walked (upstream_prover_layout) against `circuit` and the constants||sigmas
+    cap of its VerifierOnlyCircuitData bytes `vo`."""
     data = bytes(data)
     n = len(PROVER_MAGIC)
-    if data[:n] != PROVER_MAGIC:
-        dig = upstream_prover_digest(data)
-        if dig is not None:
-            return None, None, dig
+    if data[:n] != PROVER_MAGIC and upstream_prover_digest(data) is not None:
+        if circuit is None:
+            raise ValueError("an upstream prover.bin needs the circuit to be checked against")
+        cap = None
+        if vo is not None:
+            (h,) = struct.unpack_from("<Q", vo, 0)
+            cap = np.frombuffer(vo, np.uint64, 4 << h, 8)
+        return None, None, upstream_prover_layout(data, circuit, cap)
     if len(data) < n + 10 + 32 or data[:n] != PROVER_MAGIC:
         raise ValueError("neither this backend's prover.bin (bad magic) nor an upstream plonky2 "
                          "ProverOnlyCircuitData::to_bytes file of a lookup-free circuit")
@@ -330,13 +494,13 @@ class WormholeProver:
         cfg = _config_of_common(common_bytes)
         if cfg is None:
             raise ValueError("Failed to deserialize common circuit data")
-        try:
-            _, _, vd = _parse_prover_only(prover_only_bytes, common_bytes)
-        except ValueError as e:
-            raise ValueError(f"Failed to deserialize prover only data: {e}") from None
         self = cls(cfg, device)
         with self._prove_lock:
             mine = _verifier_only(self.circuit, self.prover)
+        try:
+            _, _, vd = _parse_prover_only(prover_only_bytes, common_bytes, self.circuit, mine)
+        except ValueError as e:
+            raise ValueError(f"Failed to deserialize prover only data: {e}") from None
         if not _same_preprocessing(mine, vd):
             raise ValueError("Failed to deserialize prover only data: preprocessed commitment differs")
         return self
@@ -351,15 +515,16 @@ class WormholeProver:
             raise ValueError(f"Failed to deserialize common circuit data from {str(common_data_path)!r}")
         with open(prover_data_path, "rb") as f:
             pb = f.read()
-        try:
-            _, _, vd = _parse_prover_only(pb, common)
-        except ValueError as e:
-            raise ValueError(f"Failed to deserialize prover only data from {str(prover_data_path)!r}: {e}") from None
         self = cls(cfg, device)
         with self._prove_lock:
-            if not _same_preprocessing(_verifier_only(self.circuit, self.prover), vd):
-                raise ValueError(f"Failed to deserialize prover only data from {str(prover_data_path)!r}: "
-                                 "preprocessed commitment differs")
+            mine = _verifier_only(self.circuit, self.prover)
+        try:
+            _, _, vd = _parse_prover_only(pb, common, self.circuit, mine)
+        except ValueError as e:
+            raise ValueError(f"Failed to deserialize prover only data from {str(prover_data_path)!r}: {e}") from None
+        if not _same_preprocessing(mine, vd):
+            raise ValueError(f"Failed to deserialize prover only data from {str(prover_data_path)!r}: "
+                             "preprocessed commitment differs")
         return self
 
     @classmethod

@@ -213,3 +213,97 @@ def _worker_subtrees(rank, world, port, q):
 def test_subtree_aggregation_world2_gloo():
     ok, pis_ok = _run(_worker_subtrees, 2)
     assert ok and pis_ok
+
+
+def _worker_uneven(rank, world, port, q, counts):
+    """aggregate_subtrees with invalid or unequal shards: every rank raises the
+    same error from the count exchange, before any aggregation (no rank is left
+    in a collective; no backend call happens)."""
+    import torch.distributed as dist
+
+    from qp_wormhole.distributed import aggregate_subtrees
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    calls = []
+
+    def backend(*a):
+        calls.append(a)
+        raise AssertionError("aggregation must not start")
+    try:
+        aggregate_subtrees([b"x"] * counts[rank], b"", b"", 2, dist, backend=backend)
+        msg = None
+    except ValueError as e:
+        msg = str(e)
+    dist.barrier()
+    q.put((rank, msg, len(calls)))
+    dist.destroy_process_group()
+
+
+def _run_all(target, world, *args):
+    import torch.multiprocessing as mp
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=target, args=(r, world, port, q) + args) for r in range(world)]
+    for p in procs:
+        p.start()
+    got = sorted(q.get(timeout=180) for _ in range(world))
+    for p in procs:
+        p.join(timeout=180)
+        assert p.exitcode == 0
+    return got
+
+
+@pytest.mark.parametrize("world,counts,frag", [(2, (4, 2), "different leaf counts"),
+                                               (2, (3, 4), "rank(s) [0]"),
+                                               (3, (2, 2, 2), "world size 3")])
+def test_subtree_shards_checked_on_every_rank(world, counts, frag):
+    got = _run_all(_worker_uneven, world, counts)
+    msgs = {m for _, m, _ in got}
+    assert len(msgs) == 1 and frag in msgs.pop()
+    assert all(c == 0 for _, _, c in got)
+
+
+def _worker_pipeline(rank, world, port, q):
+    """BASELINE configs[3] as bench.py times it (distributed.pipeline_aggregate_step):
+    each rank proves its leaves (stub: the reference's two proofs), aggregates
+    its subtree, the roots are gathered, rank 0 aggregates them.  Oracle CPU
+    prover as the backend."""
+    import struct
+
+    import torch.distributed as dist
+
+    from agg_oracle_backend import oracle_backend
+    from qp_wormhole.distributed import pipeline_aggregate_step
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    from current_circuit_vd import current_circuit_verifier_data
+    from oracle_lib import golden, lib as olib
+    from test_oracle_golden import current_common_bytes
+    cb = current_common_bytes()
+    vd = current_circuit_verifier_data(cb)[0]
+    fx = [golden("dummy_proof.bin"), golden("dummy_proof_zk.bin")]
+
+    def prove_leaves():
+        return fx if rank == 0 else fx[::-1]
+    root, tm = pipeline_aggregate_step(prove_leaves, cb, vd[:len(vd) - len(cb)], 2, dist, backend=oracle_backend)
+    if rank == 0:
+        rvd = root.circuit_data.verifier_data()
+        ok = olib().ora_verify(rvd, len(rvd), root.proof.to_bytes(), len(root.proof.to_bytes())) == 0
+        want = []
+        for r in range(world):
+            for pf in (fx if r == 0 else fx[::-1]):
+                want += list(struct.unpack_from("<16Q", pf, len(pf) - 128))
+        q.put((ok, [int(x) for x in root.proof.public_inputs] == want, sorted(tm)))
+    else:
+        assert root is None
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+def test_configs3_pipeline_step_world2_gloo():
+    ok, pis_ok, stages = _run(_worker_pipeline, 2)
+    assert ok and pis_ok
+    assert stages == ["gather_s", "leaves_s", "subtree_s", "top_s"]

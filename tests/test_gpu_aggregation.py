@@ -116,3 +116,57 @@ def test_deep_subtree_root_carries_every_leaf_public_input(reference_leaves):
     for pf in ls:
         want += list(struct.unpack_from("<16Q", pf, len(pf) - 128))
     assert root.proof.public_inputs == want
+
+
+def _device_vs_host(circ, vo, chunks, zk=None):
+    """qp_prover_prove_aggregation (witness generated on the device) vs the host
+    witness path (qp_aggregation_commit + qp_prover_prove) of the same chunks."""
+    import qp_wormhole
+    p = qp_wormhole.Prover(qp_wormhole.Context(0), circ, max_batch=len(chunks))
+    dev = p.prove_aggregation(vo, chunks, zk_randomness=zk)
+    ws = [circ.commit_proofs(vo, ch, zk_randomness=None if zk is None else zk[i]) for i, ch in enumerate(chunks)]
+    host = p.prove_witnesses(ws)
+    vd = p.verifier_data()
+    p.free()
+    return dev, host, vd
+
+
+def test_device_witness_equals_host_witness_levels_1_and_2(reference_leaves):
+    """The recursive verifier's generators on the device (Poseidon with swap,
+    arithmetic, BaseSum, wire split, extension division, RandomAccess): proof
+    bytes equal the host-witness path's at level 1 (the reference's own leaf
+    proofs, in three chunk orders) and level 2 (inner = the aggregation
+    circuit), and verify."""
+    import qp_wormhole
+    cb, vo, leaves = reference_leaves
+    circ = qp_wormhole.Circuit.aggregation(cb, 2)
+    assert circ.witness_levels > 0 and circ.num_generators > 100000
+    chunks = [leaves, leaves[::-1], [leaves[0], leaves[0]]]
+    dev, host, vd = _device_vs_host(circ, vo, chunks)
+    assert dev == host
+    assert all(verify(vd, d) == 0 for d in dev)
+    l1 = qp_wormhole.aggregate_chunk(leaves, cb, vo)
+    cd = l1.circuit_data
+    c2 = qp_wormhole.Circuit.aggregation(cd.common, 2)
+    dev2, host2, vd2 = _device_vs_host(c2, cd.verifier_only, [[l1.proof.to_bytes()] * 2])
+    assert dev2 == host2 and verify(vd2, dev2[0]) == 0
+
+
+def test_device_witness_zk_aggregation(reference_leaves):
+    """Under the zk config the PublicInputGate row's cells are explicit inputs
+    (device == host for the same values) or, when not given, OS randomness
+    (two runs differ, both verify)."""
+    import qp_wormhole
+    cb, vo, leaves = reference_leaves
+    zcb = bytearray(cb)
+    zcb[49] = 1  # config.zero_knowledge
+    circ = qp_wormhole.Circuit.aggregation(bytes(zcb), 2)
+    r = [[(0x9E3779B97F4A7C15 * (k + 1) + i) % 0xFFFFFFFF00000001 for i in range(circ.num_wires - 4)]
+         for k in range(2)]
+    dev, host, vd = _device_vs_host(circ, vo, [leaves, leaves[::-1]], zk=r)
+    assert dev == host and all(verify(vd, d) == 0 for d in dev)
+    p = qp_wormhole.Prover(qp_wormhole.Context(0), circ, max_batch=1)
+    a, = p.prove_aggregation(vo, [leaves])
+    b, = p.prove_aggregation(vo, [leaves])
+    assert a != b and verify(vd, a) == 0 and verify(vd, b) == 0
+    p.free()

@@ -59,20 +59,27 @@ def test_new_from_bytes_takes_an_upstream_prover_bin(bins):
     digest (the reference's generate_circuit_binaries output) loads, proves and
     verifies; one with another digest is refused."""
     import struct
+    import numpy as np
+    import qp_wormhole
     from qp_wormhole import WormholeProver
+    from upstream_prover_bin import upstream_prover_bin
     common = open(bins / "common.bin", "rb").read()
     vo = open(bins / "verifier.bin", "rb").read()
     dig = struct.unpack_from("<4Q", vo, len(vo) - 32)
-    up = struct.pack("<Q", 1500) + b"\x11" * 4096 + struct.pack("<4Q", *dig) + bytes(16)
+    circ = qp_wormhole.Circuit.wormhole()
+    up = upstream_prover_bin(circ, np.frombuffer(vo, np.uint64, 64, 8), dig)
     wp = WormholeProver.new_from_bytes(up, common)
     proof = wp.commit(WI.test_inputs()).prove()
     vd = vo + common
     from oracle_lib import lib as olib
     pb = proof.to_bytes()
     assert olib().ora_verify(vd, len(vd), pb, len(pb)) == 0
-    bad = struct.pack("<Q", 1500) + b"\x11" * 4096 + struct.pack("<4Q", dig[0] ^ 1, *dig[1:]) + bytes(16)
+    bad = upstream_prover_bin(circ, np.frombuffer(vo, np.uint64, 64, 8), [dig[0] ^ 1] + list(dig[1:]))
     with pytest.raises(ValueError, match="commitment differs"):
         WormholeProver.new_from_bytes(bad, common)
+    foreign = struct.pack("<Q", 1500) + b"\x11" * 40000 + struct.pack("<4Q", *dig) + bytes(16)
+    with pytest.raises(ValueError, match="not found"):
+        WormholeProver.new_from_bytes(foreign, common)
 
 
 def test_zk_binaries_and_default(bins, tmp_path, monkeypatch):

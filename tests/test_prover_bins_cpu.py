@@ -6,6 +6,7 @@ for anything else or a header that disagrees with the common data
 import hashlib
 import struct
 
+import numpy as np
 import pytest
 
 from qp_wormhole import prover as P
@@ -31,28 +32,83 @@ def test_unrecognised_prover_bin_is_rejected_clearly():
         P._parse_prover_only(b"\x05\x00\x00\x00" + b"\x11" * 200, nz)
 
 
-def _upstream_shaped(digest, ngen=1500, body=4096):
-    """generators.len() || (opaque body) || circuit digest || 0u64 || 0u64 -- the
-    frame of ProverOnlyCircuitData::to_bytes for a lookup-free circuit."""
-    return struct.pack("<Q", ngen) + b"\x11" * body + struct.pack("<4Q", *digest) + bytes(16)
-
-
-def test_upstream_prover_bin_recognised_by_the_reference_circuit_digest():
-    """The reference's circuit digest (reconstructed from its own proofs) is the
-    native circuit's, so an upstream prover.bin of the Wormhole circuit matches."""
+def _reference_vd():
     from current_circuit_vd import current_circuit_verifier_data
     from test_oracle_golden import current_common_bytes
-    nz = P._common_of("standard_recursion_config")
     vd, cap, dig = current_circuit_verifier_data(current_common_bytes())
-    vo = vd[:len(vd) - len(current_common_bytes())]
-    parsed = P._parse_prover_only(_upstream_shaped([int(x) for x in dig]), nz)
-    assert parsed[:2] == (None, None)
-    assert P._same_preprocessing(vo, parsed[2])
-    other = [int(dig[0]) ^ 1] + [int(x) for x in dig[1:]]
-    assert not P._same_preprocessing(vo, P._parse_prover_only(_upstream_shaped(other), nz)[2])
-    # a file with lookup tables (non-empty tail) or no generators is not taken for one
-    assert P.upstream_prover_digest(_upstream_shaped(dig)[:-8] + struct.pack("<Q", 1)) is None
-    assert P.upstream_prover_digest(_upstream_shaped(dig, ngen=0)) is None
+    return vd[:len(vd) - len(current_common_bytes())], [int(x) for x in dig]
+
+
+@pytest.fixture(scope="module")
+def circ():
+    import qp_wormhole
+    return qp_wormhole.Circuit.wormhole()
+
+
+def test_host_coefficients_are_the_constants_sigmas_polynomials(circ):
+    """qp_circuit_constants_sigmas_coeffs (host ifft) interpolates the columns:
+    evaluated at w_n^i (Horner) they give back the values."""
+    Pm = 0xFFFFFFFF00000001
+    co, vals = circ.constants_sigmas_coeffs(), circ.constants_sigmas()
+    w = pow(7277203076849721926, 1 << (32 - circ.degree_bits), Pm)
+    for col in (0, 3, 4, 50, 83):
+        for i in (0, 1, 777, circ.n - 1):
+            x, acc = pow(w, i, Pm), 0
+            for c in reversed([int(v) for v in co[col]]):
+                acc = (acc * x + c) % Pm
+            assert acc == int(vals[col][i])
+
+
+def test_upstream_prover_bin_walked_against_the_circuit(circ):
+    """A file framed as upstream ProverOnlyCircuitData::to_bytes carrying this
+    circuit's preprocessing (the reference's cap and digest, reconstructed from
+    its own proofs; the native circuit's columns) is accepted, with either
+    length-prefix gap; its digest is the reference's."""
+    from upstream_prover_bin import upstream_prover_bin
+    nz = P._common_of("standard_recursion_config")
+    vo, dig = _reference_vd()
+    cap = np.frombuffer(vo, np.uint64, 64, 8)
+    for gap in (0, 8):
+        data = upstream_prover_bin(circ, cap, dig, gap=gap)
+        parsed = P._parse_prover_only(data, nz, circ, vo)
+        assert parsed[:2] == (None, None) and P._same_preprocessing(vo, parsed[2])
+    other = [dig[0] ^ 1] + dig[1:]
+    assert not P._same_preprocessing(vo, P._parse_prover_only(upstream_prover_bin(circ, cap, other), nz, circ, vo)[2])
+
+
+def test_truncated_or_foreign_upstream_blobs_are_rejected(circ):
+    """The old tail check accepted anything ending in digest || 0 || 0; the walk
+    refuses truncations (at every section), a flipped coefficient or sigma, a
+    different cap, and a foreign blob with the right tail."""
+    from upstream_prover_bin import upstream_prover_bin
+    nz = P._common_of("standard_recursion_config")
+    vo, dig = _reference_vd()
+    cap = np.frombuffer(vo, np.uint64, 64, 8)
+    good = upstream_prover_bin(circ, cap, dig)
+    tail = good[-48:]
+    foreign = struct.pack("<Q", 1500) + b"\x11" * 40000 + tail
+    assert P.upstream_prover_digest(foreign) is not None  # what the tail check used to accept
+    with pytest.raises(ValueError, match="coefficients of this circuit not found"):
+        P._parse_prover_only(foreign, nz, circ, vo)
+    n = circ.n
+    for cut in (len(good) // 10, len(good) // 3, len(good) // 2, len(good) - 8 * n - 100, len(good) - 60):
+        with pytest.raises(ValueError):
+            P._parse_prover_only(good[:cut] + tail, nz, circ, vo)
+    # one coefficient of column 40, one sigma value, one cap element
+    k = good.find(circ.constants_sigmas_coeffs()[40].tobytes())
+    for pos, what in ((k + 8 * 5, "coefficient column 40"), (good.find(circ.constants_sigmas()[10].tobytes()) + 16,
+                                                             "sigma")):
+        bad = bytearray(good)
+        bad[pos] ^= 1
+        with pytest.raises(ValueError, match=what):
+            P._parse_prover_only(bytes(bad), nz, circ, vo)
+    cap2 = cap.copy()
+    cap2[5] ^= 1
+    with pytest.raises(ValueError, match="Merkle cap"):
+        P._parse_prover_only(good, nz, circ, vo[:8] + cap2.tobytes() + vo[8 + 512:])
+    # without the circuit an upstream file cannot be checked
+    with pytest.raises(ValueError, match="needs the circuit"):
+        P._parse_prover_only(good, nz)
 
 
 def test_header_must_agree_with_common_data():
