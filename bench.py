@@ -84,6 +84,59 @@ def pmc_traffic(kernel, ncols, log_n, proofs, lanes_per_proof=None):
     return None
 
 
+def mix_ceiling(ceil):
+    """k_leaf_hash's issue ceiling (tools/issue_ceiling.py): its instruction mix at
+    the measured per-class costs, re-priced at the kernel's own clock when the
+    profile has it."""
+    if not ceil:
+        return None
+    return ceil.get("ceiling_at_leaf_clock_wave_instr_per_s") or ceil["ceiling_wave_instr_per_s"]
+
+
+def profile_stamp(path):
+    """lib_sha16 a profile summary was stamped with (tools/libhash.py), or None."""
+    d = load_json(path)
+    if isinstance(d, list):
+        d = d[0] if d else None
+    return d.get("lib_sha16") if isinstance(d, dict) else None
+
+
+def segregate_profile_fields(rec):
+    """Fields read from committed profile summaries (PMC traffic, instructions per
+    permutation, mix ceiling, kernel-time share, GPU busy fraction) stay in place
+    only when the summary was stamped with the hash of the library this run
+    loaded; otherwise they move under rec["from_profile"] with their source and
+    stamp, and the in-place value becomes None."""
+    sys.path.insert(0, os.path.join(ROOT, "tools"))
+    from libhash import lib_sha16
+    from qp_wormhole._native import LIB_PATH
+    mine = lib_sha16(LIB_PATH)
+    moved = {}
+
+    def check(path, owner, keys, label):
+        if owner is None:
+            return
+        st = profile_stamp(path)
+        if st == mine:
+            return
+        for k in keys:
+            if owner.get(k) is not None:
+                moved[f"{label}.{k}"] = {"value": owner[k], "source": os.path.relpath(path, ROOT), "lib_sha16": st}
+                owner[k] = None
+    check(PMC_FILE, rec.get("roofline"), ["traffic"], "roofline")
+    check(PMC_FILE, rec.get("valu_kernels"), ["quotient_hbm_bytes_per_launch"], "valu_kernels")
+    dk = rec.get("dominant_kernel")
+    check(PMC_SQ_FILE, dk, ["instr_per_perm", "achieved", "frac", "frac_of_mix_ceiling"], "dominant_kernel")
+    check(CEIL_FILE, dk, ["mix_ceiling", "frac_of_mix_ceiling"], "dominant_kernel")
+    check(KSUM1_FILE, dk, ["share_of_kernel_time"], "dominant_kernel")
+    check(KSUM_FILE, rec.get("gpu_busy_frac"), ["value"], "gpu_busy_frac")
+    rec["profile_build"] = {"lib_sha16": mine, "all_profiles_of_this_build": not moved}
+    if moved:
+        moved["note"] = ("read from profile summaries of another build (their lib_sha16 differs from the loaded "
+                         "library's): not this build's measurement")
+        rec["from_profile"] = moved
+
+
 def parse():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -142,10 +195,23 @@ def make_witnesses(circuit, inputs):
     return wires, pis
 
 
-def cpu_baseline(circuit, wires, pis, sample, min_seconds):
-    """oracle/prover.c (C + OpenMP restatement of plonky2 prove): at least
-    `sample` proofs of the bench's own witnesses, continuing (cycling through
-    them) until `min_seconds` of CPU proving have been timed."""
+def cpu_model():
+    try:
+        for line in open("/proc/cpuinfo"):
+            if line.startswith("model name"):
+                return line.split(":", 1)[1].strip()
+    except OSError:
+        pass
+    return None
+
+
+def cpu_baseline(circuit, inputs, sample, min_seconds):
+    """The GPU line's work on the host cores, proof by proof: commit() + witness
+    generation (this library's host generator, circuit.commit: the C++
+    restatement of generate_partial_witness) and prove() (oracle/prover.c, the
+    C + OpenMP restatement of plonky2's prover), for at least `sample` of the
+    bench's own CircuitInputs, continuing (cycling through them) until
+    `min_seconds` have been timed."""
     from oracle_lib import U64P, lib as olib
     L = olib()
     L.ora_prove.argtypes = [ctypes.c_char_p, ctypes.c_size_t, U64P, U64P, U64P, ctypes.c_size_t, ctypes.c_char_p,
@@ -158,19 +224,25 @@ def cpu_baseline(circuit, wires, pis, sample, min_seconds):
     dig = np.zeros(4, np.uint64)
     t = time.perf_counter()
     done = 0
+    t_wit = 0.0
     while done < sample or time.perf_counter() - t < min_seconds:
-        i = done % wires.shape[0]
-        rc = L.ora_prove(cb, len(cb), cs, np.ascontiguousarray(wires[i]), np.ascontiguousarray(pis[i]),
-                         pis.shape[1], out, 400000, ctypes.byref(ln), cap, dig)
+        t0 = time.perf_counter()
+        w = circuit.commit(inputs[done % len(inputs)])
+        wires, pis = w.wires(), w.public_inputs()
+        w.free()
+        t_wit += time.perf_counter() - t0
+        rc = L.ora_prove(cb, len(cb), cs, wires, pis, len(pis), out, 400000, ctypes.byref(ln), cap, dig)
         assert rc == 0
         done += 1
     dt = time.perf_counter() - t
-    sample = done
     cores = int(os.environ.get("OMP_NUM_THREADS", os.cpu_count() or 1))
-    return {"value": sample / dt, "unit": "proofs/s", "cores": cores, "kind": "port",
-            "sample": f"{sample} {circuit.kind} proofs (deg {circuit.degree_bits}, standard_recursion_config), "
-                      f"C+OpenMP restatement "
-                      f"oracle/prover.c, {dt:.1f} s"}
+    return {"value": done / dt, "unit": "proofs/s", "cores": cores, "kind": "port",
+            "sample": f"{done} {circuit.kind} proofs (deg {circuit.degree_bits}, standard_recursion_config) from the "
+                      f"bench's CircuitInputs, {dt:.1f} s: commit + witness generation {t_wit:.2f} s (host C++, one "
+                      f"thread), prove {dt - t_wit:.1f} s (oracle/prover.c, C + OpenMP)",
+            "host": {"nproc": os.cpu_count(), "cpu_model": cpu_model(), "omp_threads": cores},
+            "note": "the GPU line's work (commit, witness generation, prove) on the host cores; a C restatement "
+                    "of plonky2, not the Rust reference (no cargo here): quote no GPU/CPU ratio"}
 
 
 def reference_parity(qp_wormhole, device):
@@ -251,14 +323,19 @@ def configs3(args, circuit, prover, provers, cin, per, NP, B, dist, world, rank,
     if rank != 0:
         return None
     from oracle_lib import lib as olib
-    rvd, rp = root.circuit_data.verifier_data(), root.proof.to_bytes()
+    from qp_wormhole.prover import _common_degree_bits
+    tops = root if isinstance(root, list) else [root]
+    ok = all(olib().ora_verify(t.circuit_data.verifier_data(), len(t.circuit_data.verifier_data()),
+                               t.proof.to_bytes(), len(t.proof.to_bytes())) == 0 for t in tops)
     leaves = world * ns
     return {"workload": f"{leaves}_leaves_as_{world}x{ns}_per_gpu_subtrees_branching2",
-            "value": leaves / dt, "unit": "leaf proofs/s (proved and aggregated into one root)",
-            "seconds": dt, "leaves": leaves, "aggregation_proofs": leaves - 1,
+            "value": leaves / dt, "unit": "leaf proofs/s (proved and aggregated into one root)"
+            if len(tops) == 1 else f"leaf proofs/s (proved and aggregated into {len(tops)} top proofs)",
+            "seconds": dt, "leaves": leaves, "aggregation_proofs": leaves - len(tops),
             "stages_rank0_s": tm,
-            "root_verified": olib().ora_verify(rvd, len(rvd), rp, len(rp)) == 0,
-            "root_public_inputs": len(root.proof.public_inputs),
+            "root_verified" if len(tops) == 1 else "top_proofs_verified": ok,
+            "top_circuit_degree_bits": _common_degree_bits(tops[0].circuit_data.common),
+            "root_public_inputs": sum(len(t.proof.public_inputs) for t in tops),
             "note": "one timed pass after an untimed one that builds the level circuits; leaves e2e from "
                     "CircuitInputs, per-GPU subtree (device witness generation, batched levels), roots gathered "
                     "over RCCL (world > 1), top levels on rank 0; root verified by the oracle verifier after the "
@@ -374,7 +451,7 @@ def main():
         lat = sorted(ts)[1]
     # recursive aggregation of this run's leaf proofs (BASELINE
     # configs[3]'s consumer; wormhole/aggregator/src/circuits/tree.rs): one level of
-    # `agg_leaves` leaves (agg_leaves/2 aggregation proofs, degree 2^14, batched) and a
+    # `agg_leaves` leaves (agg_leaves/2 aggregation proofs, degree 2^13, batched) and a
     # default tree (8 leaves, branching 2, depth 3) end to end; after the timed region
     agg = None
     if rank == 0 and not voting and args.agg_leaves and proofs is not None:
@@ -401,7 +478,8 @@ def main():
                "tree8_root_ms": tree_ms, "root_verified": olib().ora_verify(rvd, len(rvd), rp, len(rp)) == 0,
                "aggregation_circuit_degree_bits": _common_degree_bits(root.circuit_data.common),
                "proof_bytes": len(rp),
-               "note": "aggregate_chunk circuits (native recursive verifier of 2 proofs, degree 2^14), device "
+               "note": "aggregate_chunk circuits (recursive verifier of 2 proofs on upstream's gate set, degree "
+                       "2^13 at level 1), device "
                        "witness generation + batched GPU prove; one level = nl/2 chunks; tree = 4+2+1 proofs"}
     # BASELINE configs[3] as one measured pipeline (every rank, after the headline):
     # leaves -> per-GPU subtree root -> RCCL gather of the roots -> tree root on rank 0
@@ -517,8 +595,11 @@ def main():
                 "share_of_kernel_time": ksum1["leaf_hash_share"] if ksum1 else None,
                 "achieved": ach, "peak": VALU_PEAK_WAVE_INSTR_S, "unit": "wave-instructions/s",
                 "frac": ach / VALU_PEAK_WAVE_INSTR_S, "instr_per_perm": ipp,
-                "mix_ceiling": ceil["ceiling_wave_instr_per_s"] if ceil else None,
-                "frac_of_mix_ceiling": ach / ceil["ceiling_wave_instr_per_s"] if ceil else None,
+                "mix_ceiling": mix_ceiling(ceil),
+                "mix_ceiling_priced_at": ("the leaf hash's own clock (GRBM_GUI_ACTIVE per dispatch)"
+                                          if ceil and ceil.get("ceiling_at_leaf_clock_wave_instr_per_s")
+                                          else "the calibration kernels' clocks") if ceil else None,
+                "frac_of_mix_ceiling": ach / mix_ceiling(ceil) if ceil else None,
                 "sources": {"instr_per_perm": os.path.relpath(PMC_SQ_FILE, ROOT),
                             "mix_ceiling": os.path.relpath(CEIL_FILE, ROOT) if ceil else None,
                             "share": os.path.relpath(KSUM1_FILE, ROOT) if ksum1 else None,
@@ -533,10 +614,9 @@ def main():
                                     "note": "union of kernel intervals / window, rocprofv3 kernel trace of this bench "
                                             "(3 provers), cut to the timed steps by the trace markers"}
         rec["stage_ms_per_step"]["note"] = f"prover 0 ({per[0]} proofs), host + device"
+        segregate_profile_fields(rec)
         if world == 1 and args.cpu_sample > 0:
-            rec["cpu_baseline"] = cpu_baseline(circuit, wires, pis, args.cpu_sample, args.cpu_seconds)
-            rec["cpu_baseline"]["note"] = ("times prove() from host-generated witnesses; commit + witness "
-                                           "generation are not included on the CPU side")
+            rec["cpu_baseline"] = cpu_baseline(circuit, inputs, args.cpu_sample, args.cpu_seconds)
         print(json.dumps(rec), flush=True)
     for p in provers:
         p.free()

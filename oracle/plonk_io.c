@@ -65,7 +65,14 @@ static void rd_gate(rd_t *r, or_gate_t *g) {
         g->p0 = rd_u64(r); break;
     case G_NOOP: case G_POSEIDON: case G_PUBLIC_INPUT: case G_POSEIDON_MDS: break;
     case G_RANDOM_ACCESS: g->p0 = rd_u64(r); g->p1 = rd_u64(r); g->p2 = rd_u64(r); break;
-    default: r->err = 4; break; /* CosetInterpolation/Lookup: not in the leaf circuits */
+    case G_COSET_INTERP: { /* subgroup_bits, degree, barycentric_weights (field vec; recomputed) */
+        g->p0 = rd_u64(r); g->p1 = rd_u64(r);
+        uint64_t nw = rd_u64(r);
+        if (g->p0 > 6 || nw != ((uint64_t)1 << g->p0) || g->p1 < 2) { r->err = 4; break; }
+        for (uint64_t i = 0; i < nw; i++) rd_u64(r);
+        break;
+    }
+    default: r->err = 4; break; /* Lookup gates: not supported */
     }
 }
 static void wr_gate(wr_t *w, const or_gate_t *g) {
@@ -74,6 +81,14 @@ static void wr_gate(wr_t *w, const or_gate_t *g) {
     case G_ARITHMETIC: case G_ARITH_EXT: case G_BASE_SUM: case G_CONSTANT: case G_MUL_EXT:
     case G_REDUCING: case G_REDUCING_EXT: case G_EXPONENTIATION: wr_u64(w, g->p0); break;
     case G_RANDOM_ACCESS: wr_u64(w, g->p0); wr_u64(w, g->p1); wr_u64(w, g->p2); break;
+    case G_COSET_INTERP: { /* weights of the subgroup: w^i / n */
+        const uint64_t np = (uint64_t)1 << g->p0;
+        const gl_t om = gl_root_of_unity((unsigned)g->p0), ninv = gl_inv(np);
+        gl_t x = 1;
+        wr_u64(w, g->p0); wr_u64(w, g->p1); wr_u64(w, np);
+        for (uint64_t i = 0; i < np; i++) { wr_u64(w, gl_mul(x, ninv)); x = gl_mul(x, om); }
+        break;
+    }
     default: break;
     }
 }

@@ -30,6 +30,12 @@ static inline int gate_degree(GateKind k) {
     case G_ARITHMETIC: return 3;
     case G_POSEIDON: return 7;
     case G_RANDOM_ACCESS: return RA_BITS + 1;
+    case G_ARITH_EXT: return 3;
+    case G_MUL_EXT: return 3;
+    case G_REDUCING: return 2;
+    case G_REDUCING_EXT: return 2;
+    case G_POSEIDON_MDS: return 1;
+    case G_COSET_INTERP: return CI_DEGREE;
     default: return 0;
   }
 }
@@ -365,14 +371,21 @@ CircuitData CircuitBuilder::build() {
   // gate set in common-data order (degree, id string)
   bool present[G_NKINDS] = {false};
   for (auto &r : rows_) present[r.kind] = true;
-  // CommonCircuitData.gates: sorted by (degree, id)
-  const GateKind order[] = {G_NOOP, G_CONSTANT, G_PUBLIC_INPUT, G_BASE_SUM, G_ARITHMETIC, G_RANDOM_ACCESS, G_POSEIDON};
+  // CommonCircuitData.gates: sorted by (degree, id string) -- e.g. degree 1:
+  // "ConstantGate.." < "PoseidonMdsGate.." < "PublicInputGate"; degree 2:
+  // "BaseSumGate.." < "ReducingExtensionGate.." < "ReducingGate.."; degree 3:
+  // "ArithmeticExtensionGate.." < "ArithmeticGate.." < "MulExtensionGate.."
+  const GateKind order[] = {G_NOOP, G_CONSTANT, G_POSEIDON_MDS, G_PUBLIC_INPUT, G_BASE_SUM, G_REDUCING_EXT,
+                            G_REDUCING, G_ARITH_EXT, G_ARITHMETIC, G_MUL_EXT, G_RANDOM_ACCESS, G_COSET_INTERP,
+                            G_POSEIDON};
   for (GateKind k : order)
     if (present[k]) {
       cd.gate_kinds.push_back(k);
       cd.gate_params.push_back(k == G_CONSTANT ? ncg : k == G_BASE_SUM ? base_sum_limbs_ : k == G_ARITHMETIC ? arith_ops_
-                               : k == G_RANDOM_ACCESS ? RA_BITS : 0);
-      cd.gate_params2.push_back(k == G_RANDOM_ACCESS ? RA_COPIES : 0);
+                               : k == G_RANDOM_ACCESS ? RA_BITS : k == G_ARITH_EXT ? AE_OPS : k == G_MUL_EXT ? ME_OPS
+                               : k == G_REDUCING ? RED_COEFFS : k == G_REDUCING_EXT ? REDE_COEFFS
+                               : k == G_COSET_INTERP ? CI_BITS : 0);
+      cd.gate_params2.push_back(k == G_RANDOM_ACCESS ? RA_COPIES : k == G_COSET_INTERP ? CI_DEGREE : 0);
       cd.gate_params3.push_back(k == G_RANDOM_ACCESS ? RA_EXTRA : 0);
     }
   const uint32_t num_gates = (uint32_t)cd.gate_kinds.size();
@@ -401,7 +414,8 @@ CircuitData CircuitBuilder::build() {
   uint32_t max_gate_consts = 0;
   for (GateKind k : cd.gate_kinds)
     max_gate_consts = std::max<uint32_t>(max_gate_consts, k == G_CONSTANT ? ncg : k == G_ARITHMETIC ? 2
-                                                          : k == G_RANDOM_ACCESS ? RA_EXTRA : 0);
+                                                          : k == G_RANDOM_ACCESS ? RA_EXTRA : k == G_ARITH_EXT ? 2
+                                                          : k == G_MUL_EXT ? 1 : 0);
   cd.num_constants = nsel + max_gate_consts;
   // constraint count = max over gates
   cd.num_gate_constraints = 0;
@@ -409,7 +423,10 @@ CircuitData CircuitBuilder::build() {
     GateKind k = cd.gate_kinds[i];
     uint32_t c = k == G_CONSTANT ? ncg : k == G_PUBLIC_INPUT ? 4 : k == G_BASE_SUM ? base_sum_limbs_ + 1
                : k == G_ARITHMETIC ? arith_ops_ : k == G_POSEIDON ? 123
-               : k == G_RANDOM_ACCESS ? RA_COPIES * (RA_BITS + 2) + RA_EXTRA : 0;
+               : k == G_RANDOM_ACCESS ? RA_COPIES * (RA_BITS + 2) + RA_EXTRA
+               : k == G_ARITH_EXT ? 2 * AE_OPS : k == G_MUL_EXT ? 2 * ME_OPS : k == G_REDUCING ? 2 * RED_COEFFS
+               : k == G_REDUCING_EXT ? 2 * REDE_COEFFS : k == G_POSEIDON_MDS ? 24
+               : k == G_COSET_INTERP ? 4 + 4 * CI_NINT : 0;
     cd.num_gate_constraints = std::max(cd.num_gate_constraints, c);
   }
   // num_partial_products: routed wires in chunks of qdf, minus one
@@ -513,6 +530,13 @@ CircuitData CircuitBuilder::build() {
           gout[gi].push_back(wpt(g.row, ra_wire_claimed(g.op)));
           for (uint32_t i = 0; i < RA_BITS; i++) gout[gi].push_back(wpt(g.row, ra_wire_bit(i, g.op)));
           break;
+        default: {
+          std::vector<std::pair<uint32_t, uint32_t>> rd, wr;
+          gen_row_wires(g.kind, g.row, g.op, rd, wr);
+          for (auto &rc : rd) gin[gi].push_back(wpt(rc.first, rc.second));
+          for (auto &rc : wr) gout[gi].push_back(wpt(rc.first, rc.second));
+          break;
+        }
       }
       std::sort(gin[gi].begin(), gin[gi].end());
       gin[gi].erase(std::unique(gin[gi].begin(), gin[gi].end()), gin[gi].end());
@@ -614,6 +638,11 @@ CircuitData CircuitBuilder::build() {
           g.s[4] = sid[pt(g.e)];
           g.s[5] = sid[pt(g.f)];
           break;
+        case GEN_ARITH_EXT:
+        case GEN_MUL_EXT:
+          g.k0 = rows_[g.row].c0;
+          g.k1 = rows_[g.row].c1;
+          break;
         default:
           break;
       }
@@ -670,6 +699,13 @@ CircuitData CircuitBuilder::build() {
             wr.push_back(cd.wire_slot[(size_t)g.row * W + ra_wire_claimed(g.op)]);
             for (uint32_t i = 0; i < RA_BITS; i++) wr.push_back(cd.wire_slot[(size_t)g.row * W + ra_wire_bit(i, g.op)]);
             break;
+          default: {
+            std::vector<std::pair<uint32_t, uint32_t>> rw, ww;
+            gen_row_wires(g.kind, g.row, g.op, rw, ww);
+            for (auto &rc : rw) rd.push_back(cd.wire_slot[(size_t)rc.first * W + rc.second]);
+            for (auto &rc : ww) wr.push_back(cd.wire_slot[(size_t)rc.first * W + rc.second]);
+            break;
+          }
         }
         uint32_t l = 0;
         for (uint32_t s : rd) {
@@ -698,8 +734,8 @@ CircuitData CircuitBuilder::build() {
           d.s[1] = g.op;  // number of BaseSum gates from `row`
         } else if (g.kind == GEN_EXT_DIV) {
           d.k0 = g.s[4] | (uint64_t)g.s[5] << 32;  // quotient slots
-        } else if (g.kind == GEN_RANDOM_ACCESS) {
-          d.s[0] = g.op;  // copy
+        } else if (g.kind == GEN_RANDOM_ACCESS || g.kind == GEN_ARITH_EXT || g.kind == GEN_MUL_EXT) {
+          d.s[0] = g.op;  // copy / op
         }
       }
     }
@@ -780,7 +816,17 @@ std::vector<uint8_t> CircuitData::common_bytes() const {
   for (size_t i = 0; i < gate_kinds.size(); i++) {
     w.u32(gate_serial_id(gate_kinds[i]));
     GateKind k = gate_kinds[i];
-    if (k == G_CONSTANT || k == G_BASE_SUM || k == G_ARITHMETIC) w.u64(gate_params[i]);
+    if (k == G_CONSTANT || k == G_BASE_SUM || k == G_ARITHMETIC || k == G_ARITH_EXT || k == G_MUL_EXT ||
+        k == G_REDUCING || k == G_REDUCING_EXT)
+      w.u64(gate_params[i]);
+    if (k == G_COSET_INTERP) {  // CosetInterpolationGate { subgroup_bits, degree, barycentric_weights }
+      w.u64(gate_params[i]);
+      w.u64(gate_params2[i]);
+      const uint32_t np = 1u << gate_params[i];
+      const F om = gl::root_of_unity(gate_params[i]), ninv = gl::inv(np);
+      w.u64(np);
+      for (uint32_t j = 0, x = 0; j < np; j++, (void)x) w.u64(gl::mul(gl::pow(om, j), ninv));  // 1 / prod_{l != j}(w^j - w^l) = w^j / n
+    }
     if (k == G_RANDOM_ACCESS) {  // RandomAccessGate { bits, num_copies, num_extra_constants }
       w.u64(gate_params[i]);
       w.u64(gate_params2[i]);
@@ -950,6 +996,78 @@ bool Witness::generate(std::string &err) {
         }
         ok = set_wire(g.row, ra_wire_claimed(g.op), wire(g.row, ra_wire_item((uint32_t)idx, g.op)));
         for (uint32_t i = 0; i < RA_BITS && ok; i++) ok = set_wire(g.row, ra_wire_bit(i, g.op), (idx >> i) & 1);
+        break;
+      }
+      case GEN_ARITH_EXT:
+      case GEN_MUL_EXT: {
+        // ArithmeticExtensionGenerator / MulExtensionGenerator: c0 m0 m1 (+ c1 addend)
+        const bool ae = g.kind == GEN_ARITH_EXT;
+        const uint32_t o = ae ? 8 * g.op : 6 * g.op;
+        gl::ext r = gl::ext_scale(gl::ext_mul(gl::ext{wire(g.row, o), wire(g.row, o + 1)},
+                                              gl::ext{wire(g.row, o + 2), wire(g.row, o + 3)}), g.k0);
+        if (ae) r = gl::ext_add(r, gl::ext_scale(gl::ext{wire(g.row, o + 4), wire(g.row, o + 5)}, g.k1));
+        const uint32_t oo = ae ? o + 6 : o + 4;
+        ok = set_wire(g.row, oo, r.c0) && set_wire(g.row, oo + 1, r.c1);
+        break;
+      }
+      case GEN_REDUCING:
+      case GEN_REDUCING_EXT: {
+        // ReducingGenerator: acc <- acc * alpha + coeff_i, every accumulator written
+        const bool base = g.kind == GEN_REDUCING;
+        const uint32_t nc = base ? RED_COEFFS : REDE_COEFFS, cw = base ? 1 : 2;
+        const gl::ext alpha{wire(g.row, 2), wire(g.row, 3)};
+        gl::ext acc{wire(g.row, 4), wire(g.row, 5)};
+        for (uint32_t i = 0; i < nc && ok; i++) {
+          const gl::ext c{wire(g.row, 6 + cw * i), base ? 0 : wire(g.row, 7 + 2 * i)};
+          acc = gl::ext_add(gl::ext_mul(acc, alpha), c);
+          const uint32_t aw = i + 1 == nc ? 0 : 6 + cw * nc + 2 * i;
+          ok = set_wire(g.row, aw, acc.c0) && set_wire(g.row, aw + 1, acc.c1);
+        }
+        break;
+      }
+      case GEN_POSEIDON_MDS: {
+        // PoseidonMdsGenerator: the MDS layer of each component
+        F a[12], b[12];
+        for (int i = 0; i < 12; i++) {
+          a[i] = wire(g.row, 2 * i);
+          b[i] = wire(g.row, 2 * i + 1);
+        }
+        mds_h(a);
+        mds_h(b);
+        for (int i = 0; i < 12 && ok; i++) ok = set_wire(g.row, 24 + 2 * i, a[i]) && set_wire(g.row, 25 + 2 * i, b[i]);
+        break;
+      }
+      case GEN_COSET_INTERP: {
+        // InterpolationGenerator (gates/coset_interpolation.rs): shifted point,
+        // partial barycentric sums over chunks of the subgroup, the value
+        const F shift = wire(g.row, 0);
+        if (!shift) {
+          err = "coset interpolation with a zero shift";
+          return false;
+        }
+        const gl::ext pt = gl::ext_scale(gl::ext{wire(g.row, CI_EVAL_POINT), wire(g.row, CI_EVAL_POINT + 1)},
+                                         gl::inv(shift));
+        ok = set_wire(g.row, CI_SHIFTED, pt.c0) && set_wire(g.row, CI_SHIFTED + 1, pt.c1);
+        const F om = gl::root_of_unity(CI_BITS), ninv = gl::inv(CI_POINTS);
+        gl::ext ev{0, 0}, pr{1, 0};
+        uint32_t lo = 0, hi = CI_DEGREE;
+        for (uint32_t it = 0; ok; it++) {
+          for (uint32_t i = lo; i < hi; i++) {
+            const F x = gl::pow(om, i);
+            const gl::ext term = gl::ext_sub(pt, gl::ext{x, 0});
+            const gl::ext v = gl::ext_scale(gl::ext{wire(g.row, CI_VALUES + 2 * i), wire(g.row, CI_VALUES + 2 * i + 1)},
+                                            gl::mul(x, ninv));
+            ev = gl::ext_add(gl::ext_mul(ev, term), gl::ext_mul(v, pr));
+            pr = gl::ext_mul(pr, term);
+          }
+          if (it == CI_NINT) break;
+          ok = set_wire(g.row, CI_INTER + 2 * it, ev.c0) && set_wire(g.row, CI_INTER + 2 * it + 1, ev.c1) &&
+               set_wire(g.row, CI_INTER + 2 * (CI_NINT + it), pr.c0) &&
+               set_wire(g.row, CI_INTER + 2 * (CI_NINT + it) + 1, pr.c1);
+          lo = 1 + (CI_DEGREE - 1) * (it + 1);
+          hi = std::min(lo + CI_DEGREE - 1, CI_POINTS);
+        }
+        if (ok) ok = set_wire(g.row, CI_EVAL_VALUE, ev.c0) && set_wire(g.row, CI_EVAL_VALUE + 1, ev.c1);
         break;
       }
       case GEN_POSEIDON: {

@@ -38,9 +38,34 @@ struct Target {
 
 enum GateKind : uint8_t {
   G_NOOP = 0, G_CONSTANT, G_PUBLIC_INPUT, G_BASE_SUM, G_ARITHMETIC, G_POSEIDON,
-  G_RANDOM_ACCESS,  // RandomAccessGate{bits 4, copies 4, extra constants 2} (the recursive verifier's)
+  // the recursive verifier's gates (plonky2 verify_proof; aggregation circuits)
+  G_RANDOM_ACCESS,   // RandomAccessGate{bits 4, copies 4, extra constants 2}
+  G_ARITH_EXT,       // ArithmeticExtensionGate{num_ops 10}: out = c0 m0 m1 + c1 addend (ext)
+  G_MUL_EXT,         // MulExtensionGate{num_ops 13}: out = c0 m0 m1 (ext)
+  G_REDUCING,        // ReducingGate{num_coeffs 43}: Horner of base coefficients by an ext alpha
+  G_REDUCING_EXT,    // ReducingExtensionGate{num_coeffs 32}: the same over ext coefficients
+  G_POSEIDON_MDS,    // PoseidonMdsGate: the 12x12 MDS layer on ext values
+  G_COSET_INTERP,    // CosetInterpolationGate{subgroup_bits 4, degree 6}
   G_NKINDS
 };
+
+// extension-field target (a, b) = a + b X, X^2 = 7 (plonky2 ExtensionTarget<2>)
+struct ExtT {
+  Target c0, c1;
+  bool operator==(const ExtT &o) const { return c0 == o.c0 && c1 == o.c1; }
+};
+
+// new_from_config shapes of the standard config (80 routed of 135 wires, D = 2)
+constexpr uint32_t AE_OPS = 10;       // ArithmeticExtensionGate: routed / (4 D)
+constexpr uint32_t ME_OPS = 13;       // MulExtensionGate: routed / (3 D)
+constexpr uint32_t RED_COEFFS = 43;   // ReducingGate::max_coeffs_len: min(routed - 3D, (wires - 2D) / (D + 1))
+constexpr uint32_t REDE_COEFFS = 32;  // ReducingExtensionGate::max_coeffs_len: min((routed - 3D) / D, (wires - 2D) / 2D)
+// CosetInterpolationGate::with_max_degree(4, 8): degree (14 / 3) + 2 = 6, 2 intermediates;
+// wires: shift 0, values 1.., evaluation point, evaluation value, intermediate
+// evals, intermediate products, shifted evaluation point
+constexpr uint32_t CI_BITS = 4, CI_POINTS = 16, CI_DEGREE = 6, CI_NINT = (CI_POINTS - 2) / (CI_DEGREE - 1);
+constexpr uint32_t CI_VALUES = 1, CI_EVAL_POINT = CI_VALUES + 2 * CI_POINTS, CI_EVAL_VALUE = CI_EVAL_POINT + 2,
+                   CI_INTER = CI_EVAL_VALUE + 2, CI_SHIFTED = CI_INTER + 4 * CI_NINT;
 
 // RandomAccessGate::new_from_config(standard config, bits = 4) (gates/random_access.rs):
 // per copy c: access index at 18c, claimed element at 18c + 1, list items at
@@ -61,6 +86,12 @@ inline uint32_t gate_serial_id(GateKind k) {
     case G_ARITHMETIC: return 0;
     case G_POSEIDON: return 11;
     case G_RANDOM_ACCESS: return 13;
+    case G_ARITH_EXT: return 1;
+    case G_MUL_EXT: return 8;
+    case G_REDUCING: return 15;
+    case G_REDUCING_EXT: return 14;
+    case G_POSEIDON_MDS: return 10;
+    case G_COSET_INTERP: return 4;
     default: return 0xFFFFFFFF;
   }
 }
@@ -94,7 +125,16 @@ enum GenKind : uint8_t {
   GEN_WIRE_SPLIT,     // WireSplitGenerator: integer -> the sums of `op` consecutive BaseSum gates from `row`
   GEN_EXT_DIV,        // QuotientGeneratorExtension: (e, f) = (a + bX) / (c + dX)
   GEN_RANDOM_ACCESS,  // RandomAccessGenerator of copy `op` of the RandomAccessGate at `row`
+  GEN_ARITH_EXT,      // ArithmeticExtensionGenerator of op `op` at `row` (constants k0, k1)
+  GEN_MUL_EXT,        // MulExtensionGenerator of op `op` at `row` (constant k0)
+  GEN_REDUCING,       // ReducingGenerator of the ReducingGate at `row`
+  GEN_REDUCING_EXT,   // ReducingExtensionGenerator of the ReducingExtensionGate at `row`
+  GEN_POSEIDON_MDS,   // PoseidonMdsGenerator of the gate at `row`
+  GEN_COSET_INTERP,   // InterpolationGenerator of the CosetInterpolationGate at `row`
 };
+// (row, column) wires a row generator reads and writes (schedule + device levels)
+void gen_row_wires(GenKind k, uint32_t row, uint32_t op, std::vector<std::pair<uint32_t, uint32_t>> &rd,
+                   std::vector<std::pair<uint32_t, uint32_t>> &wr);
 struct Gen {
   GenKind kind;
   uint32_t row = 0, op = 0;             // gate row / arithmetic op index
@@ -226,6 +266,42 @@ class CircuitBuilder {
   // a generator the gadget layer creates (GEN_EXT_DIV ...); inputs must be targets
   void add_generator(const Gen &g) { gens_.push_back(g); }
 
+  // ---- extension arithmetic on the recursion gates (gadgets/arithmetic_extension.rs)
+  ExtT zero_ext() { return {zero(), zero()}; }
+  ExtT one_ext() { return {one(), zero()}; }
+  ExtT constant_ext(F c0, F c1 = 0) { return {constant(c0), constant(c1)}; }
+  ExtT convert_to_ext(Target t) { return {t, zero()}; }
+  ExtT add_virtual_ext() { return {add_virtual_target(), add_virtual_target()}; }
+  void connect_ext(ExtT a, ExtT b) { connect(a.c0, b.c0); connect(a.c1, b.c1); }
+  // c0 m0 m1 + c1 addend: special cases, operation dedup, then an
+  // ArithmeticExtensionGate op (MulExtensionGate op when the addend is zero)
+  ExtT arithmetic_extension(F c0, F c1, ExtT m0, ExtT m1, ExtT addend);
+  ExtT add_ext(ExtT a, ExtT b) { return arithmetic_extension(1, 1, one_ext(), a, b); }
+  ExtT sub_ext(ExtT a, ExtT b) { return arithmetic_extension(1, gl_neg_one(), one_ext(), a, b); }
+  ExtT mul_ext(ExtT a, ExtT b) { return arithmetic_extension(1, 0, a, b, zero_ext()); }
+  ExtT mul_add_ext(ExtT a, ExtT b, ExtT c) { return arithmetic_extension(1, 1, a, b, c); }
+  ExtT mul_sub_ext(ExtT a, ExtT b, ExtT c) { return arithmetic_extension(1, gl_neg_one(), a, b, c); }
+  ExtT scalar_mul_ext(F c, ExtT x) { return arithmetic_extension(c, 0, one_ext(), x, zero_ext()); }
+  ExtT mul_const_add_ext(F c, ExtT x, ExtT y) { return arithmetic_extension(c, 1, one_ext(), x, y); }
+  ExtT add_const_ext(ExtT x, F c) { return add_ext(x, constant_ext(c)); }
+  ExtT square_ext(ExtT x) { return mul_ext(x, x); }
+  ExtT mul_many_ext(const std::vector<ExtT> &v);
+  // x / y: the inverse from a generator checked as y * inv == 1, then x * inv + z
+  ExtT div_add_ext(ExtT x, ExtT y, ExtT z);
+  ExtT div_ext(ExtT x, ExtT y) { return div_add_ext(x, y, zero_ext()); }
+  ExtT exp_u64_ext(ExtT base, uint64_t e);
+  ExtT exp_power_of_2_ext(ExtT base, uint32_t k);
+  // PoseidonMdsGate row: the MDS layer of 12 ext values
+  std::vector<ExtT> poseidon_mds(const std::vector<ExtT> &s);
+  // ReducingFactorTarget::reduce_base / reduce: sum_i t_i alpha^i through
+  // ReducingGate / ReducingExtensionGate rows (short inputs: arithmetic ops)
+  ExtT reduce_base(ExtT alpha, const std::vector<Target> &t);
+  ExtT reduce_ext(ExtT alpha, const std::vector<ExtT> &t);
+  ExtT reduce_arithmetic(ExtT alpha, const std::vector<ExtT> &t);
+  // CosetInterpolationGate row: the value at `point` of the polynomial through
+  // (shift w^i, values[i]), i < 16 (w = the 16th root of unity)
+  ExtT interpolate_coset(Target shift, const std::vector<ExtT> &values, ExtT point);
+
   // targets whose values the caller sets before witness generation (fill_targets)
   void mark_input(Target t) { inputs_.push_back(t); }
   void mark_inputs(const std::vector<Target> &ts) { inputs_.insert(inputs_.end(), ts.begin(), ts.end()); }
@@ -253,6 +329,11 @@ class CircuitBuilder {
   std::unordered_map<uint32_t, F> target_to_const_;
   std::map<std::pair<F, F>, std::pair<uint32_t, uint32_t>> arith_open_;  // (c0,c1) -> (row, next op)
   std::map<std::tuple<F, F, uint32_t, uint32_t, uint32_t>, Target> arith_cache_;
+  std::map<std::pair<F, F>, std::pair<uint32_t, uint32_t>> ae_open_;  // ArithmeticExtensionGate slots
+  std::map<F, std::pair<uint32_t, uint32_t>> me_open_;                 // MulExtensionGate slots
+  std::map<std::tuple<F, F, uint32_t, uint32_t, uint32_t, uint32_t, uint32_t, uint32_t>, ExtT> ext_cache_;
+  static F gl_neg_one() { return 0xFFFFFFFF00000000ull; }
+  bool as_const_ext(ExtT t, F &c0, F &c1) const { return as_const(t.c0, c0) && as_const(t.c1, c1); }
   std::pair<uint32_t, uint32_t> ra_open_{0, RA_COPIES};                  // (row, next copy) of the open RandomAccessGate
   uint32_t arith_ops_, base_sum_limbs_;
 };

@@ -277,6 +277,13 @@ int setup(qp_prover *P) {
         // k_quotient_1r evaluates the RandomAccessGate of the recursive verifier's width
         if (cd.gate_params[i] != qpk::RA_QBITS) P->generic_quotient = true;
         break;
+      // the other recursive-verifier gates: the generic (any gate list) kernel
+      case qc::G_ARITH_EXT: g.kind[i] = qpk::GK_ARITH_EXT; P->generic_quotient = true; break;
+      case qc::G_MUL_EXT: g.kind[i] = qpk::GK_MUL_EXT; P->generic_quotient = true; break;
+      case qc::G_REDUCING: g.kind[i] = qpk::GK_REDUCING; P->generic_quotient = true; break;
+      case qc::G_REDUCING_EXT: g.kind[i] = qpk::GK_REDUCING_EXT; P->generic_quotient = true; break;
+      case qc::G_POSEIDON_MDS: g.kind[i] = qpk::GK_POSEIDON_MDS; P->generic_quotient = true; break;
+      case qc::G_COSET_INTERP: g.kind[i] = qpk::GK_COSET_INTERP; P->generic_quotient = true; break;
       default:
         c->err = "unsupported gate kind for the GPU prover";
         return QP_ERR_ARG;

@@ -467,15 +467,31 @@ __device__ __noinline__ void recursion_gate(uint32_t kind, uint32_t q0, uint32_t
         uint64_t idx = 0;
         for (uint32_t i = q0; i-- > 0;) idx = gfn::add(gfn::add(idx, idx), WV(bw + i));
         A.emit(gfn::sub(idx, WV(base)));
-        // the bit-by-bit fold of the list equals sum_i item_i prod_k (bit_k(i) ? b_k : 1 - b_k)
-        uint64_t sel = 0;
-        for (uint32_t i = 0; i < vec; i++) {
-          uint64_t wgt = 1;
-          for (uint32_t k = 0; k < q0; k++) {
+        // the list folded bit by bit (random_access.rs): list[i] <- b (list[2i+1] - list[2i]) + list[2i]
+        uint64_t sel;
+        if (q0 == RA_QBITS) {
+          uint64_t list[1u << RA_QBITS];
+#pragma unroll
+          for (uint32_t i = 0; i < (1u << RA_QBITS); i++) list[i] = WV(base + 2 + i);
+#pragma unroll
+          for (uint32_t k = 0; k < RA_QBITS; k++) {
             const uint64_t b = WV(bw + k);
-            wgt = gfn::mul(wgt, (i >> k) & 1 ? b : gfn::sub(1, b));
+#pragma unroll
+            for (uint32_t i = 0; i < (1u << RA_QBITS) >> (k + 1); i++)
+              list[i] = gfn::add(gfn::mul(b, gfn::sub(list[2 * i + 1], list[2 * i])), list[2 * i]);
           }
-          sel = gfn::add(sel, gfn::mul(wgt, WV(base + 2 + i)));
+          sel = list[0];
+        } else {
+          // other widths: sum_i item_i prod_k (bit_k(i) ? b_k : 1 - b_k), the same value
+          sel = 0;
+          for (uint32_t i = 0; i < vec; i++) {
+            uint64_t wgt = 1;
+            for (uint32_t k = 0; k < q0; k++) {
+              const uint64_t b = WV(bw + k);
+              wgt = gfn::mul(wgt, (i >> k) & 1 ? b : gfn::sub(1, b));
+            }
+            sel = gfn::add(sel, gfn::mul(wgt, WV(base + 2 + i)));
+          }
         }
         A.emit(gfn::sub(sel, WV(base + 1)));
       }
@@ -485,7 +501,8 @@ __device__ __noinline__ void recursion_gate(uint32_t kind, uint32_t q0, uint32_t
     case GK_COSET_INTERP: {  // q0 subgroup bits, q1 degree
       const uint32_t np = 1u << q0, deg = q1, nint = (np - 2) / (deg - 1);
       const uint32_t sv = 1, sep = sv + 2 * np, sev = sep + 2, si = sev + 2, ssh = si + 4 * nint;
-      const uint64_t om = gl::root_of_unity(q0), inv_n = gl::inv(np);
+      // w_16 = 2^12 (the subgroup of the FRI arity-16 cosets), 1 / 2^k = p - (p - 1) / 2^k
+      const uint64_t om = q0 == 4 ? 4096 : gl::root_of_unity(q0), inv_n = gl::P - ((gl::P - 1) >> q0);
       const uint64_t shift = WV(0), sp0 = WV(ssh), sp1 = WV(ssh + 1);
       A.emit(gfn::sub(WV(sep), gfn::mul(sp0, shift)));
       A.emit(gfn::sub(WV(sep + 1), gfn::mul(sp1, shift)));

@@ -131,9 +131,20 @@ std::string parse_common(const uint8_t *b, size_t n, InnerCommon &c) {
     InnerCommon::Gate g{};
     g.id = r.u32();
     switch (g.id) {
-      case 9: case 12: case 11: break;                  // Noop, PublicInput, Poseidon
-      case 3: case 2: case 0: g.p[0] = r.u64(); break;  // Constant, BaseSum<2>, Arithmetic
+      case 9: case 12: case 11: case 10: break;         // Noop, PublicInput, Poseidon, PoseidonMds
+      case 3: case 2: case 0:                           // Constant, BaseSum<2>, Arithmetic,
+      case 1: case 8: case 15: case 14:                 // ArithmeticExtension, MulExtension, Reducing(Extension)
+        g.p[0] = r.u64();
+        break;
       case 13: g.p[0] = r.u64(); g.p[1] = r.u64(); g.p[2] = r.u64(); break;  // RandomAccess
+      case 4: {  // CosetInterpolation: subgroup_bits, degree, barycentric_weights
+        g.p[0] = r.u64();
+        g.p[1] = r.u64();
+        const uint64_t nw = r.u64();
+        if (g.p[0] > 6 || nw != (1ull << g.p[0]) || g.p[1] < 2) return "bad CosetInterpolationGate";
+        for (uint64_t i = 0; i < nw; i++) r.u64();
+        break;
+      }
       default: return "unsupported gate (DefaultGateSerializer id " + std::to_string(g.id) + ") in the inner circuit";
     }
     c.gates.push_back(g);
@@ -142,9 +153,11 @@ std::string parse_common(const uint8_t *b, size_t n, InnerCommon &c) {
   if (c.num_challenges != 2 || c.hiding) return "unsupported inner config";
   if (c.selector_indices.size() != c.gates.size() || c.k_is.size() != c.num_routed_wires)
     return "inconsistent CommonCircuitData";
-  for (auto &g : c.gates)
+  for (auto &g : c.gates) {
     if (g.id == 13 && (g.p[0] != qc::RA_BITS || g.p[1] != qc::RA_COPIES || g.p[2] != qc::RA_EXTRA))
       return "unsupported RandomAccessGate shape";
+    if (g.id == 4 && (g.p[0] != qc::CI_BITS || g.p[1] != qc::CI_DEGREE)) return "unsupported CosetInterpolationGate shape";
+  }
   return "";
 }
 
@@ -175,84 +188,27 @@ struct G {
   CircuitBuilder &b;
   explicit G(CircuitBuilder &bb) : b(bb) {}
 
+  // extension arithmetic on ArithmeticExtension / MulExtension gate ops
+  // (gadgets/arithmetic_extension.rs), as upstream's recursive verifier builds it
   Target zero() { return b.zero(); }
   Target one() { return b.one(); }
-  ExtT ext(Target x) { return {x, b.zero()}; }
-  ExtT ext_const(F c0, F c1 = 0) { return {b.constant(c0), b.constant(c1)}; }
-  ExtT ext_zero() { return {b.zero(), b.zero()}; }
-  ExtT add(ExtT a, ExtT c) { return {b.add(a.c0, c.c0), b.add(a.c1, c.c1)}; }
-  ExtT sub(ExtT a, ExtT c) { return {b.sub(a.c0, c.c0), b.sub(a.c1, c.c1)}; }
-  // (a0 + a1 X)(c0 + c1 X), X^2 = 7: (a0 c0 + 7 a1 c1) + (a0 c1 + a1 c0) X
-  ExtT mul(ExtT a, ExtT c) {
-    Target t = b.mul(a.c1, c.c1);
-    Target r0 = b.arithmetic(1, gl::EXT_W, a.c0, c.c0, t);
-    Target u = b.mul(a.c1, c.c0);
-    Target r1 = b.mul_add(a.c0, c.c1, u);
-    return {r0, r1};
-  }
-  // a * c + d
-  ExtT mul_add(ExtT a, ExtT c, ExtT d) {
-    Target t = b.mul(a.c1, c.c1);
-    Target r0 = b.add(b.arithmetic(1, gl::EXT_W, a.c0, c.c0, t), d.c0);
-    Target r1 = b.mul_add(a.c0, c.c1, b.mul_add(a.c1, c.c0, d.c1));
-    return {r0, r1};
-  }
-  // a * c - d
-  ExtT mul_sub(ExtT a, ExtT c, ExtT d) { return sub(mul(a, c), d); }
-  ExtT mul_base(ExtT a, Target s) { return {b.mul(a.c0, s), b.mul(a.c1, s)}; }
-  // a * s + d (s base)
-  ExtT mul_base_add(ExtT a, Target s, ExtT d) { return {b.mul_add(a.c0, s, d.c0), b.mul_add(a.c1, s, d.c1)}; }
-  ExtT scale(ExtT a, F c) { return {b.mul_const(c, a.c0), b.mul_const(c, a.c1)}; }
-  ExtT add_const(ExtT a, F c) { return {b.add(a.c0, b.constant(c)), a.c1}; }
-  ExtT sub_base(ExtT a, Target s) { return {b.sub(a.c0, s), a.c1}; }
-  ExtT square(ExtT a) { return mul(a, a); }
-  ExtT exp_pow2(ExtT a, uint32_t k) {
-    for (uint32_t i = 0; i < k; i++) a = square(a);
-    return a;
-  }
-  // num / den: quotient from a host generator (QuotientGeneratorExtension),
-  // checked as den * q == num
-  ExtT div(ExtT num, ExtT den) {
-    ExtT q{b.add_virtual_target(), b.add_virtual_target()};
-    qc::Gen g{};
-    g.kind = qc::GEN_EXT_DIV;
-    g.a = num.c0;
-    g.b = num.c1;
-    g.c = den.c0;
-    g.d = den.c1;
-    g.e = q.c0;
-    g.f = q.c1;
-    b.add_generator(g);
-    connect(mul(den, q), num);
-    return q;
-  }
-  void connect(ExtT a, ExtT c) {
-    b.connect(a.c0, c.c0);
-    b.connect(a.c1, c.c1);
-  }
-  ExtT mul_many(const std::vector<ExtT> &v) {
-    ExtT acc = v[0];
-    for (size_t i = 1; i < v.size(); i++) acc = mul(acc, v[i]);
-    return acc;
-  }
-  // sum_i c_i x_i with small constant c_i (MDS rows)
-  Target lin_comb(const uint64_t *c, const Target *x, size_t n) {
-    Target acc = b.mul_const(c[0], x[0]);
-    for (size_t i = 1; i < n; i++) acc = b.mul_const_add(c[i], x[i], acc);
-    return acc;
-  }
-  // ReducingFactorTarget::reduce: sum_k t_k alpha^k (Horner from the last term)
-  ExtT reduce_base_alpha(const std::vector<ExtT> &t, Target alpha) {
-    ExtT acc = ext_zero();
-    for (size_t i = t.size(); i-- > 0;) acc = mul_base_add(acc, alpha, t[i]);
-    return acc;
-  }
-  ExtT reduce_ext(const std::vector<ExtT> &t, ExtT alpha) {
-    ExtT acc = ext_zero();
-    for (size_t i = t.size(); i-- > 0;) acc = mul_add(acc, alpha, t[i]);
-    return acc;
-  }
-  // exp_from_bits_const_base: prod (1 + bit_i (base^(2^i) - 1))
+  ExtT ext(Target x) { return b.convert_to_ext(x); }
+  ExtT ext_const(F c0, F c1 = 0) { return b.constant_ext(c0, c1); }
+  ExtT ext_zero() { return b.zero_ext(); }
+  ExtT add(ExtT a, ExtT c) { return b.add_ext(a, c); }
+  ExtT sub(ExtT a, ExtT c) { return b.sub_ext(a, c); }
+  ExtT mul(ExtT a, ExtT c) { return b.mul_ext(a, c); }
+  ExtT mul_add(ExtT a, ExtT c, ExtT d) { return b.mul_add_ext(a, c, d); }
+  ExtT mul_sub(ExtT a, ExtT c, ExtT d) { return b.mul_sub_ext(a, c, d); }
+  ExtT scale(ExtT a, F c) { return b.scalar_mul_ext(c, a); }
+  ExtT add_const(ExtT a, F c) { return b.add_const_ext(a, c); }
+  ExtT div(ExtT num, ExtT den) { return b.div_ext(num, den); }
+  ExtT div_add(ExtT num, ExtT den, ExtT z) { return b.div_add_ext(num, den, z); }
+  ExtT square(ExtT a) { return b.square_ext(a); }
+  ExtT exp_pow2(ExtT a, uint32_t k) { return b.exp_power_of_2_ext(a, k); }
+  void connect(ExtT a, ExtT c) { b.connect_ext(a, c); }
+  ExtT mul_many(const std::vector<ExtT> &v) { return b.mul_many_ext(v); }
+  // exp_from_bits_const_base: prod (1 + bit_i (base^(2^i) - 1)) (base arithmetic)
   Target exp_from_bits_const_base(F base, const std::vector<Target> &bits) {
     Target p = b.one();
     F bp = base;
@@ -270,6 +226,29 @@ struct G {
   Target exp_pow2_base(Target x, uint32_t k) {
     for (uint32_t i = 0; i < k; i++) x = b.mul(x, x);
     return x;
+  }
+  // ExtensionAlgebraTarget<2> (the recursion gates' values at zeta: pairs of
+  // extension targets a + b Y, Y^2 = 7; gadgets/arithmetic_extension.rs)
+  struct Alg {
+    ExtT a, b;
+  };
+  Alg alg(const std::vector<ExtT> &w, uint32_t i) { return {w[i], w[i + 1]}; }
+  Alg alg_zero() { return {ext_zero(), ext_zero()}; }
+  Alg alg_sub(Alg x, Alg y) { return {sub(x.a, y.a), sub(x.b, y.b)}; }
+  // mul_add_ext_algebra: the W-weighted inner product first, then the plain one
+  Alg alg_mul_add(Alg x, Alg y, Alg z) {
+    ExtT r0 = b.arithmetic_extension(gl::EXT_W, 1, x.b, y.b, z.a);
+    r0 = b.mul_add_ext(x.a, y.a, r0);
+    ExtT r1 = b.mul_add_ext(x.a, y.b, z.b);
+    r1 = b.mul_add_ext(x.b, y.a, r1);
+    return {r0, r1};
+  }
+  Alg alg_mul(Alg x, Alg y) { return alg_mul_add(x, y, alg_zero()); }
+  Alg alg_scalar_mul_add(ExtT c, Alg x, Alg z) { return {mul_add(c, x.a, z.a), mul_add(c, x.b, z.b)}; }
+  Alg alg_scalar_mul(ExtT c, Alg x) { return alg_scalar_mul_add(c, x, alg_zero()); }
+  void push(std::vector<ExtT> &out, Alg x) {
+    out.push_back(x.a);
+    out.push_back(x.b);
   }
 };
 
@@ -315,42 +294,24 @@ struct Chal {
   }
 };
 
-constexpr uint64_t MDS_C[12] = {17, 15, 41, 16, 2, 28, 13, 13, 39, 18, 34, 20};
-
-// MDS layer on extension states (base constants act per component)
+// MDS layer on ext states: one PoseidonMdsGate row (mds_layer_circuit with
+// num_routed_wires >= 48)
 void mds_ext(G &g, ExtT s[12]) {
-  ExtT o[12];
-  for (int r = 0; r < 12; r++) {
-    uint64_t c[13];
-    Target x0[13], x1[13];
-    for (int i = 0; i < 12; i++) {
-      c[i] = MDS_C[i];
-      x0[i] = s[(i + r) % 12].c0;
-      x1[i] = s[(i + r) % 12].c1;
-    }
-    size_t n = 12;
-    if (r == 0) {
-      c[12] = 8;
-      x0[12] = s[0].c0;
-      x1[12] = s[0].c1;
-      n = 13;
-    }
-    o[r] = {g.lin_comb(c, x0, n), g.lin_comb(c, x1, n)};
-  }
-  for (int r = 0; r < 12; r++) s[r] = o[r];
+  std::vector<ExtT> v(s, s + 12);
+  v = g.b.poseidon_mds(v);
+  for (int r = 0; r < 12; r++) s[r] = v[r];
 }
 
-ExtT sbox_ext(G &g, ExtT x) {
-  ExtT x2 = g.square(x);
-  ExtT x4 = g.square(x2);
-  ExtT x3 = g.mul(x2, x);
-  return g.mul(x3, x4);
-}
+// sbox_monomial_circuit: exp_u64_extension(x, 7)
+ExtT sbox_ext(G &g, ExtT x) { return g.b.exp_u64_ext(x, 7); }
 
-// gates/*::eval_unfiltered (values at zeta), SURVEY.md A.5
+// gates/*::eval_unfiltered_circuit (values at zeta), in upstream plonky2's
+// operation forms (values pinned by SURVEY.md A.5 for the leaf gates; the
+// recursion gates' formulas restate upstream, parity unpinned)
 std::vector<ExtT> gate_constraints(G &g, const InnerCommon::Gate &gate, const std::vector<ExtT> &w,
                                    const ExtT *gc, const std::vector<Target> &pi_hash) {
   std::vector<ExtT> out;
+  CircuitBuilder &b = g.b;
   switch (gate.id) {
     case 9:  // Noop
       break;
@@ -358,25 +319,85 @@ std::vector<ExtT> gate_constraints(G &g, const InnerCommon::Gate &gate, const st
       for (uint32_t i = 0; i < gate.p[0]; i++) out.push_back(g.sub(gc[i], w[i]));
       break;
     case 12:  // PublicInput
-      for (uint32_t i = 0; i < 4; i++) out.push_back(g.sub_base(w[i], pi_hash[i]));
+      for (uint32_t i = 0; i < 4; i++) out.push_back(g.sub(w[i], g.ext(pi_hash[i])));
       break;
-    case 2: {  // BaseSum<2>
+    case 2: {  // BaseSum<2>: the recomposed sum, then limb (limb - 1) per limb
       const uint32_t L = (uint32_t)gate.p[0];
-      ExtT acc = w[L];
-      for (uint32_t i = L - 1; i-- > 0;) acc = g.add(g.scale(acc, 2), w[1 + i]);
-      out.push_back(g.sub(acc, w[0]));
-      for (uint32_t i = 0; i < L; i++) {
-        ExtT l = w[1 + i];
-        out.push_back(g.mul(l, g.add_const(l, NEG_ONE)));
-      }
+      std::vector<ExtT> limbs(w.begin() + 1, w.begin() + 1 + L);
+      out.push_back(g.sub(b.reduce_ext(g.ext_const(2), limbs), w[0]));
+      for (ExtT l : limbs) out.push_back(g.mul_sub(l, l, l));
       break;
     }
     case 0: {  // Arithmetic: out - (c0 m0 m1 + c1 addend)
       for (uint32_t i = 0; i < gate.p[0]; i++) {
-        ExtT prod = g.mul(g.mul(w[4 * i], w[4 * i + 1]), gc[0]);
-        ExtT comp = g.mul_add(w[4 * i + 2], gc[1], prod);
+        ExtT scaled = g.mul_many({gc[0], w[4 * i], w[4 * i + 1]});
+        ExtT comp = g.mul_add(gc[1], w[4 * i + 2], scaled);
         out.push_back(g.sub(w[4 * i + 3], comp));
       }
+      break;
+    }
+    case 1:    // ArithmeticExtension{num_ops}: out - (c0 m0 m1 + c1 addend), algebra
+    case 8: {  // MulExtension{num_ops}: out - c0 m0 m1
+      const bool ae = gate.id == 1;
+      for (uint32_t i = 0; i < gate.p[0]; i++) {
+        const uint32_t o = ae ? 8 * i : 6 * i;
+        G::Alg scaled = g.alg_scalar_mul(gc[0], g.alg_mul(g.alg(w, o), g.alg(w, o + 2)));
+        if (ae) scaled = g.alg_scalar_mul_add(gc[1], g.alg(w, o + 4), scaled);
+        g.push(out, g.alg_sub(g.alg(w, ae ? o + 6 : o + 4), scaled));
+      }
+      break;
+    }
+    case 15:    // Reducing{num_coeffs}: acc_i - (acc_{i-1} alpha + coeff_i), base coefficients
+    case 14: {  // ReducingExtension{num_coeffs}: ext coefficients
+      const uint32_t nc = (uint32_t)gate.p[0], cw = gate.id == 15 ? 1 : 2;
+      const G::Alg alpha = g.alg(w, 2);
+      G::Alg acc = g.alg(w, 4);
+      for (uint32_t i = 0; i < nc; i++) {
+        const G::Alg coeff = cw == 1 ? G::Alg{w[6 + i], g.ext_zero()} : g.alg(w, 6 + 2 * i);
+        const G::Alg next = g.alg(w, i + 1 == nc ? 0 : 6 + cw * nc + 2 * i);
+        g.push(out, g.alg_sub(g.alg_mul_add(acc, alpha, coeff), next));
+        acc = next;
+      }
+      break;
+    }
+    case 10: {  // PoseidonMds: out_r - (sum_i CIRC[i] in_{i+r} + DIAG[r] in_r), algebra
+      for (uint32_t r = 0; r < 12; r++) {
+        G::Alg res = g.alg_zero();
+        for (uint32_t i = 0; i < 12; i++)
+          res = g.alg_scalar_mul_add(g.ext_const(ps::mds_circ(i)), g.alg(w, 2 * ((i + r) % 12)), res);
+        res = g.alg_scalar_mul_add(g.ext_const(r == 0 ? 8 : 0), g.alg(w, 2 * r), res);
+        g.push(out, g.alg_sub(g.alg(w, 24 + 2 * r), res));
+      }
+      break;
+    }
+    case 4: {  // CosetInterpolation{subgroup_bits, degree}
+      const uint32_t nbits = (uint32_t)gate.p[0], deg = (uint32_t)gate.p[1], np = 1u << nbits;
+      const uint32_t nint = (np - 2) / (deg - 1);
+      const uint32_t sv = 1, sep = sv + 2 * np, sev = sep + 2, si = sev + 2, ssh = si + 4 * nint;
+      const ExtT shift = w[0];
+      const G::Alg ep = g.alg(w, sep), sp = g.alg(w, ssh);
+      g.push(out, g.alg_scalar_mul_add(g.scale(shift, gl::P - 1), sp, ep));
+      const F om = gl::root_of_unity(nbits), ninv = gl::inv(np);
+      G::Alg ev = g.alg_zero(), pr{g.ext_const(1), g.ext_zero()};
+      uint32_t lo = 0, hi = deg;
+      for (uint32_t it = 0;; it++) {
+        for (uint32_t i = lo; i < hi; i++) {
+          const F x = gl::pow(om, i);
+          const G::Alg term{g.sub(sp.a, g.ext_const(x)), sp.b};
+          const G::Alg wv = g.alg_scalar_mul(g.ext_const(gl::mul(x, ninv)), g.alg(w, sv + 2 * i));
+          ev = g.alg_mul_add(wv, pr, g.alg_mul(ev, term));
+          pr = g.alg_mul(pr, term);
+        }
+        if (it == nint) break;
+        const G::Alg ie = g.alg(w, si + 2 * it), ip = g.alg(w, si + 2 * (nint + it));
+        g.push(out, g.alg_sub(ie, ev));
+        g.push(out, g.alg_sub(ip, pr));
+        ev = ie;
+        pr = ip;
+        lo = 1 + (deg - 1) * (it + 1);
+        hi = std::min(lo + deg - 1, np);
+      }
+      g.push(out, g.alg_sub(g.alg(w, sev), ev));
       break;
     }
     case 13: {  // RandomAccess{bits, copies, extra}
@@ -386,14 +407,16 @@ std::vector<ExtT> gate_constraints(G &g, const InnerCommon::Gate &gate, const st
         const uint32_t base = (2 + vec) * cp;
         std::vector<ExtT> bw(bits);
         for (uint32_t i = 0; i < bits; i++) bw[i] = w[routed + cp * bits + i];
-        for (uint32_t i = 0; i < bits; i++) out.push_back(g.mul(bw[i], g.add_const(bw[i], NEG_ONE)));
-        ExtT idx = bw[bits - 1];
-        for (uint32_t i = bits - 1; i-- > 0;) idx = g.add(g.scale(idx, 2), bw[i]);
+        for (uint32_t i = 0; i < bits; i++) out.push_back(g.mul_sub(bw[i], bw[i], bw[i]));
+        ExtT idx = g.ext_zero();
+        for (uint32_t i = bits; i-- > 0;) idx = b.mul_const_add_ext(2, idx, bw[i]);
         out.push_back(g.sub(idx, w[base]));
         std::vector<ExtT> list(w.begin() + base + 2, w.begin() + base + 2 + vec);
         for (uint32_t i = 0; i < bits; i++) {
           std::vector<ExtT> nx(list.size() / 2);
-          for (size_t j = 0; j < nx.size(); j++) nx[j] = g.mul_add(bw[i], g.sub(list[2 * j + 1], list[2 * j]), list[2 * j]);
+          // select_ext_generalized(b, y, x) = b y - (b x - x)
+          for (size_t j = 0; j < nx.size(); j++)
+            nx[j] = g.mul_sub(bw[i], list[2 * j + 1], g.mul_sub(bw[i], list[2 * j], list[2 * j]));
           list = nx;
         }
         out.push_back(g.sub(list[0], w[base + 1]));
@@ -401,13 +424,13 @@ std::vector<ExtT> gate_constraints(G &g, const InnerCommon::Gate &gate, const st
       for (uint32_t i = 0; i < extra; i++) out.push_back(g.sub(gc[i], w[(2 + vec) * copies + i]));
       break;
     }
-    case 11: {  // Poseidon (naive rounds, wire substitution at every stored S-box input)
+    case 11: {  // Poseidon: constant layers, x^7 S-boxes, PoseidonMdsGate layers, wire checks
       ExtT swap = w[24];
-      out.push_back(g.mul(swap, g.add_const(swap, NEG_ONE)));
+      out.push_back(g.mul_sub(swap, swap, swap));
+      for (int i = 0; i < 4; i++) out.push_back(g.mul_sub(swap, g.sub(w[i + 4], w[i]), w[25 + i]));
       ExtT s[12];
       for (int i = 0; i < 4; i++) {
         ExtT delta = w[25 + i];
-        out.push_back(g.sub(g.mul(swap, g.sub(w[i + 4], w[i])), delta));
         s[i] = g.add(w[i], delta);
         s[i + 4] = g.sub(w[i + 4], delta);
       }
@@ -484,26 +507,6 @@ void verify_merkle(CircuitBuilder &b, const std::vector<Target> &leaf, const std
     for (size_t e = 0; e < cl; e++) col[e] = cap[4 * e + i];
     b.connect(b.random_access(cap_index, col), h[i]);
   }
-}
-
-// interpolate {(c g^i, e_i)} at beta (barycentric over the coset of size 2^ab):
-// p(beta) = (beta^m - c^m) / (m c^m) * sum_i e_i y_i / (beta - y_i), y_i = c g^i
-ExtT interpolate_coset(G &g, Target c, const std::vector<ExtT> &e, ExtT beta, uint32_t ab) {
-  CircuitBuilder &b = g.b;
-  const uint32_t m = 1u << ab;
-  const F om = gl::root_of_unity(ab);
-  ExtT sum = g.ext_zero();
-  F gi = 1;
-  for (uint32_t i = 0; i < m; i++) {
-    Target y = i ? b.mul_const(gi, c) : c;
-    ExtT num = g.mul_base(e[i], y);
-    sum = g.add(sum, g.div(num, g.sub_base(beta, y)));
-    gi = gl::mul(gi, om);
-  }
-  Target cm = g.exp_pow2_base(c, ab);
-  ExtT zb = g.sub_base(g.exp_pow2(beta, ab), cm);
-  Target mcm = b.mul_const(m, cm);
-  return g.div(g.mul(zb, sum), g.ext(mcm));
 }
 
 }  // namespace
@@ -584,6 +587,7 @@ static void verify_proof(CircuitBuilder &b, const InnerCommon &c, const ProofTar
 
   // ---- vanishing polynomial at zeta (eval_vanishing_poly_circuit)
   ExtT zeta_n = g.exp_pow2(zeta, log_n);
+  // evaluate_gate_constraints_circuit: per gate its filter times each constraint
   std::vector<ExtT> gate_terms(c.num_gate_constraints, g.ext_zero());
   for (size_t gi = 0; gi < c.gates.size(); gi++) {
     const uint32_t si = c.selector_indices[gi];
@@ -593,16 +597,17 @@ static void verify_proof(CircuitBuilder &b, const InnerCommon &c, const ProofTar
     for (uint32_t j = grp.first; j < grp.second; j++)
       if (j != gi) fac.push_back(g.sub(g.ext_const(j), s));
     if (nsel > 1) fac.push_back(g.sub(g.ext_const(UNUSED_SELECTOR), s));
-    ExtT filter = fac.empty() ? g.ext_const(1) : g.mul_many(fac);
+    ExtT filter = g.mul_many(fac);
     auto cs = gate_constraints(g, c.gates[gi], p.wires, p.constants_sigmas.data() + nsel, pi_hash);
     if (cs.size() > gate_terms.size()) throw std::runtime_error("gate constraint count exceeds num_gate_constraints");
     for (size_t k = 0; k < cs.size(); k++) gate_terms[k] = g.mul_add(filter, cs[k], gate_terms[k]);
   }
-  // L_0(zeta) = (zeta^n - 1) / (n (zeta - 1))
-  ExtT zh = g.add_const(zeta_n, NEG_ONE);
-  ExtT l0 = g.div(zh, g.scale(g.add_const(zeta, NEG_ONE), (F)1 << log_n));
+  // eval_l_0_circuit: L_0(zeta) = (zeta^n - 1) / (n (zeta - 1))
+  ExtT zh = g.sub(zeta_n, g.ext_const(1));
+  const F nn = (F)1 << log_n;
+  ExtT l0 = g.div(zh, b.arithmetic_extension(nn, nn, zeta, g.ext_const(1), g.ext(b.constant(NEG_ONE))));
   std::vector<ExtT> s_ids(R);
-  for (uint32_t j = 0; j < R; j++) s_ids[j] = g.scale(zeta, c.k_is[j]);
+  for (uint32_t j = 0; j < R; j++) s_ids[j] = b.mul_ext(b.convert_to_ext(b.constant(c.k_is[j])), zeta);
   std::vector<ExtT> z1_terms, pp_terms;
   const ExtT *sig = p.constants_sigmas.data() + c.num_constants;
   for (uint32_t i = 0; i < nc; i++) {
@@ -611,9 +616,10 @@ static void verify_proof(CircuitBuilder &b, const InnerCommon &c, const ProofTar
     std::vector<ExtT> num(R), den(R);
     for (uint32_t j = 0; j < R; j++) {
       ExtT wg = g.add(p.wires[j], g.ext(gammas[i]));
-      num[j] = g.mul_base_add(s_ids[j], betas[i], wg);
-      den[j] = g.mul_base_add(sig[j], betas[i], wg);
+      num[j] = g.mul_add(g.ext(betas[i]), s_ids[j], wg);
+      den[j] = g.mul_add(g.ext(betas[i]), sig[j], wg);
     }
+    // check_partial_products_circuit
     std::vector<ExtT> accs{z};
     for (uint32_t k = 0; k < npp; k++) accs.push_back(p.pp[i * npp + k]);
     accs.push_back(zn);
@@ -621,31 +627,27 @@ static void verify_proof(CircuitBuilder &b, const InnerCommon &c, const ProofTar
       const uint32_t lo = k * qdf, hi = std::min(R, lo + qdf);
       ExtT np = g.mul_many(std::vector<ExtT>(num.begin() + lo, num.begin() + hi));
       ExtT dp = g.mul_many(std::vector<ExtT>(den.begin() + lo, den.begin() + hi));
-      pp_terms.push_back(g.sub(g.mul(accs[k], np), g.mul(accs[k + 1], dp)));
+      pp_terms.push_back(g.mul_sub(accs[k], np, g.mul(accs[k + 1], dp)));
     }
   }
   std::vector<ExtT> terms = z1_terms;
   terms.insert(terms.end(), pp_terms.begin(), pp_terms.end());
   terms.insert(terms.end(), gate_terms.begin(), gate_terms.end());
+  // verify_proof_with_challenges: vanishing(zeta) == Z_H(zeta) * sum_k q_k zeta^(n k)
   for (uint32_t i = 0; i < nc; i++) {
-    ExtT van = g.reduce_base_alpha(terms, alphas[i]);
+    ExtT van = b.reduce_ext(g.ext(alphas[i]), terms);
     std::vector<ExtT> chunk(p.quotient.begin() + i * qdf, p.quotient.begin() + (i + 1) * qdf);
-    ExtT rec = g.reduce_ext(chunk, zeta_n);
+    ExtT rec = b.reduce_ext(zeta_n, chunk);
     g.connect(van, g.mul(zh, rec));
   }
 
   // ---- FRI (verify_fri_proof)
   const F g_n = gl::root_of_unity(log_n);
   ExtT zeta_next = g.scale(zeta, g_n);
-  // precomputed reduced openings (ReducingFactorTarget over each batch)
-  ExtT red0 = g.reduce_ext(zbatch, fri_alpha);
-  ExtT red1 = g.reduce_ext(p.zs_next, fri_alpha);
-  // powers of alpha for the per-query base reductions (the same values as Horner)
+  // PrecomputedReducedOpeningsTarget::from_os_and_alpha
+  ExtT red0 = b.reduce_ext(fri_alpha, zbatch);
+  ExtT red1 = b.reduce_ext(fri_alpha, p.zs_next);
   const size_t nb0 = zbatch.size();
-  std::vector<ExtT> apow(nb0);
-  apow[0] = g.ext_const(1);
-  for (size_t k = 1; k < nb0; k++) apow[k] = g.mul(apow[k - 1], fri_alpha);
-  ExtT alpha_sq = apow[nc];  // shift of the zeta-batch sum by alpha^(#g*zeta batch)
   const std::vector<Target> *caps[4] = {&vd_cap, &p.wires_cap, &p.zs_cap, &p.quot_cap};
   const F phi = gl::root_of_unity(logN);
   for (uint32_t q = 0; q < c.num_query_rounds; q++) {
@@ -656,27 +658,18 @@ static void verify_proof(CircuitBuilder &b, const InnerCommon &c, const ProofTar
     for (int o = 0; o < 4; o++) verify_merkle(b, qt.leaf[o], bits, cap_idx, *caps[o], qt.sib[o]);
     std::vector<Target> rbits(bits.rbegin(), bits.rend());
     Target x = b.mul(b.constant(gl::GEN), g.exp_from_bits_const_base(phi, rbits));
-    // fri_combine_initial
-    Target acc0 = b.zero(), acc1 = b.zero();
-    size_t k = 0;
-    for (int o = 0; o < 4; o++)
-      for (Target v : qt.leaf[o]) {
-        if (k == 0) {
-          acc0 = v;
-        } else {
-          acc0 = b.mul_add(apow[k].c0, v, acc0);
-          acc1 = b.mul_add(apow[k].c1, v, acc1);
-        }
-        k++;
-      }
-    ExtT rv0{acc0, acc1};
-    // the g*zeta batch: the first nc polynomials of oracle 2 (the Z's)
-    std::vector<ExtT> zl;
-    for (uint32_t i = 0; i < nc; i++) zl.push_back(g.ext(qt.leaf[2][i]));
-    ExtT rv1 = g.reduce_ext(zl, fri_alpha);
-    ExtT t0 = g.div(g.sub(rv0, red0), g.sub(g.ext(x), zeta));
-    ExtT t1 = g.div(g.sub(rv1, red1), g.sub(g.ext(x), zeta_next));
-    ExtT old_eval = g.mul_add(t0, alpha_sq, t1);
+    // fri_combine_initial: per batch reduce_base of the opened leaf values,
+    // shift the running sum by alpha^(batch length), div_add
+    ExtT xe = g.ext(x);
+    std::vector<Target> ev0;
+    for (int o = 0; o < 4; o++) ev0.insert(ev0.end(), qt.leaf[o].begin(), qt.leaf[o].end());
+    if (ev0.size() != nb0) throw std::runtime_error("opened leaf widths differ from the zeta batch");
+    ExtT rv0 = b.reduce_base(fri_alpha, ev0);
+    ExtT sum = g.div_add(g.sub(rv0, red0), g.sub(xe, zeta), g.ext_zero());
+    std::vector<Target> ev1(qt.leaf[2].begin(), qt.leaf[2].begin() + nc);
+    ExtT rv1 = b.reduce_base(fri_alpha, ev1);
+    sum = g.mul(b.exp_u64_ext(fri_alpha, ev1.size()), sum);
+    ExtT old_eval = g.div_add(g.sub(rv1, red1), g.sub(xe, zeta_next), sum);
     // folding layers
     Target sx = x;
     for (size_t l = 0; l < c.arity_bits.size(); l++) {
@@ -690,16 +683,18 @@ static void verify_proof(CircuitBuilder &b, const InnerCommon &c, const ProofTar
         e0[i] = ev[i].c0;
         e1[i] = ev[i].c1;
       }
+      // random_access_extension
       g.connect(ExtT{b.random_access(within_idx, e0), b.random_access(within_idx, e1)}, old_eval);
       // compute_evaluation: interpolate the bit-reversed evals over the coset
-      // starting at x * g_inv^rev(within)
+      // starting at x * g_inv^rev(within) (CosetInterpolationGate)
       const F gen = gl::root_of_unity(ab);
       const F g_inv = gl::pow(gen, (1ull << ab) - 1);
       std::vector<Target> rwithin(within.rbegin(), within.rend());
       Target start = b.mul(g.exp_from_bits_const_base(g_inv, rwithin), sx);
       std::vector<ExtT> erev(ev.size());
       for (uint32_t i = 0; i < ev.size(); i++) erev[gl::rev_bits(i, ab)] = ev[i];
-      old_eval = interpolate_coset(g, start, erev, fri_betas[l], ab);
+      if (ab != qc::CI_BITS) throw std::runtime_error("FRI arity other than 16 is not supported");
+      old_eval = b.interpolate_coset(start, erev, fri_betas[l]);
       std::vector<Target> flat;
       for (ExtT e : ev) {
         flat.push_back(e.c0);
@@ -709,9 +704,8 @@ static void verify_proof(CircuitBuilder &b, const InnerCommon &c, const ProofTar
       sx = g.exp_pow2_base(sx, ab);
       bits = coset;
     }
-    // final polynomial at x (PolynomialCoeffsExtTarget::eval_scalar)
-    ExtT fe = g.ext_zero();
-    for (size_t i = p.final_poly.size(); i-- > 0;) fe = g.mul_base_add(fe, sx, p.final_poly[i]);
+    // final polynomial at x (PolynomialCoeffsExtTarget::eval_scalar: reduce by x)
+    ExtT fe = b.reduce_ext(g.ext(sx), p.final_poly);
     g.connect(fe, old_eval);
   }
 }

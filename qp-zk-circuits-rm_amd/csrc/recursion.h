@@ -7,12 +7,18 @@
 //
 // The inner circuits are this library's: the Wormhole / voting leaf circuits
 // (Noop, Constant, PublicInput, BaseSum, Arithmetic, Poseidon) and the
-// aggregation circuits themselves (+ RandomAccess).  Extension-field work is
-// expressed with base ArithmeticGate operations (4 per product), Merkle caps
-// and coset evaluations are selected with RandomAccessGate copies, FRI coset
-// interpolation is barycentric with host-generated quotients checked in-circuit.
-// Values, not layout, are what the verifier must reproduce: every challenge,
-// vanishing term and FRI check equals plonky2's.
+// aggregation circuits themselves.  The gadgets are upstream's recursive
+// verifier's, on upstream's gates: extension arithmetic on
+// ArithmeticExtension / MulExtension ops (special cases and operation dedup as
+// gadgets/arithmetic_extension.rs), divisions through an inverse generator,
+// the in-circuit Poseidon gate evaluation on PoseidonMds layers, the alpha
+// reductions on Reducing / ReducingExtension rows, the FRI coset checks on
+// CosetInterpolation rows, Merkle caps and coset evaluations selected with
+// RandomAccess copies.  Two degree-13 Wormhole proofs then fit 2^13 rows
+// (7,596 gates), and so do two aggregation proofs (7,917).  Values are pinned
+// (every challenge, vanishing term and FRI check equals plonky2's, SURVEY.md
+// A.4-A.7: the reference's own proofs verify inside); the gate layout restates
+// upstream without a fixture (parity unpinned).
 #pragma once
 #include <stdint.h>
 #include <string>
@@ -24,9 +30,7 @@ namespace qr {
 using qc::F;
 using qc::Target;
 
-struct ExtT {
-  Target c0, c1;
-};
+using qc::ExtT;
 
 // CommonCircuitData of the circuit whose proofs are verified (parsed bytes)
 struct InnerCommon {

@@ -68,9 +68,18 @@ int qp_circuit_gate_desc(const qp_circuit *c, qp_gate_desc *g) {
       case qc::G_BASE_SUM: g->kind[i] = QP_GATE_BASE_SUM; break;
       case qc::G_ARITHMETIC: g->kind[i] = QP_GATE_ARITHMETIC; break;
       case qc::G_POSEIDON: g->kind[i] = QP_GATE_POSEIDON; break;
+      case qc::G_RANDOM_ACCESS: g->kind[i] = QP_GATE_RANDOM_ACCESS; break;
+      case qc::G_ARITH_EXT: g->kind[i] = QP_GATE_ARITHMETIC_EXTENSION; break;
+      case qc::G_MUL_EXT: g->kind[i] = QP_GATE_MUL_EXTENSION; break;
+      case qc::G_REDUCING: g->kind[i] = QP_GATE_REDUCING; break;
+      case qc::G_REDUCING_EXT: g->kind[i] = QP_GATE_REDUCING_EXTENSION; break;
+      case qc::G_POSEIDON_MDS: g->kind[i] = QP_GATE_POSEIDON_MDS; break;
+      case qc::G_COSET_INTERP: g->kind[i] = QP_GATE_COSET_INTERPOLATION; break;
       default: return QP_ERR_ARG;
     }
     g->param[i] = cd.gate_params[i];
+    g->param2[i] = i < cd.gate_params2.size() ? cd.gate_params2[i] : 0;
+    g->param3[i] = i < cd.gate_params3.size() ? cd.gate_params3[i] : 0;
     g->selector_index[i] = cd.selector_indices[i];
   }
   g->num_selectors = (uint32_t)cd.groups.size();

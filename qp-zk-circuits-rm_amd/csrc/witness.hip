@@ -29,9 +29,19 @@ struct DevGenD {  // == qc::DevGen
   uint64_t k0, k1;
 };
 enum : uint32_t { WG_CONSTANT = 0, WG_ARITH, WG_POSEIDON, WG_BASE_SPLIT, WG_EQUALITY,
-                  WG_WIRE_SPLIT, WG_EXT_DIV, WG_RANDOM_ACCESS };
+                  WG_WIRE_SPLIT, WG_EXT_DIV, WG_RANDOM_ACCESS, WG_ARITH_EXT, WG_MUL_EXT, WG_REDUCING,
+                  WG_REDUCING_EXT, WG_POSEIDON_MDS, WG_COSET_INTERP };
+// recursion-gate shapes (circuit.h): ReducingGate / ReducingExtensionGate
+// coefficients, CosetInterpolationGate{4, 6} wires
+constexpr uint32_t RED_COEFFS = 43, REDE_COEFFS = 32;
+constexpr uint32_t CI_BITS = 4, CI_POINTS = 16, CI_DEGREE = 6, CI_NINT = (CI_POINTS - 2) / (CI_DEGREE - 1);
+constexpr uint32_t CI_VALUES = 1, CI_EVAL_POINT = CI_VALUES + 2 * CI_POINTS, CI_EVAL_VALUE = CI_EVAL_POINT + 2,
+                   CI_INTER = CI_EVAL_VALUE + 2, CI_SHIFTED = CI_INTER + 4 * CI_NINT;
 // RandomAccessGate{bits 4, copies 4, extra constants 2} wire layout (circuit.h ra_wire_*)
 constexpr uint32_t RA_BITS = 4, RA_VEC = 16, RA_COPIES = 4, RA_EXTRA = 2;
+
+// both writes always happen (a && b would skip the second after a failure)
+__device__ __forceinline__ bool both(bool a, bool b) { return a && b; }
 
 __device__ __forceinline__ bool wset(uint64_t *v, uint32_t s, uint64_t x) {
   const unsigned long long old = atomicCAS((unsigned long long *)(v + s), (unsigned long long)UNSET,
@@ -124,6 +134,83 @@ __device__ bool run_gen(const DevGenD &g, uint64_t *v, const uint32_t *wslot, ui
       const uint32_t *wb = wslot + (uint64_t)g.row * W + (2 + RA_VEC) * RA_COPIES + RA_EXTRA + RA_BITS * c;
       for (uint32_t i = 0; i < RA_BITS; i++) ok &= wset(v, wb[i], (idx >> i) & 1);
       return ok;
+    }
+    case WG_ARITH_EXT:
+    case WG_MUL_EXT: {
+      // ArithmeticExtensionGenerator / MulExtensionGenerator of op s[0]
+      const uint32_t *ws = wslot + (uint64_t)g.row * W;
+      const bool ae = g.kind == WG_ARITH_EXT;
+      const uint32_t o = ae ? 8 * g.s[0] : 6 * g.s[0];
+      const gl::ext m0{rd(v, ws[o], in_ok), rd(v, ws[o + 1], in_ok)};
+      const gl::ext m1{rd(v, ws[o + 2], in_ok), rd(v, ws[o + 3], in_ok)};
+      gl::ext r = gl::ext_scale(gl::ext_mul(m0, m1), g.k0);
+      if (ae) r = gl::ext_add(r, gl::ext_scale(gl::ext{rd(v, ws[o + 4], in_ok), rd(v, ws[o + 5], in_ok)}, g.k1));
+      if (!in_ok) return false;
+      const uint32_t oo = ae ? o + 6 : o + 4;
+      return both(wset(v, ws[oo], r.c0), wset(v, ws[oo + 1], r.c1));
+    }
+    case WG_REDUCING:
+    case WG_REDUCING_EXT: {
+      // ReducingGenerator: acc <- acc alpha + coeff_i, every accumulator written
+      const uint32_t *ws = wslot + (uint64_t)g.row * W;
+      const bool base = g.kind == WG_REDUCING;
+      const uint32_t nc = base ? RED_COEFFS : REDE_COEFFS, cw = base ? 1 : 2;
+      const gl::ext alpha{rd(v, ws[2], in_ok), rd(v, ws[3], in_ok)};
+      gl::ext acc{rd(v, ws[4], in_ok), rd(v, ws[5], in_ok)};
+      bool ok = true;
+      for (uint32_t i = 0; i < nc; i++) {
+        const gl::ext c{rd(v, ws[6 + cw * i], in_ok), base ? 0 : rd(v, ws[7 + 2 * i], in_ok)};
+        acc = gl::ext_add(gl::ext_mul(acc, alpha), c);
+        const uint32_t aw = i + 1 == nc ? 0 : 6 + cw * nc + 2 * i;
+        ok &= both(wset(v, ws[aw], acc.c0), wset(v, ws[aw + 1], acc.c1));
+      }
+      return ok && in_ok;
+    }
+    case WG_POSEIDON_MDS: {
+      // PoseidonMdsGenerator: the MDS layer of each component
+      const uint32_t *ws = wslot + (uint64_t)g.row * W;
+      uint64_t a[12], b[12];
+      for (int i = 0; i < 12; i++) {
+        a[i] = rd(v, ws[2 * i], in_ok);
+        b[i] = rd(v, ws[2 * i + 1], in_ok);
+      }
+      if (!in_ok) return false;
+      ps::mds(a);
+      ps::mds(b);
+      bool ok = true;
+      for (int i = 0; i < 12; i++) ok &= both(wset(v, ws[24 + 2 * i], a[i]), wset(v, ws[25 + 2 * i], b[i]));
+      return ok;
+    }
+    case WG_COSET_INTERP: {
+      // InterpolationGenerator: shifted point, partial barycentric sums per
+      // chunk of the subgroup (intermediate wires), the value
+      const uint32_t *ws = wslot + (uint64_t)g.row * W;
+      const uint64_t shift = rd(v, ws[0], in_ok);
+      gl::ext pt{rd(v, ws[CI_EVAL_POINT], in_ok), rd(v, ws[CI_EVAL_POINT + 1], in_ok)};
+      if (!in_ok || shift == 0) return false;
+      pt = gl::ext_scale(pt, gl::inv(shift));
+      bool ok = both(wset(v, ws[CI_SHIFTED], pt.c0), wset(v, ws[CI_SHIFTED + 1], pt.c1));
+      const uint64_t om = gl::root_of_unity(CI_BITS), ninv = gl::inv(CI_POINTS);
+      gl::ext ev{0, 0}, pr{1, 0};
+      uint32_t lo = 0, hi = CI_DEGREE;
+      uint64_t x = 1;
+      for (uint32_t it = 0;; it++) {
+        for (uint32_t i = lo; i < hi; i++) {
+          const gl::ext term = gl::ext_sub(pt, gl::ext{x, 0});
+          const gl::ext val = gl::ext_scale(gl::ext{rd(v, ws[CI_VALUES + 2 * i], in_ok),
+                                                    rd(v, ws[CI_VALUES + 2 * i + 1], in_ok)}, gl::mul(x, ninv));
+          ev = gl::ext_add(gl::ext_mul(ev, term), gl::ext_mul(val, pr));
+          pr = gl::ext_mul(pr, term);
+          x = gl::mul(x, om);
+        }
+        if (it == CI_NINT) break;
+        ok &= both(wset(v, ws[CI_INTER + 2 * it], ev.c0), wset(v, ws[CI_INTER + 2 * it + 1], ev.c1));
+        ok &= both(wset(v, ws[CI_INTER + 2 * (CI_NINT + it)], pr.c0), wset(v, ws[CI_INTER + 2 * (CI_NINT + it) + 1], pr.c1));
+        lo = 1 + (CI_DEGREE - 1) * (it + 1);
+        hi = lo + CI_DEGREE - 1 < CI_POINTS ? lo + CI_DEGREE - 1 : CI_POINTS;
+      }
+      ok &= both(wset(v, ws[CI_EVAL_VALUE], ev.c0), wset(v, ws[CI_EVAL_VALUE + 1], ev.c1));
+      return ok && in_ok;
     }
     case WG_POSEIDON: {
       // PoseidonGenerator (gates/poseidon.rs), wire layout SURVEY.md A.5

@@ -70,13 +70,19 @@ class AggregatedProof:
 
 
 class _LevelProver:
-    """One aggregation circuit (inner common data, branching) with its device prover."""
+    """One aggregation circuit (inner common data, branching) with its device
+    provers: QP_AGG_PROVERS (default 2) contexts, each with its own HIP stream
+    and workspace, so one prover's host phases (transcript, query assembly)
+    overlap the other's kernels, as the leaf bench's provers do."""
 
     def __init__(self, inner_common: bytes, branching: int, device: int, max_batch: int):
-        self.circuit = Circuit.aggregation(inner_common, branching)
-        self.ctx = Context(device)
+        self.circuit = aggregation_circuit(inner_common, branching)
         self.max_batch = max_batch
-        self.prover = Prover(self.ctx, self.circuit, max_batch=max_batch)
+        nprov = max(1, int(os.environ.get("QP_AGG_PROVERS", "2")))
+        if max_batch == 1:
+            nprov = 1
+        self.provers = [Prover(Context(device), self.circuit, max_batch=max_batch) for _ in range(nprov)]
+        self.prover = self.provers[0]
         vd = self.prover.verifier_data()
         common = self.circuit.common_data()
         assert vd.endswith(common)
@@ -87,15 +93,42 @@ class _LevelProver:
         if os.environ.get("QP_AGG_WITNESS", "device") == "host":
             return self._prove_chunks_host(chunks, inner_vo)
         # device witness generation (qp_prover_prove_aggregation): the host only
-        # deserializes the inner proofs into the circuit's input targets
+        # deserializes the inner proofs into the circuit's input targets; the
+        # chunks are split evenly over the provers, each proving its share in
+        # batches of max_batch on its own stream
         npis = self.circuit.num_public_inputs
-        out = []
+        np_ = min(len(self.provers), len(chunks))
+        per = [len(chunks) // np_ + (1 if i < len(chunks) % np_ else 0) for i in range(np_)]
+        first = [sum(per[:i]) for i in range(np_)]
+        outs = [None] * np_
+        errors = []
+
+        def run(i):
+            try:
+                res = []
+                mine = chunks[first[i]:first[i] + per[i]]
+                for k in range(0, len(mine), self.max_batch):
+                    grp = mine[k:k + self.max_batch]
+                    res += self.provers[i].prove_aggregation(inner_vo, [[p.to_bytes() for p in ch] for ch in grp])
+                outs[i] = res
+            except BaseException as e:  # re-raised on the calling thread
+                errors.append(e)
+
         with self.lock:
-            for i in range(0, len(chunks), self.max_batch):
-                grp = chunks[i:i + self.max_batch]
-                for data in self.prover.prove_aggregation(inner_vo, [[p.to_bytes() for p in ch] for ch in grp]):
-                    pis = struct.unpack_from(f"<{npis}Q", data, len(data) - 8 * npis)
-                    out.append(AggregatedProof(ProofWithPublicInputs(data, pis), self.data))
+            if np_ == 1:
+                run(0)
+            else:
+                th = [threading.Thread(target=run, args=(i,)) for i in range(np_)]
+                for t in th:
+                    t.start()
+                for t in th:
+                    t.join()
+        if errors:
+            raise errors[0]
+        out = []
+        for data in (d for o in outs for d in o):
+            pis = struct.unpack_from(f"<{npis}Q", data, len(data) - 8 * npis)
+            out.append(AggregatedProof(ProofWithPublicInputs(data, pis), self.data))
         return out
 
     def _prove_chunks_host(self, chunks, inner_vo: bytes) -> List[AggregatedProof]:
@@ -118,6 +151,23 @@ class _LevelProver:
                 if f.done() and f.exception() is None:
                     f.result().free()
         return out
+
+
+# the GPU prover's largest circuit: LDS-resident NTTs of n <= 2^14 (prover.cpp setup)
+GPU_MAX_DEGREE_BITS = 14
+
+_circuits = {}
+_circuits_lock = threading.Lock()
+
+
+def aggregation_circuit(inner_common: bytes, branching: int) -> Circuit:
+    """aggregate_chunk's circuit for (inner common data, branching), built once."""
+    key = (bytes(inner_common), branching)
+    with _circuits_lock:
+        c = _circuits.get(key)
+        if c is None:
+            c = _circuits[key] = Circuit.aggregation(inner_common, branching)
+        return c
 
 
 _pool = None
@@ -186,15 +236,43 @@ def aggregate_level(proofs, common_data: bytes, verifier_only: bytes, config: Tr
     return out
 
 
+class CircuitTooLarge(ValueError):
+    """A tree level's aggregation circuit exceeds the GPU prover's size; .proofs
+    holds the level below it (the highest level that could be proven)."""
+
+    def __init__(self, msg, proofs):
+        super().__init__(msg)
+        self.proofs = proofs
+
+
 def aggregate_to_tree(leaf_proofs, common_data: bytes, verifier_only: bytes,
                       config: Optional[TreeAggregationConfig] = None, device: int = 0,
                       backend=None) -> AggregatedProof:
     """tree.rs:55-77: aggregate the first level, then each next level with the
-    previous level's circuit data, down to one root proof."""
+    previous level's circuit data, down to one root proof.  Every leaf's public
+    inputs are registered at every level, so circuits grow with the depth (the
+    root of 2048 leaves registers 32,768 and needs 2^15 rows): a level whose
+    circuit exceeds the GPU prover's 2^14 raises CircuitTooLarge carrying the
+    proofs of the level below (not with a CPU backend)."""
     config = config or TreeAggregationConfig.default()
+
+    def check(inner_common, proofs):
+        if backend is None and len(proofs) >= config.tree_branching_factor:
+            c = aggregation_circuit(inner_common, config.tree_branching_factor)
+            if c.degree_bits > GPU_MAX_DEGREE_BITS:
+                return c.degree_bits
+        return None
+
+    db = check(common_data, leaf_proofs)
+    if db is not None:
+        raise CircuitTooLarge(f"level-1 aggregation circuit is 2^{db} rows", [])
     proofs = aggregate_level(leaf_proofs, common_data, verifier_only, config, device, backend)
     while len(proofs) > 1:
         cd = proofs[0].circuit_data
+        db = check(cd.common, proofs)
+        if db is not None:
+            raise CircuitTooLarge(f"the next level's aggregation circuit is 2^{db} rows (its public inputs: every "
+                                  f"leaf's); the GPU prover proves up to 2^{GPU_MAX_DEGREE_BITS}", proofs)
         proofs = aggregate_level([p.proof for p in proofs], cd.common, cd.verifier_only, config, device, backend)
     assert len(proofs) == 1
     return proofs[0]

@@ -175,8 +175,10 @@ def aggregate_subtrees(local_proofs, common: bytes, verifier_only: bytes, branch
     leaf); rank dst aggregates the roots into the tree root.  Every rank must hold
     branching**k leaves (equal k) and world must be a power of branching
     (check_subtree_shards, before any work).  dist=None: one rank.
-    Returns the root AggregatedProof on dst, None elsewhere; timings (a dict)
-    receives the seconds of the stages: subtree_s, gather_s, top_s."""
+    Returns the root AggregatedProof on dst (or, when the tree's top level
+    needs a circuit beyond the GPU prover, the list of the highest level's
+    proofs, with timings["top_stopped"] saying why), None elsewhere; timings
+    (a dict) receives the seconds of the stages: subtree_s, gather_s, top_s."""
     import time
     from .aggregator import TreeAggregationConfig, aggregate_to_tree
     from .prover import ProofWithPublicInputs
@@ -206,8 +208,16 @@ def aggregate_subtrees(local_proofs, common: bytes, verifier_only: bytes, branch
     if world == 1:
         return sub
     cd = sub.circuit_data
-    root = aggregate_to_tree([ProofWithPublicInputs(r, []) for r in roots], cd.common, cd.verifier_only,
-                             TreeAggregationConfig.new(branching, wdepth), gpu, backend)
+    from .aggregator import CircuitTooLarge
+    try:
+        root = aggregate_to_tree([ProofWithPublicInputs(r, []) for r in roots], cd.common, cd.verifier_only,
+                                 TreeAggregationConfig.new(branching, wdepth), gpu, backend)
+    except CircuitTooLarge as e:
+        # the top of a deep tree (e.g. 2048 leaves: the root registers 32,768
+        # public inputs, 2^15 rows) is beyond the GPU prover: the proofs of the
+        # highest level it could prove are returned instead of the root
+        root = e.proofs
+        tm["top_stopped"] = str(e)
     tm["top_s"] = time.perf_counter() - t2
     return root
 

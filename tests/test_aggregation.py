@@ -46,12 +46,28 @@ def agg_circuit(ref):
 
 
 def test_aggregation_circuit_shape(agg_circuit):
+    """Upstream verify_proof's gate set (plonky2 recursive_verifier.rs /
+    fri/recursive_verifier.rs restated; parity unpinned): extension arithmetic
+    on ArithmeticExtension / MulExtension ops, PoseidonMds layers for the
+    Poseidon gate's in-circuit evaluation, Reducing(Extension) for the alpha
+    reductions, CosetInterpolation for the FRI coset checks, RandomAccess for
+    caps and coset evaluations -- two degree-13 Wormhole proofs fit 2^13 rows."""
+    from qp_wormhole._native import GATE_KINDS, gate_desc
     c = agg_circuit
-    assert c.degree_bits == 14 and 8192 < c.gates_used <= 16384
+    assert c.degree_bits == 13 and 4096 < c.gates_used <= 8192
     assert c.num_public_inputs == 32
+    g = gate_desc(c)
+    kinds = [GATE_KINDS[g.kind[i]] for i in range(g.num_gates)]
+    # CommonCircuitData.gates sorted by (degree, id string)
+    assert kinds == ["noop", "constant", "poseidon_mds", "public_input", "base_sum", "reducing_extension", "reducing",
+                     "arithmetic_extension", "arithmetic", "mul_extension", "random_access", "coset_interpolation",
+                     "poseidon"]
+    # selectors_info: greedy groups with degree + size < quotient_degree_factor + 1
+    assert [g.selector_index[i] for i in range(g.num_gates)] == [0] * 7 + [1] * 4 + [2] * 2
+    assert g.num_constants == 3 + 2 and g.num_gate_constraints == 123
     cb = c.common_data()
-    # gates: Noop, Constant, PublicInput, BaseSum, Arithmetic, RandomAccess{4,4,2}, Poseidon
-    assert cb.count(struct.pack("<I", 13) + struct.pack("<QQQ", 4, 4, 2)) == 1
+    for tag, params in ((13, (4, 4, 2)), (1, (10,)), (8, (13,)), (15, (43,)), (14, (32,)), (4, (4, 6, 16))):
+        assert cb.count(struct.pack("<I", tag) + struct.pack(f"<{len(params)}Q", *params)) == 1
 
 
 def test_reference_proofs_verify_in_circuit(ref, agg_circuit):
@@ -104,7 +120,7 @@ def test_aggregation_proof_verifies_and_level_two(ref):
     assert olib().ora_verify(vd, len(vd), l1.proof.to_bytes(), len(l1.proof.to_bytes())) == 0
     cd = l1.circuit_data
     c2 = qp_wormhole.Circuit.aggregation(cd.common, 2)
-    assert c2.degree_bits == 14
+    assert c2.degree_bits == 13
     w2 = c2.commit_proofs(cd.verifier_only, [l1.proof.to_bytes()] * 2)
     assert check_witness(c2, w2) == -1
     assert len(w2.public_inputs()) == 64

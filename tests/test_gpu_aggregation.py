@@ -2,8 +2,8 @@
 aggregate_chunk / aggregate_to_tree / WormholeProofAggregator
 (wormhole/aggregator/src/circuits/tree.rs:55-143, aggregator.rs:13-92).
 
-Parity: the aggregation circuits' GPU proofs (degree 2^14, generic quotient
-kernel with the RandomAccessGate) are byte-identical to the CPU oracle
+Parity: the aggregation circuits' GPU proofs (upstream verify_proof's gate
+set, degree 2^13, generic quotient kernel) are byte-identical to the CPU oracle
 prover's for the same witness and verify under the oracle verifier.  The
 in-circuit verifier itself is pinned by the reference's own leaf proofs
 (tests/golden/dummy_proof{,_zk}.bin verify inside it).  The aggregation
@@ -37,7 +37,7 @@ def test_aggregate_reference_proofs_gpu_equals_oracle(reference_leaves):
     cb, vo, leaves = reference_leaves
     agg = qp_wormhole.aggregate_chunk(leaves, cb, vo)
     circ = qp_wormhole.Circuit.aggregation(cb, 2)
-    assert circ.degree_bits == 14
+    assert circ.degree_bits == 13
     w = circ.commit_proofs(vo, leaves)
     ob, ovd = oracle_prove(circ, w.wires(), w.public_inputs())
     assert agg.proof.to_bytes() == ob

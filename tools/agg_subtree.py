@@ -1,0 +1,66 @@
+"""Per-GPU subtree aggregation timing (configs[3]'s per-GPU share; development
+tool): `leaves` leaf proofs (the reference's own two, alternating) -> one root
+through aggregate_to_tree (branching 2), one untimed pass that builds and
+caches the level circuits, then `reps` timed passes with per-level seconds and
+the device stage times of the level provers.  Variants come from the
+environment (QP_AGG_PROVERS, QP_AGG_WITNESS, QPGPU_QUOTIENT, QPGPU_LDE_MTW).
+python tools/agg_subtree.py [leaves] [reps]"""
+import json
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path[:0] = [os.path.join(ROOT, "qp-zk-circuits-rm_amd"), os.path.join(ROOT, "tests")]
+
+
+def main():
+    import qp_wormhole
+    from qp_wormhole import aggregator as A
+    from current_circuit_vd import current_circuit_verifier_data
+    from oracle_lib import golden, lib as olib
+    from test_oracle_golden import current_common_bytes
+    nl = int(sys.argv[1]) if len(sys.argv) > 1 else 256
+    reps = int(sys.argv[2]) if len(sys.argv) > 2 else 2
+    cb = current_common_bytes()
+    vd = current_circuit_verifier_data(cb)[0]
+    vo = vd[:len(vd) - len(cb)]
+    fx = [golden("dummy_proof.bin"), golden("dummy_proof_zk.bin")]
+    leaves = [fx[i % 2] for i in range(nl)]
+    depth = nl.bit_length() - 1
+    cfg = A.TreeAggregationConfig.new(2, depth)
+    levels = []
+    orig = A.aggregate_level
+
+    def timed_level(proofs, *a, **k):
+        t = time.perf_counter()
+        r = orig(proofs, *a, **k)
+        levels.append((len(proofs) // 2, time.perf_counter() - t))
+        return r
+    A.aggregate_level = timed_level
+    t = time.perf_counter()
+    A.aggregate_to_tree(leaves, cb, vo, cfg)
+    warm = time.perf_counter() - t
+    for lp in A._levels.values():
+        for p in lp.provers:
+            p.stage_times(reset=True)
+    res = []
+    for _ in range(reps):
+        levels.clear()
+        t = time.perf_counter()
+        root = A.aggregate_to_tree(leaves, cb, vo, cfg)
+        res.append({"seconds": time.perf_counter() - t, "levels": [(n, round(s * 1e3, 1)) for n, s in levels]})
+    stages = {}
+    for lp in A._levels.values():
+        for p in lp.provers:
+            for k, v in p.stage_times().items():
+                stages[k] = stages.get(k, 0.0) + v / reps
+    rvd, rp = root.circuit_data.verifier_data(), root.proof.to_bytes()
+    env = {k: os.environ.get(k) for k in ("QP_AGG_PROVERS", "QP_AGG_WITNESS", "QPGPU_QUOTIENT", "QPGPU_LDE_MTW")}
+    print(json.dumps({"leaves": nl, "env": env, "warm_s": round(warm, 2), "runs": res,
+                      "stage_ms_per_run_all_provers": {k: round(v, 1) for k, v in stages.items()},
+                      "root_verified": olib().ora_verify(rvd, len(rvd), rp, len(rp)) == 0}), flush=True)
+
+
+if __name__ == "__main__":
+    main()

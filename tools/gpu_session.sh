@@ -58,6 +58,10 @@ for s in "$@"; do
     test_agg) step pytest_agg 900 python -u -m pytest tests/test_gpu_aggregation.py tests/test_gpu_guards.py -x -v --timeout 400 --timeout-method thread ;;
     test_ref) step pytest_ref 600 python -u -m pytest tests/test_gpu_reference_proof.py tests/test_gpu_prover.py -x -v --timeout 300 --timeout-method thread ;;
     bench5) step bench5 600 python -u bench.py --steps 5 --warmup 1 --cpu-sample 0 ;;
+    agg_ab) step agg_dev2 300 python -u tools/agg_subtree.py 256 2 &&
+            step agg_dev1 300 env QP_AGG_PROVERS=1 python -u tools/agg_subtree.py 256 2 &&
+            step agg_host1 300 env QP_AGG_PROVERS=1 QP_AGG_WITNESS=host python -u tools/agg_subtree.py 256 2 &&
+            step agg_dev2_generic 300 env QPGPU_QUOTIENT=rereads python -u tools/agg_subtree.py 256 2 ;;
     lde_mtw_ab) for r in 1 2; do
              step prof_lde_fac_$r 300 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/prof_lde_fac_$r -o run -- python3 tools/kbench.py 16 3 &&
              export QPGPU_LDE_MTW=1 && step prof_lde_mtw_$r 300 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/prof_lde_mtw_$r -o run -- python3 tools/kbench.py 16 3 && unset QPGPU_LDE_MTW

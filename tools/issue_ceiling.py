@@ -8,7 +8,9 @@ duration of the same counter pass, so no clock assumption; the s_memtime
 kernel's static instruction mix (one permutation = the absorb-loop body) is
 read from its gfx950 assembly; the ceiling is the mix's issue time with every
 instruction at its class cost, plus its hazard s_nops at their measured cost.
-Usage: python tools/issue_ceiling.py gpurun_out/calib_isa out.json"""
+With a counter pass of tools/kbench.py (third argument) the class costs are
+re-priced at the leaf hash's own clock (GRBM_GUI_ACTIVE per dispatch).
+Usage: python tools/issue_ceiling.py gpurun_out/calib_isa out.json [gpurun_out/calib_kb]"""
 import collections
 import csv
 import json
@@ -17,6 +19,8 @@ import re
 import subprocess
 import sys
 import tempfile
+sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
+from libhash import lib_sha16  # noqa: E402
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 CSRC = os.path.join(ROOT, "qp-zk-circuits-rm_amd", "csrc")
@@ -30,7 +34,7 @@ FAST = {"v_add_u32_e32", "v_sub_u32_e32", "v_xor_b32_e32", "v_and_b32_e32", "v_o
         "v_lshrrev_b32_e32", "v_not_b32_e32", "v_subrev_u32_e32"}
 
 
-def class_costs(d):
+def dispatches(d):
     disp = collections.defaultdict(dict)
     for r in csv.DictReader(open(os.path.join(d, "run_counter_collection.csv"))):
         x = disp[r["Dispatch_Id"]]
@@ -38,13 +42,41 @@ def class_costs(d):
         x["grid"] = int(r["Grid_Size"])
         x[r["Counter_Name"]] = x.get(r["Counter_Name"], 0.0) + float(r["Counter_Value"])
         x["ns"] = int(r["End_Timestamp"]) - int(r["Start_Timestamp"])
-    c = {}
+    return disp
+
+
+# GPU clock of a dispatch: GRBM_GUI_ACTIVE counts GPU-clock cycles summed over
+# the 8 XCDs (a saturated 2.2 ms dispatch reads ~18.3 G/s = 8 x 2.28 GHz), so
+# cycles / 8 / duration is the clock the dispatch actually ran at (DVFS)
+XCDS = 8
+
+
+def clock_ghz(x):
+    return x.get("GRBM_GUI_ACTIVE", 0.0) / XCDS / x["ns"] if x.get("GRBM_GUI_ACTIVE") else None
+
+
+def class_costs(d):
+    disp = dispatches(d)
+    c, clk = {}, {}
     for name, kid in IDS.items():
         xs = [x for x in disp.values() if x["k"].split("::")[-1] == kid and x["grid"] == GRID8]
         # ns per VALU wave-instruction per SIMD (1024 SIMDs), best of the dispatches
-        c[name] = min(x["ns"] / (x["SQ_INSTS_VALU"] / 1024) for x in xs)
+        best = min(xs, key=lambda x: x["ns"] / x["SQ_INSTS_VALU"])
+        c[name] = best["ns"] / (best["SQ_INSTS_VALU"] / 1024)
+        clk[name] = clock_ghz(best)
     return {"mad": c["mad"], "fast": (c["add"] + c["mov"]) / 2, "vop3": (c["cndmask"] + c["sub_co"]) / 2,
-            "s_nop": c["mad_nop"] - c["mad"], "measured": c}
+            "s_nop": c["mad_nop"] - c["mad"], "measured": c, "clock_ghz": clk}
+
+
+def leaf_clock(d):
+    """Clock of the k_leaf_hash dispatches (the wires leaf hash: the largest grid)
+    in a counter pass of tools/kbench.py with the same GRBM counters."""
+    xs = [x for x in dispatches(d).values() if x["k"].endswith("k_leaf_hash")]
+    if not xs:
+        return None
+    g = max(x["grid"] for x in xs)
+    ck = [clock_ghz(x) for x in xs if x["grid"] == g and clock_ghz(x)]
+    return sum(ck) / len(ck) if ck else None
 
 
 def static_mix():
@@ -74,13 +106,28 @@ def main():
         by["mad" if c == cost["mad"] else "fast" if c == cost["fast"] else "vop3"] += v
         t += v * c
     t += ops["s_nop"] * cost["s_nop"]
+    # each class cost was measured at its calibration kernel's clock: re-price
+    # it at the leaf hash's own clock (cycles are what an instruction costs;
+    # the clock under DVFS differs between kernels, MI355X_MICROARCH.md)
+    lclk = leaf_clock(sys.argv[3]) if len(sys.argv) > 3 else None
+    t_leaf = None
+    if lclk:
+        ck = cost["clock_ghz"]
+        cyc = {"mad": cost["mad"] * ck["mad"], "fast": (cost["measured"]["add"] * ck["add"] +
+                                                        cost["measured"]["mov"] * ck["mov"]) / 2,
+               "vop3": (cost["measured"]["cndmask"] * ck["cndmask"] + cost["measured"]["sub_co"] * ck["sub_co"]) / 2,
+               "s_nop": cost["measured"]["mad_nop"] * ck["mad_nop"] - cost["mad"] * ck["mad"]}
+        t_leaf = (sum(by[k] * cyc[k] for k in ("mad", "fast", "vop3")) + ops["s_nop"] * cyc["s_nop"]) / lclk
     out = {
         "kernel": "qpk::k_leaf_hash",
+        "lib_sha16": lib_sha16(),
         "class_ns_per_wave_instr_per_simd": cost,
         "static_mix_per_permutation": {"valu": n_valu, "s_nop": ops["s_nop"], "by_class": dict(by),
                                        "top": dict(collections.Counter(valu).most_common(8))},
         "ceiling_ns_per_wave_permutation_per_simd": t,
         "ceiling_wave_instr_per_s": n_valu / (t * 1e-9) * 1024,
+        "leaf_hash_clock_ghz": lclk,
+        "ceiling_at_leaf_clock_wave_instr_per_s": n_valu / (t_leaf * 1e-9) * 1024 if t_leaf else None,
         "sources": {"class costs": "tools/pmc_calib.sh counter pass over tools/isa_chains (8 waves/SIMD)",
                     "mix": "hipcc -S of csrc/merkle.hip (this tree)",
                     "s_nop": "mad+s_nop 0 block minus mad block (same pass)"},

@@ -14,8 +14,11 @@ the GPU.
 Usage: python tools/kernel_summary.py run_kernel_trace.csv out.json [label]"""
 import csv
 import json
+import os
 import sys
 from collections import defaultdict
+sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
+from libhash import lib_sha16  # noqa: E402
 
 MARKER = "spin_kernel"
 
@@ -56,7 +59,7 @@ def main():
         per[n][1] += 1
     window = hi - lo
     total = sum(v[0] for v in per.values())
-    rec = {"source": path, "label": sys.argv[3] if len(sys.argv) > 3 else "", "scope": scope,
+    rec = {"source": path, "label": sys.argv[3] if len(sys.argv) > 3 else "", "scope": scope, "lib_sha16": lib_sha16(),
            "window_ms": window / 1e6, "kernel_ms": total,
            "gpu_busy_frac": union_ms([(a, b) for a, b, _ in sel]) / window,
            "leaf_hash_share": per.get("qpk::k_leaf_hash", [0])[0] / total,

@@ -9,8 +9,11 @@ run a little long.)
 Usage: python tools/pmc_sq_summary.py <pmc_dir> [out.json]"""
 import csv
 import json
+import os
 import sys
 from collections import defaultdict
+sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
+from libhash import lib_sha16  # noqa: E402
 
 PEAK = 1024 * 2.4e9 / 2
 
@@ -32,6 +35,7 @@ def main():
     for (k, g, wg), xs in sorted(groups.items(), key=lambda kv: -sum(x["ms"] for x in kv[1])):
         m = {c: sum(x.get(c, 0) for x in xs) / len(xs) for c in xs[0] if c.startswith("SQ_") or c == "ms"}
         rec = {"kernel": k, "grid_lanes": g, "workgroup": wg, "vgpr": xs[0]["vgpr"], "dispatches": len(xs),
+               "lib_sha16": lib_sha16(),
                "ms": m["ms"]}
         if "SQ_INSTS_VALU" in m:
             rec["valu_per_lane"] = m["SQ_INSTS_VALU"] * 64 / g

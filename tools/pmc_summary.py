@@ -11,8 +11,11 @@ Usage: python tools/pmc_summary.py <fetch_dir> <write_dir> [out.json]
 """
 import csv
 import json
+import os
 import sys
 from collections import defaultdict
+sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
+from libhash import lib_sha16  # noqa: E402
 
 
 def load(d, counter):
@@ -35,6 +38,7 @@ def main():
         fk = sum(f) / len(f) if f else None
         wk = sum(w) / len(w) if w else None
         rec = {"kernel": key[0], "grid_lanes": key[1], "wg": key[2], "launches": max(len(f), len(w)),
+               "lib_sha16": lib_sha16(),
                "fetch_kib": fk, "write_kib": wk,
                "hbm_read_bytes": 2 * fk * 1024 if fk is not None else None,
                "hbm_write_bytes": wk * 1024 if wk is not None else None}
