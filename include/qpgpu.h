@@ -146,6 +146,15 @@ void qp_circuit_free(qp_circuit *c);
  * info[7..8] = witness generators, dependency levels of the device schedule
  * (info must hold 9 words)                                                  */
 int qp_circuit_info(const qp_circuit *c, uint32_t *info);
+/* generator and gate-row census: gens[k] = generators of GenKind k (constant,
+ * arithmetic, Poseidon, BaseSum split, equality, wire split, extension
+ * division, RandomAccess, ArithmeticExtension, MulExtension, Reducing,
+ * ReducingExtension, PoseidonMds, CosetInterpolation: 14 words); rows[k] =
+ * gate rows of kind k (noop, constant, public input, BaseSum, arithmetic,
+ * Poseidon, RandomAccess, ArithmeticExtension, MulExtension, Reducing,
+ * ReducingExtension, PoseidonMds, CosetInterpolation: 13 words; the n rows
+ * of the trace, padding counted as noop).  Test/diagnostic entry point.     */
+int qp_circuit_census(const qp_circuit *c, uint32_t *gens, uint32_t *rows);
 /* CommonCircuitData::to_bytes (plonky2 util/serialization.rs) */
 int qp_circuit_common_data(const qp_circuit *c, uint8_t *out, size_t cap, size_t *len);
 /* preprocessed constants||sigmas values over H, [num_constants+num_routed][n] */

@@ -668,6 +668,10 @@ CircuitData CircuitBuilder::build() {
       for (uint32_t s : cd.input_slots) avail[s] = 0;
       std::vector<uint32_t> lvl(cd.schedule.size());
       uint32_t nlev = 0;
+      // writers per slot (saturating at 2): host-set slots count as one
+      std::vector<uint8_t> nwr(nslots, 0);
+      for (uint32_t s : cd.input_slots) nwr[s] = 1;
+      for (uint32_t s : cd.zk_slots) nwr[s] = 1;
       for (size_t i = 0; i < cd.schedule.size(); i++) {
         const Gen &g = cd.schedule[i];
         std::vector<uint32_t> rd, wr;
@@ -714,26 +718,44 @@ CircuitData CircuitBuilder::build() {
         }
         lvl[i] = l;
         nlev = std::max(nlev, l + 1);
-        for (uint32_t s : wr)
+        for (uint32_t s : wr) {
           if (s) avail[s] = std::min(avail[s], l + 1);
+          if (nwr[s] < 2) nwr[s]++;
+        }
       }
+      // slots with one writer take a plain store on the device; the shared
+      // zero slot and slots written twice keep the compare-and-swap that
+      // detects "set twice with different values" (DEV_MULTI, witness.hip)
+      nwr[0] = 2;
+      if (nslots >= DEV_MULTI) throw std::runtime_error("device witness schedule: too many value slots");
+      auto flag = [&](uint32_t s) { return s < nslots && nwr[s] >= 2 ? s | DEV_MULTI : s; };
+      cd.dev_wslot.resize(cd.wire_slot.size());
+      for (size_t i = 0; i < cd.wire_slot.size(); i++) cd.dev_wslot[i] = flag(cd.wire_slot[i]);
       cd.level_off.assign(nlev + 1, 0);
       for (uint32_t l : lvl) cd.level_off[l + 1]++;
       for (uint32_t l = 0; l < nlev; l++) cd.level_off[l + 1] += cd.level_off[l];
       std::vector<uint32_t> fill(cd.level_off.begin(), cd.level_off.end() - 1);
       cd.dev_gens.resize(cd.schedule.size());
-      for (size_t i = 0; i < cd.schedule.size(); i++) {
+      // within a level, generators of one kind are contiguous (a wave then runs
+      // one switch arm instead of serialising several)
+      std::vector<uint32_t> order(cd.schedule.size());
+      for (size_t i = 0; i < order.size(); i++) order[i] = (uint32_t)i;
+      std::stable_sort(order.begin(), order.end(), [&](uint32_t x, uint32_t y) {
+        return lvl[x] != lvl[y] ? lvl[x] < lvl[y] : cd.schedule[x].kind < cd.schedule[y].kind;
+      });
+      for (size_t k = 0; k < order.size(); k++) {
+        const size_t i = order[k];
         const Gen &g = cd.schedule[i];
         DevGen &d = cd.dev_gens[fill[lvl[i]]++];
         d.kind = g.kind;
         d.row = g.row;
-        for (int j = 0; j < 4; j++) d.s[j] = g.s[j];
+        for (int j = 0; j < 4; j++) d.s[j] = flag(g.s[j]);
         d.k0 = g.k0;
         d.k1 = g.k1;
         if (g.kind == GEN_WIRE_SPLIT) {
           d.s[1] = g.op;  // number of BaseSum gates from `row`
         } else if (g.kind == GEN_EXT_DIV) {
-          d.k0 = g.s[4] | (uint64_t)g.s[5] << 32;  // quotient slots
+          d.k0 = flag(g.s[4]) | (uint64_t)flag(g.s[5]) << 32;  // quotient slots
         } else if (g.kind == GEN_RANDOM_ACCESS || g.kind == GEN_ARITH_EXT || g.kind == GEN_MUL_EXT) {
           d.s[0] = g.op;  // copy / op
         }

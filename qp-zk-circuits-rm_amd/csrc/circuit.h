@@ -151,7 +151,10 @@ struct Gen {
 // workgroup can run one proof's generators level by level (same layout as the
 // device struct in witness.hip).  Kind-specific packing: WIRE_SPLIT s[1] = gate
 // count; EXT_DIV k0 = the two quotient slots (lo | hi << 32); RANDOM_ACCESS
-// s[0] = copy.
+// s[0] = copy.  Slot fields carry DEV_MULTI (below).
+// slot ids in DevGen and CircuitData::dev_wslot carry DEV_MULTI when the slot
+// has more than one writer (or is the shared zero slot)
+constexpr uint32_t DEV_MULTI = 0x80000000u;
 struct DevGen {
   uint32_t kind, row;
   uint32_t s[4];
@@ -195,7 +198,8 @@ struct CircuitData {
   std::vector<uint32_t> zk_slots;
   uint32_t pi_row = 0;
   bool device_witness = true;           // every generator kind has a device form (witness.hip)
-  std::vector<DevGen> dev_gens;         // generators ordered by dependency level
+  std::vector<DevGen> dev_gens;         // generators ordered by dependency level, then kind
+  std::vector<uint32_t> dev_wslot;      // wire_slot with DEV_MULTI flags (device witness)
   std::vector<uint32_t> level_off;      // [levels + 1] offsets into dev_gens
   // commitments (filled by the prover backend at setup)
   F constants_sigmas_cap[64 * 4] = {0};

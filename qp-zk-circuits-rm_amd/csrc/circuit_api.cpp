@@ -231,6 +231,16 @@ int qp_circuit_info(const qp_circuit *c, uint32_t *info) {
   return QP_OK;
 }
 
+int qp_circuit_census(const qp_circuit *c, uint32_t *gens, uint32_t *rows) {
+  if (!c || !gens || !rows) return QP_ERR_ARG;
+  memset(gens, 0, 14 * sizeof(uint32_t));
+  memset(rows, 0, qc::G_NKINDS * sizeof(uint32_t));
+  for (const auto &g : c->cd.schedule)
+    if (g.kind < 14) gens[g.kind]++;
+  for (const auto &r : c->cd.rows) rows[r.kind]++;
+  return QP_OK;
+}
+
 int qp_circuit_common_data(const qp_circuit *c, uint8_t *out, size_t cap, size_t *len) {
   if (!c) return QP_ERR_ARG;
   auto b = c->cd.common_bytes();

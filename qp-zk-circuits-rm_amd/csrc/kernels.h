@@ -47,8 +47,9 @@ struct Twiddles {
   uint64_t *pt_fwd = nullptr, *pt_inv = nullptr;
   // merged first-pass twiddles of k_lde_cosets per (log_n, r), n = 16 T,
   // N = n 2^r: at mtw_off[log_n][r], mtw[(16 s + m) T + t] = w_N^(t (s + 2^r brev4(m)))
-  // (QPGPU_LDE_MTW=1 only: N words per (log_n, r) re-read by every column's
-  // workgroup, which missed L2 -- round-3 PMC: LDE reads 4.8x algorithmic)
+  // (QPGPU_LDE_MODE=0, the default: N words per (log_n, r) re-read by every
+  // column's workgroup -- round-3 PMC: LDE reads 4.8x algorithmic -- yet the
+  // factored modes' extra vector loads cost more, profiles/r04_lde_ab.log)
   uint64_t *mtw = nullptr;
   uint64_t mtw_off[TW_LOG + 1][LDE_MAX_RATE + 1] = {};
   // coset steps of k_lde_cosets per (log_n, r): at utw_off[log_n][r],

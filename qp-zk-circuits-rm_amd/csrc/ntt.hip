@@ -195,7 +195,11 @@ __global__ void __launch_bounds__(512) QP_NTT_OCC k_lde(const uint64_t *__restri
 // before and by the merged w_N^{t(s + B brev4(m))} (N words, 512 KiB at
 // n = 2^13, evicted by the streaming output) after the DFT.
 // The remaining levels run in LDS (ntt_lds_from); output rows in leaf order.
-template <int LOG_T, bool MTW>
+// MODE (QPGPU_LDE_MODE): 0 = MTW (default; measured 548 vs 701 us per
+// 64-column launch for mode 1 at n = 2^13, profiles/r04_lde_ab.log), 1 =
+// factored with both tables re-read per coset, 2 = factored with the coset
+// steps held in registers, 3 = factored with both tables held in registers.
+template <int LOG_T, int MODE>
 __global__ void __launch_bounds__(1 << LOG_T) QP_NTT_OCC k_lde_cosets(const uint64_t *__restrict__ coeffs, uint64_t c_stride,
                                                           uint64_t c_bstride, uint64_t *__restrict__ out,
                                                           uint64_t o_stride, uint64_t o_bstride, uint32_t rate_bits,
@@ -224,6 +228,17 @@ __global__ void __launch_bounds__(1 << LOG_T) QP_NTT_OCC k_lde_cosets(const uint
   // MTW = false: utw = the coset steps w_N^{t+Tm} (mtw argument), p1 = the
   // first pass's twiddles w_n^{t brev4(m)}
   const uint64_t *ut = mtw + t, *p1 = pt + pt_offset(LOG_N) + t;
+  constexpr bool MTW = MODE == 0;
+  // coset-independent tables held in registers (modes 2 and 3)
+  uint64_t hu[16], hp[16];
+  if constexpr (MODE >= 2) {
+#pragma unroll
+    for (int m = 0; m < 16; m++) hu[m] = ut[T * m];
+  }
+  if constexpr (MODE == 3) {
+#pragma unroll
+    for (int m = 0; m < 16; m++) hp[m] = p1[T * m];
+  }
   for (uint32_t s = 0; s < B; s++) {
     uint64_t r[16];
     if constexpr (MTW) {
@@ -239,13 +254,23 @@ __global__ void __launch_bounds__(1 << LOG_T) QP_NTT_OCC k_lde_cosets(const uint
     } else {
       if (s) {
         // a_m w_N^{s(t+Tm)} from coset s - 1's registers
-        a[0] = nt::mul(a[0], ut[0]);
-        nt::mul_rows(a, [&](int m) { return ut[T * m]; });
+        if constexpr (MODE >= 2) {
+          a[0] = nt::mul(a[0], hu[0]);
+          nt::mul_rows(a, [&](int m) { return hu[m]; });
+        } else {
+          a[0] = nt::mul(a[0], ut[0]);
+          nt::mul_rows(a, [&](int m) { return ut[T * m]; });
+        }
       }
 #pragma unroll
       for (int m = 0; m < 16; m++) r[m] = a[m];
       nt::dft16<false>(r);
-      if (t) nt::mul_rows(r, [&](int m) { return p1[T * m]; });
+      if (t) {
+        if constexpr (MODE == 3)
+          nt::mul_rows(r, [&](int m) { return hp[m]; });
+        else
+          nt::mul_rows(r, [&](int m) { return p1[T * m]; });
+      }
     }
 #pragma unroll
     for (int m = 0; m < 16; m++) lds[nt::lp(t) + nt::lp(T * m)] = r[m];
@@ -368,17 +393,21 @@ void lde(const Twiddles &t, const uint64_t *coeffs, uint64_t c_stride, uint64_t 
     }
     const uint32_t T = 1u << (log_n - 4);
     const uint64_t shift_T = gl::pow(shift, T);
-    // QPGPU_LDE_MTW=1: the merged-table form (A/B)
-    static const bool use_mtw = getenv_flag("QPGPU_LDE_MTW");
+    // QPGPU_LDE_MODE=1..3: the factored forms (A/B)
+    static const int mode = [] {
+      const char *v = getenv("QPGPU_LDE_MODE");
+      return v && *v >= '0' && *v <= '3' ? *v - '0' : 0;
+    }();
+#define QP_LDE_LAUNCH(LT, M, TAB)                                                                                   \
+  k_lde_cosets<LT, M><<<g, 1u << LT, lds_bytes, s>>>(coeffs, c_stride, c_bstride, out, o_stride, o_bstride,        \
+                                                     rate_bits, shift, shift_T, TAB, t.pt_fwd, t.ptw)
 #define QP_LDE_COSETS(LT)                                                                                          \
-  if (use_mtw)                                                                                                     \
-    k_lde_cosets<LT, true><<<g, 1u << LT, lds_bytes, s>>>(coeffs, c_stride, c_bstride, out, o_stride, o_bstride,   \
-                                                          rate_bits, shift, shift_T,                               \
-                                                          t.mtw + t.mtw_off[log_n][rate_bits], t.pt_fwd, t.ptw);   \
-  else                                                                                                             \
-    k_lde_cosets<LT, false><<<g, 1u << LT, lds_bytes, s>>>(coeffs, c_stride, c_bstride, out, o_stride, o_bstride,  \
-                                                           rate_bits, shift, shift_T,                              \
-                                                           t.utw + t.utw_off[log_n][rate_bits], t.pt_fwd, t.ptw)
+  switch (mode) {                                                                                                  \
+    case 1: QP_LDE_LAUNCH(LT, 1, t.utw + t.utw_off[log_n][rate_bits]); break;                                      \
+    case 2: QP_LDE_LAUNCH(LT, 2, t.utw + t.utw_off[log_n][rate_bits]); break;                                      \
+    case 3: QP_LDE_LAUNCH(LT, 3, t.utw + t.utw_off[log_n][rate_bits]); break;                                      \
+    default: QP_LDE_LAUNCH(LT, 0, t.mtw + t.mtw_off[log_n][rate_bits]); break;                                     \
+  }
     switch (log_n) {
       case 10: QP_LDE_COSETS(6); break;
       case 11: QP_LDE_COSETS(7); break;
@@ -387,6 +416,7 @@ void lde(const Twiddles &t, const uint64_t *coeffs, uint64_t c_stride, uint64_t 
       default: QP_LDE_COSETS(10); break;
     }
 #undef QP_LDE_COSETS
+#undef QP_LDE_LAUNCH
     return;
   }
   dim3 grid(1u << rate_bits, ncols, nbat);

@@ -403,7 +403,7 @@ int setup(qp_prover *P) {
       TRY(P->wg_gens.alloc(cd.dev_gens.size() * 5));
       TRY(hipMemcpy(P->wg_gens.p, cd.dev_gens.data(), cd.dev_gens.size() * sizeof(qc::DevGen), hipMemcpyHostToDevice));
       TRY(up32(P->wg_lvl, cd.level_off));
-      TRY(up32(P->wg_wslot, cd.wire_slot));
+      TRY(up32(P->wg_wslot, cd.dev_wslot));
       TRY(up32(P->wg_in_slots, cd.input_slots));
       TRY(P->wg_in.alloc((size_t)B * std::max<uint32_t>(P->wg_nin, 1)));
       TRY(P->wg_err.alloc((B + 1) / 2));

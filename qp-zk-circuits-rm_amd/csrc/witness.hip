@@ -43,8 +43,16 @@ constexpr uint32_t RA_BITS = 4, RA_VEC = 16, RA_COPIES = 4, RA_EXTRA = 2;
 // both writes always happen (a && b would skip the second after a failure)
 __device__ __forceinline__ bool both(bool a, bool b) { return a && b; }
 
+// slot ids of the generator records and the wire-slot table carry MULTI when
+// the slot has several writers (circuit.cpp, qc::DEV_MULTI): only those take
+// the compare-and-swap; a single writer stores (a write needs no round trip)
+constexpr uint32_t MULTI = 0x80000000u;
 __device__ __forceinline__ bool wset(uint64_t *v, uint32_t s, uint64_t x) {
-  const unsigned long long old = atomicCAS((unsigned long long *)(v + s), (unsigned long long)UNSET,
+  if (!(s & MULTI)) {
+    v[s] = x;
+    return true;
+  }
+  const unsigned long long old = atomicCAS((unsigned long long *)(v + (s & ~MULTI)), (unsigned long long)UNSET,
                                            (unsigned long long)x);
   return old == UNSET || old == x;
 }
@@ -67,7 +75,7 @@ __global__ void k_witness_inputs(uint64_t *vals, uint64_t v_bstride, const uint3
 // a generator input still UNSET means a scheduling bug or a missing input: the
 // generator fails (reported like a conflict) instead of computing on 2^64-1
 __device__ __forceinline__ uint64_t rd(const uint64_t *v, uint32_t s, bool &ok) {
-  const uint64_t x = v[s];
+  const uint64_t x = v[s & ~MULTI];
   ok &= x != UNSET;
   return x;
 }
@@ -90,7 +98,7 @@ __device__ bool run_gen(const DevGenD &g, uint64_t *v, const uint32_t *wslot, ui
       bool ok = true;
       for (uint32_t l = 0; l < limbs; l++) {
         const uint64_t bit = (sum >> l) & 1;
-        if (zslot && ws[l] == zslot) ok &= bit == 0;
+        if (zslot && (ws[l] & ~MULTI) == zslot) ok &= bit == 0;
         else ok &= wset(v, ws[l], bit);
       }
       return ok;

@@ -200,6 +200,20 @@ class Circuit:
          self.gates_used, self.num_gate_constraints, self.num_generators, self.witness_levels) = list(info)
         self.n = 1 << self.degree_bits
 
+    GEN_KINDS = ("constant", "arithmetic", "poseidon", "base_split", "equality", "wire_split", "ext_div",
+                 "random_access", "arith_ext", "mul_ext", "reducing", "reducing_ext", "poseidon_mds", "coset_interp")
+    GATE_KINDS = ("noop", "constant", "public_input", "base_sum", "arithmetic", "poseidon", "random_access",
+                  "arith_ext", "mul_ext", "reducing", "reducing_ext", "poseidon_mds", "coset_interp")
+
+    def census(self):
+        """({generator kind: count}, {gate kind: rows}) of the built circuit
+        (qp_circuit_census; all n rows, padding counted as noop)."""
+        g, r = (ctypes.c_uint32 * 14)(), (ctypes.c_uint32 * 13)()
+        rc = lib().qp_circuit_census(self.h, g, r)
+        if rc:
+            raise QpError(rc, "qp_circuit_census")
+        return dict(zip(self.GEN_KINDS, g)), dict(zip(self.GATE_KINDS, r))
+
     @classmethod
     def wormhole(cls, zero_knowledge=False):
         h = ctypes.c_void_p()

@@ -30,6 +30,28 @@ def check_witness(circ, w):
     return L.ora_check_witness(cb, len(cb), circ.constants_sigmas(), w.wires(), pis, len(pis))
 
 
+def check_census(circ):
+    """The generator schedule against the trace (qp_circuit_census): one
+    generator per row of the single-generator gates (Poseidon, PoseidonMds,
+    Reducing(Extension), CosetInterpolation, Constant, BaseSum), one per used op
+    of the multi-op gates (at most num_ops per row, at least one per row: an
+    extension op is ONE ArithmeticExtension / MulExtension generator, not the
+    ~4 base-field ops of a base-arithmetic recursive verifier, hence ~16k
+    generators for 8k rows), four per RandomAccess row, and their total is the
+    schedule the device witness runs (info word 7)."""
+    g, r = circ.census()
+    assert sum(g.values()) == circ.num_generators and sum(r.values()) == circ.n
+    for gk, rk in (("poseidon", "poseidon"), ("poseidon_mds", "poseidon_mds"), ("reducing", "reducing"),
+                   ("reducing_ext", "reducing_ext"), ("coset_interp", "coset_interp"), ("constant", "constant"),
+                   ("base_split", "base_sum")):
+        assert g[gk] == r[rk], (gk, g[gk], r[rk])
+    for gk, ops in (("arithmetic", 20), ("arith_ext", 10), ("mul_ext", 13)):
+        assert r[gk] <= g[gk] <= ops * r[gk], (gk, g[gk], r[gk])
+    assert g["random_access"] == 4 * r["random_access"]
+    assert r["public_input"] == 1 and g["equality"] == 0
+    return g, r
+
+
 @pytest.fixture(scope="module")
 def ref():
     from current_circuit_vd import current_circuit_verifier_data
@@ -65,6 +87,12 @@ def test_aggregation_circuit_shape(agg_circuit):
     # selectors_info: greedy groups with degree + size < quotient_degree_factor + 1
     assert [g.selector_index[i] for i in range(g.num_gates)] == [0] * 7 + [1] * 4 + [2] * 2
     assert g.num_constants == 3 + 2 and g.num_gate_constraints == 123
+    gens, rows = check_census(c)
+    # the recursive verifier's every gate kind is present, and its extension
+    # arithmetic runs on the extension gates
+    assert all(rows[k] > 0 for k in ("random_access", "arith_ext", "mul_ext", "reducing", "reducing_ext",
+                                     "poseidon_mds", "coset_interp"))
+    assert gens["arith_ext"] + gens["mul_ext"] > gens["arithmetic"]
     cb = c.common_data()
     for tag, params in ((13, (4, 4, 2)), (1, (10,)), (8, (13,)), (15, (43,)), (14, (32,)), (4, (4, 6, 16))):
         assert cb.count(struct.pack("<I", tag) + struct.pack(f"<{len(params)}Q", *params)) == 1

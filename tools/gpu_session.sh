@@ -62,10 +62,16 @@ for s in "$@"; do
             step agg_dev1 300 env QP_AGG_PROVERS=1 python -u tools/agg_subtree.py 256 2 &&
             step agg_host1 300 env QP_AGG_PROVERS=1 QP_AGG_WITNESS=host python -u tools/agg_subtree.py 256 2 &&
             step agg_dev2_generic 300 env QPGPU_QUOTIENT=rereads python -u tools/agg_subtree.py 256 2 ;;
-    lde_mtw_ab) for r in 1 2; do
-             step prof_lde_fac_$r 300 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/prof_lde_fac_$r -o run -- python3 tools/kbench.py 16 3 &&
-             export QPGPU_LDE_MTW=1 && step prof_lde_mtw_$r 300 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/prof_lde_mtw_$r -o run -- python3 tools/kbench.py 16 3 && unset QPGPU_LDE_MTW
-           done ;;
+    lde_modes) for r in 1 2; do for m in 0 1 2 3; do
+             step prof_lde_m${m}_$r 300 env QPGPU_LDE_MODE=$m rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/prof_lde_m${m}_$r -o run -- python3 tools/kbench.py 16 3 || exit 1
+           done; done ;;
+    lde_pmc) for m in 0 3; do
+             export QPGPU_LDE_MODE=$m
+             step pmc_lde_fetch_m$m 120 rocprofv3 --pmc FETCH_SIZE --output-format csv -d gpurun_out/pmc_lde_fetch_m$m -o run -- python3 tools/kbench.py 16 1 &&
+             step pmc_lde_sq_m$m 120 rocprofv3 --pmc SQ_WAVES SQ_INSTS_VALU SQ_ACTIVE_INST_VALU SQ_WAVE_CYCLES SQ_WAIT_INST_ANY SQ_INSTS_VMEM_RD SQ_BUSY_CYCLES SQ_WAIT_ANY --output-format csv -d gpurun_out/pmc_lde_sq_m$m -o run -- python3 tools/kbench.py 16 1 || exit 1
+           done; unset QPGPU_LDE_MODE ;;
+    aggprof) step prof_agg 300 env QP_AGG_PROVERS=1 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/prof_agg -o run -- python3 tools/agg_subtree.py 256 1 ;;
+    aggpmc) step pmc_agg_wit 300 env QP_AGG_PROVERS=1 rocprofv3 --pmc SQ_WAVES SQ_INSTS_VALU SQ_WAVE_CYCLES SQ_WAIT_INST_ANY SQ_INSTS_VMEM_RD SQ_INSTS_VMEM_WR SQ_ACTIVE_INST_VALU SQ_INSTS_SALU --kernel-include-regex k_witness_gen --output-format csv -d gpurun_out/pmc_agg_wit -o run -- python3 tools/agg_subtree.py 256 1 ;;
     *) echo "unknown step $s" ;;
   esac
 done
