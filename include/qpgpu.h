@@ -153,8 +153,10 @@ int qp_circuit_info(const qp_circuit *c, uint32_t *info);
  * gate rows of kind k (noop, constant, public input, BaseSum, arithmetic,
  * Poseidon, RandomAccess, ArithmeticExtension, MulExtension, Reducing,
  * ReducingExtension, PoseidonMds, CosetInterpolation: 13 words; the n rows
- * of the trace, padding counted as noop).  Test/diagnostic entry point.     */
-int qp_circuit_census(const qp_circuit *c, uint32_t *gens, uint32_t *rows);
+ * of the trace, padding counted as noop); level_gens (may be null; 14 words
+ * per device-witness level, info word 8 levels) = the generators of each
+ * dependency level by kind.  Test/diagnostic entry point.                   */
+int qp_circuit_census(const qp_circuit *c, uint32_t *gens, uint32_t *rows, uint32_t *level_gens);
 /* CommonCircuitData::to_bytes (plonky2 util/serialization.rs) */
 int qp_circuit_common_data(const qp_circuit *c, uint8_t *out, size_t cap, size_t *len);
 /* preprocessed constants||sigmas values over H, [num_constants+num_routed][n] */

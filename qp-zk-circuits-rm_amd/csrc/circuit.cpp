@@ -760,6 +760,19 @@ CircuitData CircuitBuilder::build() {
           d.s[0] = g.op;  // copy / op
         }
       }
+      // each level's Poseidon generators are contiguous (kind order): their
+      // range lets the device pick the cooperative form for narrow levels
+      cd.level_pos.assign(2 * (size_t)nlev, 0);
+      for (uint32_t l = 0; l < nlev; l++) {
+        uint32_t first = cd.level_off[l + 1], cnt = 0;
+        for (uint32_t i = cd.level_off[l]; i < cd.level_off[l + 1]; i++)
+          if (cd.dev_gens[i].kind == GEN_POSEIDON) {
+            first = std::min(first, i);
+            cnt++;
+          }
+        cd.level_pos[2 * l] = first;
+        cd.level_pos[2 * l + 1] = cnt;
+      }
     }
   }
   return cd;

@@ -201,6 +201,7 @@ struct CircuitData {
   std::vector<DevGen> dev_gens;         // generators ordered by dependency level, then kind
   std::vector<uint32_t> dev_wslot;      // wire_slot with DEV_MULTI flags (device witness)
   std::vector<uint32_t> level_off;      // [levels + 1] offsets into dev_gens
+  std::vector<uint32_t> level_pos;      // [levels][2]: first Poseidon generator of the level, count
   // commitments (filled by the prover backend at setup)
   F constants_sigmas_cap[64 * 4] = {0};
   F circuit_digest[4] = {0};

@@ -231,8 +231,17 @@ int qp_circuit_info(const qp_circuit *c, uint32_t *info) {
   return QP_OK;
 }
 
-int qp_circuit_census(const qp_circuit *c, uint32_t *gens, uint32_t *rows) {
+int qp_circuit_census(const qp_circuit *c, uint32_t *gens, uint32_t *rows, uint32_t *level_gens) {
   if (!c || !gens || !rows) return QP_ERR_ARG;
+  if (level_gens) {
+    const auto &lo = c->cd.level_off;
+    for (size_t l = 0; l + 1 < lo.size(); l++) {
+      uint32_t *o = level_gens + 14 * l;
+      memset(o, 0, 14 * sizeof(uint32_t));
+      for (uint32_t i = lo[l]; i < lo[l + 1]; i++)
+        if (c->cd.dev_gens[i].kind < 14) o[c->cd.dev_gens[i].kind]++;
+    }
+  }
   memset(gens, 0, 14 * sizeof(uint32_t));
   memset(rows, 0, qc::G_NKINDS * sizeof(uint32_t));
   for (const auto &g : c->cd.schedule)

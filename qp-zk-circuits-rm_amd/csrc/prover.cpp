@@ -124,7 +124,7 @@ struct qp_prover {
     double pend_units = 0;
   } kt[8];
   // device witness generation (witness.hip): schedule + per-proof slot values
-  DevBuf wg_gens, wg_lvl, wg_wslot, wg_wslot_cm, wg_in_slots, wg_pi_slots, wg_vals, wg_in, wg_err, wg_pis;
+  DevBuf wg_gens, wg_lvl, wg_lpos, wg_wslot, wg_wslot_cm, wg_in_slots, wg_pi_slots, wg_vals, wg_in, wg_err, wg_pis;
   uint32_t wg_nslots = 0, wg_nin = 0, wg_nlev = 0;
   bool quotient_rereads = false;
   bool quotient_fused = false;  // A/B: QPGPU_QUOTIENT=fused selects k_quotient_fused where it applies
@@ -403,6 +403,7 @@ int setup(qp_prover *P) {
       TRY(P->wg_gens.alloc(cd.dev_gens.size() * 5));
       TRY(hipMemcpy(P->wg_gens.p, cd.dev_gens.data(), cd.dev_gens.size() * sizeof(qc::DevGen), hipMemcpyHostToDevice));
       TRY(up32(P->wg_lvl, cd.level_off));
+      TRY(up32(P->wg_lpos, cd.level_pos));
       TRY(up32(P->wg_wslot, cd.dev_wslot));
       TRY(up32(P->wg_in_slots, cd.input_slots));
       TRY(P->wg_in.alloc((size_t)B * std::max<uint32_t>(P->wg_nin, 1)));
@@ -512,7 +513,7 @@ int check_tables(qp_prover *P, int which, bool wires_on_device) {
       need.push_back({"fri.coeffs", l < P->fcoef.size() ? P->fcoef[l].p : nullptr});
     }
   } else {
-    need = {{"wg_gens", P->wg_gens.p}, {"wg_lvl", P->wg_lvl.p}, {"wg_wslot", P->wg_wslot.p},
+    need = {{"wg_gens", P->wg_gens.p}, {"wg_lvl", P->wg_lvl.p}, {"wg_lpos", P->wg_lpos.p}, {"wg_wslot", P->wg_wslot.p},
             {"wg_wslot_cm", P->wg_wslot_cm.p}, {"wg_pi_slots", P->wg_pi_slots.p}, {"wg_vals", P->wg_vals.p},
             {"wg_pis", P->wg_pis.p}, {"wg_err", P->wg_err.p}, {"h_in", P->h_in}};
     if (P->wg_nin) {
@@ -1002,6 +1003,7 @@ int gen_witness_batch(qp_prover *P, uint32_t nb) {
   a.v_bstride = P->wg_nslots;
   a.gens = P->wg_gens.p;
   a.level_off = (const uint32_t *)P->wg_lvl.p;
+  a.level_pos = (const uint32_t *)P->wg_lpos.p;
   a.nlevels = P->wg_nlev;
   a.wslot = (const uint32_t *)P->wg_wslot.p;
   a.W = P->W;
@@ -1009,7 +1011,25 @@ int gen_witness_batch(qp_prover *P, uint32_t nb) {
   a.zero_slot = P->circuit->cd.zero_const_slot;
   a.num_consts = P->circuit->cd.config.num_constants;
   a.err = (uint32_t *)P->wg_err.p;
-  qpk::k_witness_gen<<<nb, 256, 0, s>>>(a);
+  // QPGPU_WIT_THREADS: workgroup size of the witness kernel (one workgroup
+  // per proof; 256 or 512)
+  static const unsigned wthreads = [] {
+    const char *e = getenv("QPGPU_WIT_THREADS");
+    return e && !strcmp(e, "512") ? 512u : 256u;
+  }();
+  // QPGPU_WIT_COOP: Poseidon count up to which a level runs its Poseidon
+  // generators one per wave (12 lanes cooperating on one permutation) instead
+  // of one per lane; default 4 per wave, 0 disables
+  static const uint32_t coop_per_wave = [] {
+    const char *e = getenv("QPGPU_WIT_COOP");
+    return e ? (uint32_t)atoi(e) : 4u;
+  }();
+  a.coop_max = coop_per_wave * (wthreads / 64);
+  qpk::k_witness_gen<<<nb, wthreads, 0, s>>>(a);
+  // QPGPU_WIT_TWICE=1 (diagnostic): a second pass over the same values (every
+  // write repeats the value already there), to time the kernel with warm caches
+  static const bool twice = getenv("QPGPU_WIT_TWICE") && !strcmp(getenv("QPGPU_WIT_TWICE"), "1");
+  if (twice) qpk::k_witness_gen<<<nb, wthreads, 0, s>>>(a);
   qpk::k_witness_expand<<<dim3((unsigned)std::min<uint64_t>(cdiv(nw, 256), 1024), nb), 256, 0, s>>>(
       P->wg_vals.p, P->wg_nslots, (const uint32_t *)P->wg_wslot_cm.p, nw, P->wires.vals.p, P->wires.cbs(),
       (const uint32_t *)P->wg_pi_slots.p, P->npis, P->wg_pis.p);

@@ -17,6 +17,7 @@
 #include <hip/hip_runtime.h>
 #include "field.h"
 #include "poseidon.h"
+#include "poseidon_dev.h"
 #include "witness_kernels.h"
 
 namespace qpk {
@@ -80,7 +81,279 @@ __device__ __forceinline__ uint64_t rd(const uint64_t *v, uint32_t s, bool &ok) 
   return x;
 }
 
-__device__ bool run_gen(const DevGenD &g, uint64_t *v, const uint32_t *wslot, uint32_t W, uint32_t limbs,
+// PoseidonGenerator on the throughput permutation (poseidon_fast.h: round
+// constants as literal operands, sparse partial rounds whose lane 0 before
+// each S-box is the plain form's S-box input): the gate's wires are written
+// as the rounds reach them.  State values are non-canonical in [0, 2^64)
+// between rounds; every written value is canonicalised.  The slot ids of a
+// phase's writes are loaded one phase ahead, so their latency hides behind
+// the rounds (a lookup per write would stall the lane on every store).
+__device__ __noinline__ bool wset_multi(uint64_t *v, uint32_t s, uint64_t x) { return wset(v, s, x); }
+__device__ __forceinline__ void wput(uint64_t *v, uint32_t s, uint64_t x, bool &ok) {
+  x = psd::canon(x);
+  if (!(s & MULTI)) v[s] = x;
+  else ok &= wset_multi(v, s, x);
+}
+template <int N>
+__device__ __forceinline__ void slots_load(uint32_t (&sl)[N], const uint32_t *ws, uint32_t j0) {
+#pragma unroll
+  for (int i = 0; i < N; i++) sl[i] = ws[j0 + i];
+}
+struct WitPartialHook {
+  uint64_t *v;
+  const uint32_t *sl;  // the 22 partial-round slots
+  bool &ok;
+  __device__ __forceinline__ uint64_t operator()(int T, uint64_t s0) const {
+    wput(v, sl[T], s0, ok);
+    return s0;
+  }
+};
+template <int T>
+__device__ __forceinline__ void wit_partial(uint64_t *v, const uint32_t (&sl)[22], bool &ok, uint64_t s[12]) {
+  if constexpr (T < 22) {
+    constexpr int G = (22 - T) < QP_PF_GROUP ? (22 - T) : QP_PF_GROUP;
+    if constexpr (G > 1) {
+      pf::partial_group<T, G>(s, WitPartialHook{v, sl, ok});
+    } else {
+      wput(v, sl[T], s[0], ok);
+      pf::partial_sparse<T>(s);
+    }
+    wit_partial<T + G>(v, sl, ok, s);
+  }
+}
+// rolled form (QP_WIT_POSEIDON=2): every round a loop iteration with the
+// round constants from memory, plain partial rounds (full MDS): a few
+// thousand instructions of code instead of the unrolled form's ~280 KB
+__device__ __noinline__ bool poseidon_witness_rolled(uint64_t *v, const uint32_t *__restrict__ ws) {
+  bool in_ok = true, ok = true;
+  uint64_t s[12];
+  for (int i = 0; i < 12; i++) s[i] = rd(v, ws[i], in_ok);
+  const uint64_t swap = rd(v, ws[24], in_ok);
+  if (!in_ok) return false;
+  for (int i = 0; i < 4; i++) wput(v, ws[25 + i], gl::mul(swap, gl::sub(s[i + 4], s[i])), ok);
+  if (swap == 1)
+    for (int i = 0; i < 4; i++) {
+      const uint64_t t = s[i];
+      s[i] = s[i + 4];
+      s[i + 4] = t;
+    }
+#pragma unroll
+  for (int i = 0; i < 12; i++) s[i] = pf::add_c(s[i], ps::rc_cx(i));
+  uint32_t sl[12];
+#pragma unroll 1
+  for (int r = 0; r < 4; r++) {
+    if (r) {
+#pragma unroll
+      for (int i = 0; i < 12; i++) wput(v, sl[i], s[i], ok);
+    }
+    slots_load(sl, ws, r < 3 ? 29 + 12 * r : 65);
+    pf::full_round_dyn(s, ps::RC_DEV + (r + 1) * 12);
+  }
+#pragma unroll 1
+  for (int r = 0; r < 22; r++) {
+    const uint32_t nx = ws[r < 21 ? 66 + r : 87];
+    wput(v, sl[0], s[0], ok);
+    sl[0] = nx;
+    s[0] = pf::sbox(s[0]);
+    uint32_t lo[12], hi[12];
+#pragma unroll
+    for (int i = 0; i < 12; i++) {
+      lo[i] = pf::lo32(s[i]);
+      hi[i] = pf::hi32(s[i]);
+    }
+    pf::mds_rows_block_dyn<0>(s, lo, hi, ps::RC_DEV + (r + 5) * 12);
+  }
+  slots_load(sl, ws, 87);
+#pragma unroll 1
+  for (int r = 0; r < 3; r++) {
+#pragma unroll
+    for (int i = 0; i < 12; i++) wput(v, sl[i], s[i], ok);
+    slots_load(sl, ws, 99 + 12 * r);
+    pf::full_round_dyn(s, ps::RC_DEV + (r + 27) * 12);
+  }
+#pragma unroll
+  for (int i = 0; i < 12; i++) wput(v, sl[i], s[i], ok);
+  slots_load(sl, ws, 12);
+  pf::sbox12(s);
+  pf::mds<3, -1>(s);
+#pragma unroll
+  for (int i = 0; i < 12; i++) wput(v, sl[i], s[i], ok);
+  return ok;
+}
+
+__device__ __noinline__ bool poseidon_witness(uint64_t *v, const uint32_t *__restrict__ ws) {
+  bool in_ok = true, ok = true;
+  uint64_t s[12];
+  uint32_t sd[4], sa[12], sb[12];
+  for (int i = 0; i < 12; i++) s[i] = rd(v, ws[i], in_ok);
+  const uint64_t swap = rd(v, ws[24], in_ok);
+  slots_load(sd, ws, 25);
+  slots_load(sa, ws, 29);
+  if (!in_ok) return false;
+#pragma unroll
+  for (int i = 0; i < 4; i++) wput(v, sd[i], gl::mul(swap, gl::sub(s[i + 4], s[i])), ok);
+  if (swap == 1)
+    for (int i = 0; i < 4; i++) {
+      const uint64_t t = s[i];
+      s[i] = s[i + 4];
+      s[i + 4] = t;
+    }
+#pragma unroll
+  for (int i = 0; i < 12; i++) s[i] = pf::add_c(s[i], ps::rc_cx(i));
+  // first full rounds: the state entering rounds 1..3 (after their constants)
+  pf::sbox12(s);
+  pf::mds<3, 1>(s);
+  slots_load(sb, ws, 41);
+#pragma unroll
+  for (int i = 0; i < 12; i++) wput(v, sa[i], s[i], ok);
+  pf::sbox12(s);
+  pf::mds<3, 2>(s);
+  slots_load(sa, ws, 53);
+#pragma unroll
+  for (int i = 0; i < 12; i++) wput(v, sb[i], s[i], ok);
+  pf::sbox12(s);
+  pf::mds<3, 3>(s);
+  uint32_t sp[22];
+  slots_load(sp, ws, 65);
+#pragma unroll
+  for (int i = 0; i < 12; i++) wput(v, sa[i], s[i], ok);
+  pf::sbox12(s);
+  pf::mds_init_sparse(s);
+  slots_load(sa, ws, 87);
+  wit_partial<0>(v, sp, ok, s);
+  // second full rounds: the state entering rounds 26..29, then the output
+#pragma unroll
+  for (int r = 0; r < 4; r++) {
+    slots_load(sb, ws, r < 3 ? 99 + 12 * r : 12);
+#pragma unroll
+    for (int i = 0; i < 12; i++) wput(v, sa[i], s[i], ok);
+    pf::sbox12(s);
+    if (r == 0) pf::mds<3, 27>(s);
+    else if (r == 1) pf::mds<3, 28>(s);
+    else if (r == 2) pf::mds<3, 29>(s);
+    else pf::mds<3, -1>(s);
+#pragma unroll
+    for (int i = 0; i < 12; i++) sa[i] = sb[i];
+  }
+#pragma unroll
+  for (int i = 0; i < 12; i++) wput(v, sa[i], s[i], ok);
+  return ok;
+}
+
+// Cooperative PoseidonGenerator: one wave, lane i < 12 holding state element
+// i, for the narrow levels of the schedule (the transcript sponges and the
+// public-input hash are chains of single permutations, one level each).  Per
+// round: constant add and S-box lane-parallel, then the MDS row of lane r from
+// the 12 S-box outputs broadcast through v_readlane (24 SGPR values) times
+// the lane's own circulant coefficients, four accumulators of 6 products.
+// The dependent chain of a round is one S-box plus six products (the
+// one-lane form runs all 12 S-boxes and 12 MDS rows in sequence).  All 64
+// lanes must be active; lanes >= 12 compute and never write.
+__device__ __forceinline__ uint64_t wave_mds_row(uint64_t y, const uint32_t (&coef)[12]) {
+  const uint32_t lo = (uint32_t)y, hi = (uint32_t)(y >> 32);
+  uint64_t al[2] = {0, 0}, ah[2] = {0, 0};
+#pragma unroll
+  for (int j = 0; j < 12; j++) {
+    const uint32_t xl = __builtin_amdgcn_readlane(lo, j), xh = __builtin_amdgcn_readlane(hi, j);
+    al[j & 1] += (uint64_t)xl * coef[j];
+    ah[j & 1] += (uint64_t)xh * coef[j];
+  }
+  return pf::reduce_row(al[0] + al[1], ah[0] + ah[1]);
+}
+__device__ __noinline__ bool poseidon_coop(uint64_t *v, const uint32_t *__restrict__ ws) {
+  const uint32_t lane = threadIdx.x & 63;
+  const bool act = lane < 12;
+  const uint32_t i = act ? lane : 0;
+  // MDS row i: coefficient of element j = CIRC[(j - i) mod 12] (+ 8 on the diagonal of row 0)
+  uint32_t coef[12];
+#pragma unroll
+  for (int j = 0; j < 12; j++) coef[j] = ps::mds_circ((j - (int)i + 12) % 12) + (i == 0 && j == 0 ? 8u : 0u);
+  bool in_ok = true, ok = true;
+  const uint32_t partner = i < 4 ? i + 4 : i < 8 ? i - 4 : i;
+  const uint64_t a = rd(v, ws[i], in_ok), b = rd(v, ws[partner], in_ok);
+  const uint64_t swap = rd(v, ws[24], in_ok);
+  uint32_t sl = ws[act ? 29 + i : 29];
+  if (!__all(in_ok)) return false;
+  if (act && i < 4) wput(v, ws[25 + i], gl::mul(swap, gl::sub(b, a)), ok);
+  uint64_t x = swap == 1 && i < 8 ? b : a;
+  x = pf::add_c(x, ps::RC_DEV[i]);
+  // rounds 0..3: the state entering rounds 1..3 (after their constants) is written
+#pragma unroll 1
+  for (int r = 0; r < 4; r++) {
+    if (r && act) wput(v, sl, x, ok);
+    sl = ws[act ? (r < 3 ? 29 + 12 * r + i : 65) : 29];
+    const uint64_t rc = ps::RC_DEV[(r + 1) * 12 + i];
+    x = pf::add_c(wave_mds_row(pf::sbox(x), coef), rc);
+  }
+  // partial rounds 4..25: lane 0's S-box input is the wire
+#pragma unroll 1
+  for (int r = 4; r < 26; r++) {
+    if (lane == 0) wput(v, sl, x, ok);
+    sl = ws[lane == 0 ? (r < 25 ? 66 + (r - 4) : 87) : (act ? 87 + i : 87)];
+    const uint64_t rc = ps::RC_DEV[(r + 1) * 12 + i];
+    const uint64_t y = pf::sbox(x);
+    x = pf::add_c(wave_mds_row(lane == 0 ? y : x, coef), rc);
+  }
+  if (act) sl = ws[87 + i];
+  // rounds 26..29: the state entering each is written, then the output
+#pragma unroll 1
+  for (int r = 26; r < 30; r++) {
+    if (act) wput(v, sl, x, ok);
+    sl = ws[act ? (r < 29 ? 87 + 12 * (r - 25) + i : 12 + i) : 12];
+    x = wave_mds_row(pf::sbox(x), coef);
+    if (r < 29) x = pf::add_c(x, ps::RC_DEV[(r + 1) * 12 + i]);
+  }
+  if (act) wput(v, sl, x, ok);
+  return ok;
+}
+
+// the first form (ps:: plain rounds, a lookup per write), QP_WIT_POSEIDON=0
+__device__ __noinline__ bool poseidon_witness_plain(const DevGenD &g, uint64_t *v, const uint32_t *wslot, uint32_t W) {
+  const uint32_t *ws = wslot + (uint64_t)g.row * W;
+  bool in_ok = true;
+  uint64_t s[12];
+  for (int i = 0; i < 12; i++) s[i] = rd(v, ws[i], in_ok);
+  const uint64_t swap = rd(v, ws[24], in_ok);
+  if (!in_ok) return false;
+  bool ok = true;
+  for (int i = 0; i < 4; i++) ok &= wset(v, ws[25 + i], gl::mul(swap, gl::sub(s[i + 4], s[i])));
+  if (swap == 1)
+    for (int i = 0; i < 4; i++) {
+      const uint64_t t = s[i];
+      s[i] = s[i + 4];
+      s[i + 4] = t;
+    }
+  int rc = 0;
+  for (int r = 0; r < 4; r++, rc++) {
+    for (int i = 0; i < 12; i++) s[i] = gl::add(s[i], ps::rc(rc * 12 + i));
+    if (r)
+      for (int i = 0; i < 12; i++) ok &= wset(v, ws[29 + (r - 1) * 12 + i], s[i]);
+    for (int i = 0; i < 12; i++) s[i] = ps::sbox(s[i]);
+    ps::mds(s);
+  }
+  for (int r = 0; r < 22; r++, rc++) {
+    for (int i = 0; i < 12; i++) s[i] = gl::add(s[i], ps::rc(rc * 12 + i));
+    ok &= wset(v, ws[65 + r], s[0]);
+    s[0] = ps::sbox(s[0]);
+    ps::mds(s);
+  }
+  for (int r = 0; r < 4; r++, rc++) {
+    for (int i = 0; i < 12; i++) s[i] = gl::add(s[i], ps::rc(rc * 12 + i));
+    for (int i = 0; i < 12; i++) ok &= wset(v, ws[87 + r * 12 + i], s[i]);
+    for (int i = 0; i < 12; i++) s[i] = ps::sbox(s[i]);
+    ps::mds(s);
+  }
+  for (int i = 0; i < 12; i++) ok &= wset(v, ws[12 + i], s[i]);
+  return ok;
+}
+
+// measured (tools/gpu_session.sh wit_ab, 256-leaf subtree, profiles/r04_wit_ab.log):
+// rolled 0.566 s, unrolled 0.607 s, plain 0.668 s
+#ifndef QP_WIT_POSEIDON
+#define QP_WIT_POSEIDON 2
+#endif
+
+__device__ bool run_gen(const DevGenD &g, uint64_t *__restrict__ v, const uint32_t *__restrict__ wslot, uint32_t W, uint32_t limbs,
                         uint32_t zslot, uint32_t num_consts) {
   bool in_ok = true;
   switch (g.kind) {
@@ -159,18 +432,37 @@ __device__ bool run_gen(const DevGenD &g, uint64_t *v, const uint32_t *wslot, ui
     }
     case WG_REDUCING:
     case WG_REDUCING_EXT: {
-      // ReducingGenerator: acc <- acc alpha + coeff_i, every accumulator written
-      const uint32_t *ws = wslot + (uint64_t)g.row * W;
+      // ReducingGenerator: acc <- acc alpha + coeff_i, every accumulator
+      // written.  Chunks of 8 coefficients: the chunk's slot ids, then its
+      // values, are loaded together (two memory latencies per chunk instead
+      // of two per coefficient)
+      const uint32_t *__restrict__ ws = wslot + (uint64_t)g.row * W;
       const bool base = g.kind == WG_REDUCING;
       const uint32_t nc = base ? RED_COEFFS : REDE_COEFFS, cw = base ? 1 : 2;
       const gl::ext alpha{rd(v, ws[2], in_ok), rd(v, ws[3], in_ok)};
       gl::ext acc{rd(v, ws[4], in_ok), rd(v, ws[5], in_ok)};
       bool ok = true;
-      for (uint32_t i = 0; i < nc; i++) {
-        const gl::ext c{rd(v, ws[6 + cw * i], in_ok), base ? 0 : rd(v, ws[7 + 2 * i], in_ok)};
-        acc = gl::ext_add(gl::ext_mul(acc, alpha), c);
-        const uint32_t aw = i + 1 == nc ? 0 : 6 + cw * nc + 2 * i;
-        ok &= both(wset(v, ws[aw], acc.c0), wset(v, ws[aw + 1], acc.c1));
+      constexpr uint32_t CH = 8;
+      for (uint32_t c0 = 0; c0 < nc; c0 += CH) {
+        uint32_t cs[2 * CH], as[2 * CH];
+        uint64_t cv[2 * CH];
+#pragma unroll
+        for (uint32_t k = 0; k < CH; k++) {
+          const uint32_t i = c0 + k < nc ? c0 + k : nc - 1;
+          cs[2 * k] = ws[6 + cw * i];
+          cs[2 * k + 1] = base ? 0 : ws[7 + 2 * i];
+          const uint32_t aw = i + 1 == nc ? 0 : 6 + cw * nc + 2 * i;
+          as[2 * k] = ws[aw];
+          as[2 * k + 1] = ws[aw + 1];
+        }
+#pragma unroll
+        for (uint32_t k = 0; k < 2 * CH; k++) cv[k] = (k & 1) && base ? 0 : rd(v, cs[k], in_ok);
+#pragma unroll
+        for (uint32_t k = 0; k < CH; k++) {
+          if (c0 + k >= nc) break;
+          acc = gl::ext_add(gl::ext_mul(acc, alpha), gl::ext{cv[2 * k], cv[2 * k + 1]});
+          ok &= both(wset(v, as[2 * k], acc.c0), wset(v, as[2 * k + 1], acc.c1));
+        }
       }
       return ok && in_ok;
     }
@@ -195,69 +487,41 @@ __device__ bool run_gen(const DevGenD &g, uint64_t *v, const uint32_t *wslot, ui
       const uint32_t *ws = wslot + (uint64_t)g.row * W;
       const uint64_t shift = rd(v, ws[0], in_ok);
       gl::ext pt{rd(v, ws[CI_EVAL_POINT], in_ok), rd(v, ws[CI_EVAL_POINT + 1], in_ok)};
+      // the 16 values, loaded together before any write
+      uint64_t vals[2 * CI_POINTS];
+#pragma unroll
+      for (uint32_t k = 0; k < 2 * CI_POINTS; k++) vals[k] = rd(v, ws[CI_VALUES + k], in_ok);
       if (!in_ok || shift == 0) return false;
       pt = gl::ext_scale(pt, gl::inv(shift));
       bool ok = both(wset(v, ws[CI_SHIFTED], pt.c0), wset(v, ws[CI_SHIFTED + 1], pt.c1));
       const uint64_t om = gl::root_of_unity(CI_BITS), ninv = gl::inv(CI_POINTS);
       gl::ext ev{0, 0}, pr{1, 0};
-      uint32_t lo = 0, hi = CI_DEGREE;
       uint64_t x = 1;
-      for (uint32_t it = 0;; it++) {
-        for (uint32_t i = lo; i < hi; i++) {
-          const gl::ext term = gl::ext_sub(pt, gl::ext{x, 0});
-          const gl::ext val = gl::ext_scale(gl::ext{rd(v, ws[CI_VALUES + 2 * i], in_ok),
-                                                    rd(v, ws[CI_VALUES + 2 * i + 1], in_ok)}, gl::mul(x, ninv));
-          ev = gl::ext_add(gl::ext_mul(ev, term), gl::ext_mul(val, pr));
-          pr = gl::ext_mul(pr, term);
-          x = gl::mul(x, om);
+      // points [0, 6), then [6, 11), [11, 16): the partial sums after the first
+      // two chunks are the intermediate wires (compile-time indices: vals stays
+      // in registers)
+#pragma clang loop unroll(full)
+      for (uint32_t i = 0; i < CI_POINTS; i++) {
+        if (i >= CI_DEGREE && (i - 1) % (CI_DEGREE - 1) == 0) {
+          const uint32_t it = (i - 1) / (CI_DEGREE - 1) - 1;
+          ok &= both(wset(v, ws[CI_INTER + 2 * it], ev.c0), wset(v, ws[CI_INTER + 2 * it + 1], ev.c1));
+          ok &= both(wset(v, ws[CI_INTER + 2 * (CI_NINT + it)], pr.c0),
+                     wset(v, ws[CI_INTER + 2 * (CI_NINT + it) + 1], pr.c1));
         }
-        if (it == CI_NINT) break;
-        ok &= both(wset(v, ws[CI_INTER + 2 * it], ev.c0), wset(v, ws[CI_INTER + 2 * it + 1], ev.c1));
-        ok &= both(wset(v, ws[CI_INTER + 2 * (CI_NINT + it)], pr.c0), wset(v, ws[CI_INTER + 2 * (CI_NINT + it) + 1], pr.c1));
-        lo = 1 + (CI_DEGREE - 1) * (it + 1);
-        hi = lo + CI_DEGREE - 1 < CI_POINTS ? lo + CI_DEGREE - 1 : CI_POINTS;
+        const gl::ext term = gl::ext_sub(pt, gl::ext{x, 0});
+        const gl::ext val = gl::ext_scale(gl::ext{vals[2 * i], vals[2 * i + 1]}, gl::mul(x, ninv));
+        ev = gl::ext_add(gl::ext_mul(ev, term), gl::ext_mul(val, pr));
+        pr = gl::ext_mul(pr, term);
+        x = gl::mul(x, om);
       }
       ok &= both(wset(v, ws[CI_EVAL_VALUE], ev.c0), wset(v, ws[CI_EVAL_VALUE + 1], ev.c1));
       return ok && in_ok;
     }
-    case WG_POSEIDON: {
+    case WG_POSEIDON:
       // PoseidonGenerator (gates/poseidon.rs), wire layout SURVEY.md A.5
-      const uint32_t *ws = wslot + (uint64_t)g.row * W;
-      uint64_t s[12];
-      for (int i = 0; i < 12; i++) s[i] = rd(v, ws[i], in_ok);
-      const uint64_t swap = rd(v, ws[24], in_ok);
-      if (!in_ok) return false;
-      bool ok = true;
-      for (int i = 0; i < 4; i++) ok &= wset(v, ws[25 + i], gl::mul(swap, gl::sub(s[i + 4], s[i])));
-      if (swap == 1)
-        for (int i = 0; i < 4; i++) {
-          const uint64_t t = s[i];
-          s[i] = s[i + 4];
-          s[i + 4] = t;
-        }
-      int rc = 0;
-      for (int r = 0; r < 4; r++, rc++) {
-        for (int i = 0; i < 12; i++) s[i] = gl::add(s[i], ps::rc(rc * 12 + i));
-        if (r)
-          for (int i = 0; i < 12; i++) ok &= wset(v, ws[29 + (r - 1) * 12 + i], s[i]);
-        for (int i = 0; i < 12; i++) s[i] = ps::sbox(s[i]);
-        ps::mds(s);
-      }
-      for (int r = 0; r < 22; r++, rc++) {
-        for (int i = 0; i < 12; i++) s[i] = gl::add(s[i], ps::rc(rc * 12 + i));
-        ok &= wset(v, ws[65 + r], s[0]);
-        s[0] = ps::sbox(s[0]);
-        ps::mds(s);
-      }
-      for (int r = 0; r < 4; r++, rc++) {
-        for (int i = 0; i < 12; i++) s[i] = gl::add(s[i], ps::rc(rc * 12 + i));
-        for (int i = 0; i < 12; i++) ok &= wset(v, ws[87 + r * 12 + i], s[i]);
-        for (int i = 0; i < 12; i++) s[i] = ps::sbox(s[i]);
-        ps::mds(s);
-      }
-      for (int i = 0; i < 12; i++) ok &= wset(v, ws[12 + i], s[i]);
-      return ok;
-    }
+      if constexpr (QP_WIT_POSEIDON == 2) return poseidon_witness_rolled(v, wslot + (uint64_t)g.row * W);
+      else if constexpr (QP_WIT_POSEIDON == 1) return poseidon_witness(v, wslot + (uint64_t)g.row * W);
+      else return poseidon_witness_plain(g, v, wslot, W);
     default:
       return false;
   }
@@ -265,20 +529,32 @@ __device__ bool run_gen(const DevGenD &g, uint64_t *v, const uint32_t *wslot, ui
 
 // one workgroup per proof; levels separated by workgroup barriers.  Every
 // wave reaches every barrier (no early exit), so the grid always drains.
-__global__ void __launch_bounds__(256) k_witness_gen(const WitnessGenArgs a) {
+__global__ void __launch_bounds__(512) k_witness_gen(const WitnessGenArgs a) {
   const uint32_t b = blockIdx.x;
   uint64_t *v = a.vals + (uint64_t)b * a.v_bstride;
   const DevGenD *gens = (const DevGenD *)a.gens;
+  const uint32_t nwaves = blockDim.x >> 6, wave = threadIdx.x >> 6;
   bool ok = true;
   uint32_t bad = 0;
   for (uint32_t l = 0; l < a.nlevels; l++) {
     const uint32_t lo = a.level_off[l], hi = a.level_off[l + 1];
+    const uint32_t plo = a.level_pos[2 * l], pcnt = a.level_pos[2 * l + 1];
+    // narrow levels: their Poseidon generators one per wave (poseidon_coop),
+    // the level's other generators one per lane as usual
+    const bool coop = pcnt && pcnt <= a.coop_max;
     for (uint32_t i = lo + threadIdx.x; i < hi; i += blockDim.x) {
+      if (coop && i >= plo && i < plo + pcnt) continue;
       if (!run_gen(gens[i], v, a.wslot, a.W, a.limbs, a.zero_slot, a.num_consts) && ok) {
         ok = false;
         bad = i + 1;
       }
     }
+    if (coop)
+      for (uint32_t p = plo + wave; p < plo + pcnt; p += nwaves)  // wave-uniform: every lane active
+        if (!poseidon_coop(v, a.wslot + (uint64_t)gens[p].row * a.W) && ok) {
+          ok = false;
+          bad = p + 1;
+        }
     __syncthreads();
   }
   if (!ok) atomicCAS(a.err + b, 0u, bad);

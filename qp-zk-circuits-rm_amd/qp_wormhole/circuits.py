@@ -205,14 +205,20 @@ class Circuit:
     GATE_KINDS = ("noop", "constant", "public_input", "base_sum", "arithmetic", "poseidon", "random_access",
                   "arith_ext", "mul_ext", "reducing", "reducing_ext", "poseidon_mds", "coset_interp")
 
-    def census(self):
+    def census(self, levels=False):
         """({generator kind: count}, {gate kind: rows}) of the built circuit
-        (qp_circuit_census; all n rows, padding counted as noop)."""
+        (qp_circuit_census; all n rows, padding counted as noop); levels=True
+        adds the device witness schedule: per dependency level {kind: count}."""
         g, r = (ctypes.c_uint32 * 14)(), (ctypes.c_uint32 * 13)()
-        rc = lib().qp_circuit_census(self.h, g, r)
+        lv = (ctypes.c_uint32 * (14 * max(self.witness_levels, 1)))() if levels else None
+        rc = lib().qp_circuit_census(self.h, g, r, lv)
         if rc:
             raise QpError(rc, "qp_circuit_census")
-        return dict(zip(self.GEN_KINDS, g)), dict(zip(self.GATE_KINDS, r))
+        out = (dict(zip(self.GEN_KINDS, g)), dict(zip(self.GATE_KINDS, r)))
+        if levels:
+            out += ([{k: v for k, v in zip(self.GEN_KINDS, lv[14 * l:14 * l + 14]) if v}
+                     for l in range(self.witness_levels)],)
+        return out
 
     @classmethod
     def wormhole(cls, zero_knowledge=False):

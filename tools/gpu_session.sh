@@ -72,6 +72,23 @@ for s in "$@"; do
            done; unset QPGPU_LDE_MODE ;;
     aggprof) step prof_agg 300 env QP_AGG_PROVERS=1 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/prof_agg -o run -- python3 tools/agg_subtree.py 256 1 ;;
     aggpmc) step pmc_agg_wit 300 env QP_AGG_PROVERS=1 rocprofv3 --pmc SQ_WAVES SQ_INSTS_VALU SQ_WAVE_CYCLES SQ_WAIT_INST_ANY SQ_INSTS_VMEM_RD SQ_INSTS_VMEM_WR SQ_ACTIVE_INST_VALU SQ_INSTS_SALU --kernel-include-regex k_witness_gen --output-format csv -d gpurun_out/pmc_agg_wit -o run -- python3 tools/agg_subtree.py 256 1 ;;
+    lde_batch) for nb in 16 43 86; do
+             step prof_lde_b$nb 300 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/prof_lde_b$nb -o run -- python3 tools/kbench.py $nb 2 || exit 1
+           done ;;
+    wit_ab) step wit_def 300 python -u tools/agg_subtree.py 256 2 &&
+            step wit_wp0 300 env QPGPU_LIB=gpurun_ab/libqpgpu_wp0.so python -u tools/agg_subtree.py 256 2 &&
+            step wit_wp2 300 env QPGPU_LIB=gpurun_ab/libqpgpu_wp2.so python -u tools/agg_subtree.py 256 2 &&
+            step wit_wp2_test 600 env QPGPU_LIB=gpurun_ab/libqpgpu_wp2.so python -u -m pytest tests/test_gpu_aggregation.py -x -q --timeout 400 --timeout-method thread ;;
+    wit_ab2) step wit_t256 300 python -u tools/agg_subtree.py 256 2 &&
+             step wit_t512 300 env QPGPU_WIT_THREADS=512 python -u tools/agg_subtree.py 256 2 &&
+             step wit_t512_test 600 env QPGPU_WIT_THREADS=512 python -u -m pytest tests/test_gpu_aggregation.py tests/test_gpu_witness.py -x -q --timeout 400 --timeout-method thread ;;
+    wit_prof) step prof_wit2 300 env QP_AGG_PROVERS=1 QPGPU_WIT_TWICE=1 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/prof_wit2 -o run -- python3 tools/agg_subtree.py 256 1 &&
+              step agg_p4 300 env QP_AGG_PROVERS=4 python -u tools/agg_subtree.py 256 2 &&
+              step agg_p3 300 env QP_AGG_PROVERS=3 python -u tools/agg_subtree.py 256 2 ;;
+    coop_ab) step coop_def 300 python -u tools/agg_subtree.py 256 2 &&
+             step coop_off 300 env QPGPU_WIT_COOP=0 python -u tools/agg_subtree.py 256 2 &&
+             step coop_16 300 env QPGPU_WIT_COOP=16 python -u tools/agg_subtree.py 256 2 &&
+             step coop_t512 300 env QPGPU_WIT_THREADS=512 python -u tools/agg_subtree.py 256 2 ;;
     *) echo "unknown step $s" ;;
   esac
 done
