@@ -59,9 +59,9 @@ int qp_ctx_synchronize(qp_ctx *c) {
 
 static int check_shape(qp_ctx *c, uint32_t npolys, uint32_t log_n, uint32_t rate_bits, uint32_t cap_h) {
   if (!c) return QP_ERR_ARG;
-  if (npolys == 0 || log_n > 14 || rate_bits > 6 || log_n + rate_bits > qpk::TW_LOG ||
+  if (npolys == 0 || log_n > qpk::BIG_LOG_MAX || rate_bits > 6 || log_n + rate_bits > qpk::TW_LOG ||
       cap_h > log_n + rate_bits) {
-    c->err = "unsupported shape (need log_n <= 14, log_n + rate_bits <= 16, cap_h <= log N)";
+    c->err = "unsupported shape (need log_n <= 16, log_n + rate_bits <= 18, cap_h <= log N)";
     return QP_ERR_ARG;
   }
   return QP_OK;

@@ -11,19 +11,24 @@
 
 namespace qpk {
 
-constexpr unsigned TW_LOG = 17;  // twiddle tables cover sizes up to 2^17 (degree-2^14 circuits at rate 3)
-// Twiddle table layout (2^16 words per direction): [0, 2^15) holds w_{2^16}^j
-// (= w_{2^17}^{2j}), [2^15, 2^16) holds w_{2^17}^{2j+1}.  Every size <= 2^16
-// reads only the first half, with the locality of a plain 2^16 table; the odd
-// powers serve size-2^17 transforms (tw_get below: E = the w_{2^17} exponent).
+constexpr unsigned TW_LOG = 18;  // twiddle tables cover sizes up to 2^18 (degree-2^15 circuits at rate 3)
+// Twiddle table layout (2^17 words per direction): [0, 2^16) holds w_{2^17}^j
+// (= w_{2^18}^{2j}), [2^16, 2^17) holds w_{2^18}^{2j+1}.  Every size <= 2^17
+// reads only the first half; the odd powers serve size-2^18 transforms
+// (tw_get below: E = the w_{2^18} exponent).
 __host__ __device__ __forceinline__ uint64_t tw_get(const uint64_t *__restrict__ tw, uint32_t E) {
-  constexpr uint32_t Q = 1u << (TW_LOG - 2);  // 2^15
+  constexpr uint32_t Q = 1u << (TW_LOG - 2);  // 2^16
   const uint32_t j = E >> 1;
   const uint64_t *t = tw + ((E & 1) ? Q : 0);
   if (j < Q) return t[j];
   const uint64_t v = t[j - Q];
-  return v ? 0xFFFFFFFF00000001ull - v : 0;  // w^(2^16) = -1
+  return v ? 0xFFFFFFFF00000001ull - v : 0;  // w^(2^17) = -1
 }
+// the largest transform one workgroup holds in LDS (2^14 words: 135 KB with
+// padding); larger ones (the degree-2^15 top levels of an aggregation tree)
+// run their first log_n - 14 radix-2 levels in HBM, then 2^14-point blocks
+// in LDS (ntt.hip "transforms beyond one workgroup's LDS")
+constexpr uint32_t LDS_LOG_MAX = 14, BIG_LOG_MAX = 16;
 // LDS slots of a size-n NTT workgroup: one pad slot per 32 elements (ntt16.h lp())
 __host__ __device__ constexpr uint32_t ntt_lds_words(uint32_t n) { return n + (n >> 5); }
 #define QP_HAVE_LDS_WORDS 1
@@ -70,6 +75,15 @@ void twiddles_free(Twiddles &t);
 // batch: nbat independent matrices at in + b*in_bstride etc.
 void intt(const Twiddles &t, const uint64_t *in, uint64_t in_stride, uint64_t *out, uint64_t out_stride,
           uint32_t ncols, uint32_t log_n, uint32_t nbat, uint64_t in_bstride, uint64_t out_bstride, hipStream_t s);
+
+// in-place radix-2 DIF over each column (natural in, bit-reversed out, values
+// canonical), any 2^log_n <= 2^BIG_LOG_MAX: HBM levels down to 2^LDS_LOG_MAX
+// blocks, then the blocks in LDS.  nsub columns per (col, batch) group, nsub_stride apart
+void dif_big(const Twiddles &t, uint64_t *x, uint64_t c_stride, uint32_t ncols, uint32_t nsub, uint64_t nsub_stride,
+             uint32_t log_n, bool inv, uint32_t nbat, uint64_t bstride, hipStream_t s);
+// in place per column: x[k] <- x[rev_n(k)] * c0 * base^k (the bit-reversal of a DIF result)
+void bitrev_scale(uint64_t *x, uint64_t stride, uint32_t ncols, uint32_t log_n, uint64_t c0, uint64_t base,
+                  uint32_t nbat, uint64_t bstride, hipStream_t s);
 
 // coefficients (n) -> coset LDE (N = n << rate_bits) at shift*w_N^j, written in
 // Merkle-leaf (bit-reversed) order.  (plonky2 PolynomialBatch::lde_values)

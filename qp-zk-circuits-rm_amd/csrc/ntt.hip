@@ -360,6 +360,103 @@ k_lde_cosets8(const uint64_t *__restrict__ coeffs, uint64_t c_stride, uint64_t c
   }
 }
 
+// ---- transforms beyond one workgroup's LDS (n = 2^15, 2^16: the top levels
+// of a 2048-leaf aggregation tree register every leaf's public inputs and
+// need 2^15 rows).  A DIF's levels of half-width H >= 2^LDS_LOG_MAX pair
+// elements across 2^14-blocks: those run as one HBM pass each
+// (x_j, x_{j+H} -> x_j + x_{j+H}, (x_j - x_{j+H}) w_{2H}^{j mod H}); the
+// remaining 14 levels are the blocks' own size-2^14 DIFs, in LDS with the
+// same pass tables as every other NTT.  Off the Wormhole hot path (one or two
+// proofs per tree), so the HBM levels are plain radix-2.
+
+// one radix-2 DIF level of half-width 2^log_h over columns of 2^log_n values
+__global__ void __launch_bounds__(256) k_dif_level(uint64_t *x, uint64_t c_stride, uint32_t nsub, uint64_t nsub_stride,
+                                                   uint64_t bstride, uint32_t log_n, uint32_t log_h,
+                                                   const uint64_t *__restrict__ tw) {
+  const uint32_t col = blockIdx.y / nsub, sub = blockIdx.y % nsub;
+  uint64_t *v = x + blockIdx.z * bstride + (uint64_t)col * c_stride + (uint64_t)sub * nsub_stride;
+  const uint64_t half = 1ull << (log_n - 1), H = 1ull << log_h;
+  for (uint64_t j = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; j < half; j += (uint64_t)gridDim.x * blockDim.x) {
+    const uint64_t off = j & (H - 1), i0 = ((j >> log_h) << (log_h + 1)) + off, i1 = i0 + H;
+    const uint64_t a = v[i0], b = v[i1];
+    v[i0] = gl::add(a, b);
+    v[i1] = gl::mul(gl::sub(a, b), nt::tw_pow(tw, (uint32_t)off, log_h + 1));
+  }
+}
+
+// the size-2^LDS_LOG_MAX DIF of every block, in place (canonical out)
+template <bool INV>
+__global__ void __launch_bounds__(512) QP_NTT_OCC k_dif_blocks(uint64_t *x, uint64_t c_stride, uint32_t nsub,
+                                                               uint64_t nsub_stride, uint64_t bstride,
+                                                               const uint64_t *__restrict__ pt) {
+  extern __shared__ __attribute__((aligned(16))) uint64_t lds[];
+  constexpr uint32_t M = 1u << LDS_LOG_MAX;
+  const uint32_t col = blockIdx.y / nsub, sub = blockIdx.y % nsub;
+  uint64_t *v = x + blockIdx.z * bstride + (uint64_t)col * c_stride + (uint64_t)sub * nsub_stride +
+                ((uint64_t)blockIdx.x << LDS_LOG_MAX);
+  for (uint32_t i = threadIdx.x; i < M; i += blockDim.x) lds[nt::lp(i)] = v[i];
+  __syncthreads();
+  nt::ntt_lds<INV>(lds, LDS_LOG_MAX, pt);
+  for (uint32_t i = threadIdx.x; i < M; i += blockDim.x) v[i] = nt::canon(lds[nt::lp(i)]);
+}
+
+// in place: x[k] <- x[rev(k)] * c0 * base^k (pairs k < rev(k) swapped by one thread)
+__global__ void __launch_bounds__(256) k_bitrev_scale(uint64_t *x, uint64_t stride, uint32_t log_n, uint64_t c0,
+                                                      uint64_t base, uint64_t bstride) {
+  uint64_t *v = x + blockIdx.z * bstride + (uint64_t)blockIdx.y * stride;
+  const uint32_t n = 1u << log_n, gs = gridDim.x * blockDim.x;
+  for (uint32_t k = blockIdx.x * blockDim.x + threadIdx.x; k < n; k += gs) {
+    const uint32_t r = gl::rev_bits(k, log_n);
+    if (r < k) continue;
+    const uint64_t fk = base == 1 ? c0 : gl::mul(c0, gl::pow(base, k));
+    const uint64_t a = v[k], b = v[r];
+    v[k] = gl::mul(b, fk);
+    if (r != k) v[r] = gl::mul(a, base == 1 ? c0 : gl::mul(c0, gl::pow(base, r)));
+  }
+}
+
+// LDE input of coset block y % B of column y / B: c_k (shift w_N^s)^k, s = rev_r(y % B)
+__global__ void __launch_bounds__(256) k_coset_scale(const uint64_t *__restrict__ coeffs, uint64_t c_stride,
+                                                     uint64_t *__restrict__ out, uint64_t o_stride, uint32_t log_n,
+                                                     uint32_t rate_bits, uint64_t shift,
+                                                     const uint64_t *__restrict__ tw, uint64_t c_bstride,
+                                                     uint64_t o_bstride) {
+  const uint32_t B = 1u << rate_bits, col = blockIdx.y / B, sp = blockIdx.y % B;
+  const uint32_t s = gl::rev_bits(sp, rate_bits);
+  const uint64_t *a = coeffs + blockIdx.z * c_bstride + (uint64_t)col * c_stride;
+  uint64_t *o = out + blockIdx.z * o_bstride + (uint64_t)col * o_stride + ((uint64_t)sp << log_n);
+  const uint64_t base = gl::mul(shift, nt::tw_pow(tw, s, log_n + rate_bits));
+  const uint32_t n = 1u << log_n, stride = gridDim.x * blockDim.x;
+  uint32_t k = blockIdx.x * blockDim.x + threadIdx.x;
+  uint64_t f = gl::pow(base, k);
+  const uint64_t step = gl::pow(base, stride);
+  for (; k < n; k += stride) {
+    o[k] = gl::mul(a[k], f);
+    f = gl::mul(f, step);
+  }
+}
+
+void dif_big(const Twiddles &t, uint64_t *x, uint64_t c_stride, uint32_t ncols, uint32_t nsub, uint64_t nsub_stride,
+             uint32_t log_n, bool inv, uint32_t nbat, uint64_t bstride, hipStream_t s) {
+  if (!ncols || !nbat || log_n <= LDS_LOG_MAX || log_n > BIG_LOG_MAX) return;
+  const dim3 g((unsigned)std::min<uint64_t>((1ull << (log_n - 1)) / 256, 256), ncols * nsub, nbat);
+  for (uint32_t lh = log_n - 1; lh >= LDS_LOG_MAX; lh--)
+    k_dif_level<<<g, 256, 0, s>>>(x, c_stride, nsub, nsub_stride, bstride, log_n, lh, inv ? t.inv : t.fwd);
+  const dim3 gb(1u << (log_n - LDS_LOG_MAX), ncols * nsub, nbat);
+  const size_t lds = 8u * qpk::ntt_lds_words(1u << LDS_LOG_MAX);
+  if (inv)
+    k_dif_blocks<true><<<gb, 512, lds, s>>>(x, c_stride, nsub, nsub_stride, bstride, t.pt_inv);
+  else
+    k_dif_blocks<false><<<gb, 512, lds, s>>>(x, c_stride, nsub, nsub_stride, bstride, t.pt_fwd);
+}
+
+void bitrev_scale(uint64_t *x, uint64_t stride, uint32_t ncols, uint32_t log_n, uint64_t c0, uint64_t base,
+                  uint32_t nbat, uint64_t bstride, hipStream_t s) {
+  if (!ncols || !nbat) return;
+  const dim3 g((unsigned)std::min<uint64_t>(((1ull << log_n) + 255) / 256, 64), ncols, nbat);
+  k_bitrev_scale<<<g, 256, 0, s>>>(x, stride, log_n, c0, base, bstride);
+}
+
 static unsigned ntt_threads(uint32_t log_n) {
   uint32_t half = log_n ? (1u << (log_n - 1)) : 1;
   return half < 64 ? 64 : (half > 512 ? 512 : half);
@@ -369,6 +466,18 @@ void intt(const Twiddles &t, const uint64_t *in, uint64_t in_stride, uint64_t *o
           uint32_t ncols, uint32_t log_n, uint32_t nbat, uint64_t in_bstride, uint64_t out_bstride, hipStream_t s) {
   if (!ncols || !nbat) return;
   uint64_t n_inv = gl::inv((uint64_t)1 << log_n);
+  if (log_n > LDS_LOG_MAX) {
+    // the values into out, an in-place inverse DIF, then the in-place
+    // bit-reversal scaled by 1/n
+    const uint64_t n = 1ull << log_n;
+    for (uint32_t b = 0; b < nbat; b++)
+      if (out + b * out_bstride != in + b * in_bstride)
+        (void)hipMemcpy2DAsync(out + b * out_bstride, out_stride * 8, in + b * in_bstride, in_stride * 8, n * 8,
+                               (size_t)ncols, hipMemcpyDeviceToDevice, s);
+    dif_big(t, out, out_stride, ncols, 1, 0, log_n, true, nbat, out_bstride, s);
+    bitrev_scale(out, out_stride, ncols, log_n, n_inv, 1, nbat, out_bstride, s);
+    return;
+  }
   dim3 grid(ncols, nbat);
   k_intt<<<grid, ntt_threads(log_n), 8u * qpk::ntt_lds_words(1u << log_n), s>>>(in, in_stride, out, out_stride, log_n, n_inv, t.pt_inv,
                                                          in_bstride, out_bstride);
@@ -378,6 +487,16 @@ void lde(const Twiddles &t, const uint64_t *coeffs, uint64_t c_stride, uint64_t 
          uint32_t ncols, uint32_t log_n, uint32_t rate_bits, uint64_t shift, uint32_t nbat, uint64_t c_bstride,
          uint64_t o_bstride, hipStream_t s) {
   if (!ncols || !nbat) return;
+  if (log_n > LDS_LOG_MAX) {
+    // every coset block of the output: the scaled coefficients, then an
+    // in-place DIF (bit-reversed = Merkle-leaf order within the block)
+    const uint32_t B = 1u << rate_bits;
+    const dim3 g((unsigned)std::min<uint64_t>((1ull << log_n) / 256, 64), ncols * B, nbat);
+    k_coset_scale<<<g, 256, 0, s>>>(coeffs, c_stride, out, o_stride, log_n, rate_bits, shift, t.fwd, c_bstride,
+                                    o_bstride);
+    dif_big(t, out, o_stride, ncols, B, 1ull << log_n, log_n, false, nbat, o_bstride, s);
+    return;
+  }
   // n = 2^14 (the aggregation circuits): 1024 threads x 16 and 135 KB of LDS,
   // one workgroup per CU
   if (rate_bits >= 1 && rate_bits <= LDE_MAX_RATE && log_n >= LDE_COSETS_MIN_LOG && log_n <= LDE_COSETS_MAX_LOG &&

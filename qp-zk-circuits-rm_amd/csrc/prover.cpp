@@ -252,9 +252,9 @@ int setup(qp_prover *P) {
   P->common = cd.common_bytes();
   // zero_knowledge is accepted: under the reference's `no_random` feature the zk
   // config adds neither blinding rows nor salt columns (see DESIGN.md "zk")
-  if (P->nc != 2 || (1u << P->rate_bits) != P->qdf || P->log_n > 14 || P->log_n < 6 || P->nchunks > 16 ||
-      P->NC > 8 || P->arity.size() > 8 || P->nq > 64) {
-    c->err = "unsupported circuit shape for the GPU prover (need 2 challenges, qdf = blowup, 2^6 <= n <= 2^14)";
+  if (P->nc != 2 || (1u << P->rate_bits) != P->qdf || P->log_n > qpk::BIG_LOG_MAX - 1 || P->log_n < 6 ||
+      P->log_n + P->rate_bits > qpk::TW_LOG || P->nchunks > 16 || P->NC > 8 || P->arity.size() > 8 || P->nq > 64) {
+    c->err = "unsupported circuit shape for the GPU prover (need 2 challenges, qdf = blowup, 2^6 <= n <= 2^15)";
     return QP_ERR_ARG;
   }
   qpk::GateDesc &g = P->gdesc;
@@ -611,7 +611,12 @@ int prove_batch(qp_prover *P, const uint64_t *d_wires, const uint64_t *const *wi
   else
     qpk::k_pp_rows<<<dim3(cdiv(n, 256), nb), 256, 0, s>>>(wv, P->sigmas.p, P->kis.p, P->chal.p, P->prods.p,
                                                            P->log_n, P->R, P->qdf, nc, P->wires.cbs(), pbs, c->tw.fwd);
-  qpk::k_z_scan<<<dim3(nc, nb), 1024, 8u * (qpk::ntt_lds_words(n) + 1024), s>>>(P->prods.p, P->zs.vals.p, P->log_n, nc, P->nchunks, pbs, P->zs.cbs());
+  if (P->log_n <= qpk::LDS_LOG_MAX)
+    qpk::k_z_scan<true><<<dim3(nc, nb), 1024, 8u * (qpk::ntt_lds_words(n) + 1024), s>>>(
+        P->prods.p, P->zs.vals.p, P->log_n, nc, P->nchunks, pbs, P->zs.cbs());
+  else
+    qpk::k_z_scan<false><<<dim3(nc, nb), 1024, 8u * 1024, s>>>(P->prods.p, P->zs.vals.p, P->log_n, nc, P->nchunks,
+                                                              pbs, P->zs.cbs());
   P->zs.build_from_values(c, nb);
   TRY(hipGetLastError());
   if ((rc = fetch_caps(P, P->zs.dig.p, P->zs.dbs(), logN, nb))) return rc;
@@ -670,9 +675,21 @@ int prove_batch(qp_prover *P, const uint64_t *d_wires, const uint64_t *const *wi
       qpk::k_quotient_1r<<<dim3(cdiv(N, 256), nb), 256, 0, s>>>(a);
     kt_end(P, 3, (double)nb * N);
     const uint64_t n_inv = gl::inv(n);
-    qpk::k_qintt_blocks<<<dim3(B, nc, nb), 512, 8u * qpk::ntt_lds_words(1u << P->log_n), s>>>(P->qvals.p, P->cbuf.p, P->log_n, P->rate_bits,
-                                                                     (uint64_t)nc * N, (uint64_t)nc * N, c->tw.fwd,
-                                                                     c->tw.pt_inv, n_inv, gl::inv(gl::GEN));
+    if (P->log_n <= qpk::LDS_LOG_MAX) {
+      qpk::k_qintt_blocks<<<dim3(B, nc, nb), 512, 8u * qpk::ntt_lds_words(1u << P->log_n), s>>>(
+          P->qvals.p, P->cbuf.p, P->log_n, P->rate_bits, (uint64_t)nc * N, (uint64_t)nc * N, c->tw.fwd, c->tw.pt_inv,
+          n_inv, gl::inv(gl::GEN));
+    } else {
+      // n > 2^14: gather each coset block into natural order, inverse DIF in
+      // place, then per coset the bit-reversal scaled by (g w_N^s)^-k / n
+      qpk::k_qintt_gather_big<<<dim3(64, nc * B, nb), 256, 0, s>>>(P->qvals.p, P->cbuf.p, P->log_n, P->rate_bits,
+                                                                  (uint64_t)nc * N, (uint64_t)nc * N);
+      qpk::dif_big(c->tw, P->cbuf.p, (uint64_t)B * n, nc, B, n, P->log_n, true, nb, (uint64_t)nc * N, s);
+      const uint64_t wN = gl::root_of_unity(logN), ginv = gl::inv(gl::GEN);
+      for (uint32_t sc = 0; sc < B; sc++)
+        qpk::bitrev_scale(P->cbuf.p + (uint64_t)sc * n, (uint64_t)B * n, nc, P->log_n, n_inv,
+                          gl::mul(ginv, gl::inv(gl::pow(wN, sc))), nb, (uint64_t)nc * N, s);
+    }
     const uint64_t winv_r = gl::inv(gl::root_of_unity(P->rate_bits));
     const uint64_t gninv = gl::inv(gl::pow(gl::GEN, n));
     qpk::k_qintt_radix<<<dim3(cdiv(n, 256), nc, nb), 256, 0, s>>>(P->cbuf.p, P->quot.coeffs.p, P->log_n, P->rate_bits,
@@ -743,8 +760,11 @@ int prove_batch(qp_prover *P, const uint64_t *d_wires, const uint64_t *const *wi
     fa.chal = P->chal.p;
     fa.comp = P->comp.p;
     qpk::k_fri_compose<<<dim3(cdiv(n, 256), nb), 256, 0, s>>>(fa);
-    qpk::k_fri_divide<<<nb, (unsigned)std::min<uint64_t>(1024, n / 8), 0, s>>>(P->comp.p, P->fin.p, P->log_n,
-                                                                             P->chal.p, 2 * N, N);
+    if (n / std::min<uint64_t>(1024, n / 8) <= 16)
+      qpk::k_fri_divide<16><<<nb, (unsigned)std::min<uint64_t>(1024, n / 8), 0, s>>>(P->comp.p, P->fin.p, P->log_n,
+                                                                                   P->chal.p, 2 * N, N);
+    else
+      qpk::k_fri_divide<64><<<nb, 1024, 0, s>>>(P->comp.p, P->fin.p, P->log_n, P->chal.p, 2 * N, N);
     TRY(hipGetLastError());
   }
   {

@@ -67,6 +67,7 @@ template <int R, int QDF>
 __global__ void k_pp_rows_t(const uint64_t *wires, const uint64_t *sigmas, const uint64_t *k_is, const uint64_t *chal,
                             uint64_t *prods, uint32_t log_n, uint64_t w_bstride, uint64_t p_bstride,
                             const uint64_t *tw);
+template <bool STAGE>
 __global__ void k_z_scan(const uint64_t *prods, uint64_t *zs, uint32_t log_n, uint32_t nc, uint32_t nchunks,
                          uint64_t p_bstride, uint64_t z_bstride);
 template <int PH>
@@ -75,6 +76,8 @@ __global__ void k_quotient_1r(QuotientArgs a);
 // k_quotient_1r for R = 80 routed wires in chunks of 8 with the Poseidon gate:
 // the sweep rides on the gate's wire reads (every wire read once)
 __global__ void k_quotient_fused(QuotientArgs a);
+__global__ void k_qintt_gather_big(const uint64_t *vals, uint64_t *out, uint32_t log_n, uint32_t rate_bits,
+                                   uint64_t v_bstride, uint64_t o_bstride);
 __global__ void k_qintt_blocks(const uint64_t *vals, uint64_t *out, uint32_t log_n, uint32_t rate_bits,
                                uint64_t v_bstride, uint64_t o_bstride, const uint64_t *tw, const uint64_t *pt_inv,
                                uint64_t n_inv, uint64_t ginv);
@@ -84,6 +87,7 @@ constexpr int OPEN_PB = 8;  // polys per k_openings block
 __global__ void k_openings(const uint64_t *coeffs, uint64_t c_bstride, uint32_t npolys, uint32_t log_n,
                            const uint64_t *pts, uint32_t pt_off, uint64_t *out, uint32_t out_off);
 __global__ void k_fri_compose(FriComposeArgs a);
+template <int MAXPER>
 __global__ void k_fri_divide(const uint64_t *comp, uint64_t *fin, uint32_t log_n, const uint64_t *chal,
                              uint64_t f_bstride, uint64_t f_cstride);
 __global__ void k_fri_leaf(const uint64_t *vals, uint64_t *dig, uint32_t log_len, uint32_t ab, uint64_t v_bstride,

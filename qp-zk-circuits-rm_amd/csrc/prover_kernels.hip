@@ -163,22 +163,30 @@ template __global__ void k_pp_rows_t<80, 8>(const uint64_t *, const uint64_t *, 
 // chunk scanned from LDS, Z written back over them), so every HBM access is a
 // coalesced row sweep: n reads of the full products, (npp) reads of the
 // partial products, (1 + npp) n writes per challenge.
+// STAGE = true: the row products are staged in LDS (n <= 2^14); false: read
+// from HBM (the degree-2^15/2^16 top aggregation circuits), Z written there
+template <bool STAGE>
 __global__ void __launch_bounds__(1024) k_z_scan(const uint64_t *__restrict__ prods, uint64_t *__restrict__ zs,
                                                  uint32_t log_n, uint32_t nc, uint32_t nchunks, uint64_t p_bstride,
                                                  uint64_t z_bstride) {
-  extern __shared__ __attribute__((aligned(16))) uint64_t zbuf[];  // [lp(n)] rows, then [T] partials
+  extern __shared__ __attribute__((aligned(16))) uint64_t zbuf[];  // [lp(n)] rows (STAGE), then [T] partials
   const uint32_t n = 1u << log_n;
   const uint32_t c = blockIdx.x, b = blockIdx.y;
   prods += b * p_bstride + (uint64_t)c * nchunks * n;
   zs += b * z_bstride;
   const uint64_t *full = prods + (uint64_t)(nchunks - 1) * n;
   const uint32_t T = blockDim.x, t = threadIdx.x, per = (n + T - 1) / T;
-  uint64_t *part = zbuf + nt::lp(n);
-  for (uint32_t i = t; i < n; i += T) zbuf[nt::lp(i)] = full[i];
-  __syncthreads();
+  uint64_t *part = STAGE ? zbuf + nt::lp(n) : zbuf;
+  // staged: row i at zbuf[lp(i)]; unstaged: Z itself is built in zs column c
+  uint64_t *zc = zs + (uint64_t)c * n;
+  auto row = [&](uint32_t i) -> uint64_t { return STAGE ? zbuf[nt::lp(i)] : full[i]; };
+  if constexpr (STAGE) {
+    for (uint32_t i = t; i < n; i += T) zbuf[nt::lp(i)] = full[i];
+    __syncthreads();
+  }
   const uint32_t lo = min(t * per, n), hi = min(lo + per, n);
   uint64_t local = 1;
-  for (uint32_t i = lo; i < hi; i++) local = gl::mul(local, zbuf[nt::lp(i)]);
+  for (uint32_t i = lo; i < hi; i++) local = gl::mul(local, row(i));
   part[t] = local;
   __syncthreads();
   // inclusive Hillis-Steele scan over T partial products
@@ -190,18 +198,21 @@ __global__ void __launch_bounds__(1024) k_z_scan(const uint64_t *__restrict__ pr
   }
   uint64_t z = t ? part[t - 1] : 1;
   for (uint32_t i = lo; i < hi; i++) {
-    const uint64_t f = zbuf[nt::lp(i)];
-    zbuf[nt::lp(i)] = z;
+    const uint64_t f = row(i);
+    if constexpr (STAGE) zbuf[nt::lp(i)] = z;
+    else zc[i] = z;
     z = gl::mul(z, f);
   }
   __syncthreads();
   const uint32_t npp = nchunks - 1;
   for (uint32_t i = t; i < n; i += T) {
-    const uint64_t zi = zbuf[nt::lp(i)];
-    zs[(uint64_t)c * n + i] = zi;
+    const uint64_t zi = STAGE ? zbuf[nt::lp(i)] : zc[i];
+    if constexpr (STAGE) zc[i] = zi;
     for (uint32_t j = 0; j < npp; j++) zs[((uint64_t)nc + c * npp + j) * n + i] = gl::mul(zi, prods[(uint64_t)j * n + i]);
   }
 }
+template __global__ void k_z_scan<true>(const uint64_t *, uint64_t *, uint32_t, uint32_t, uint32_t, uint64_t, uint64_t);
+template __global__ void k_z_scan<false>(const uint64_t *, uint64_t *, uint32_t, uint32_t, uint32_t, uint64_t, uint64_t);
 
 // ---------------------------------------------------------------- a8
 //
@@ -1200,6 +1211,22 @@ __global__ void __launch_bounds__(512) k_qintt_blocks(const uint64_t *__restrict
   }
 }
 
+// coset iNTT stage 1 for n > 2^14: block sp (coset s = rev_r(sp), values in
+// bit-reversed order) gathered into natural order at block s of out; the
+// caller then runs the inverse DIF in place (dif_big) and the bit-reversal
+// scaled by base^-k / n (bitrev_scale), as k_qintt_blocks does in LDS
+__global__ void __launch_bounds__(256) k_qintt_gather_big(const uint64_t *__restrict__ vals, uint64_t *__restrict__ out,
+                                                          uint32_t log_n, uint32_t rate_bits, uint64_t v_bstride,
+                                                          uint64_t o_bstride) {
+  const uint32_t n = 1u << log_n, B = 1u << rate_bits, c = blockIdx.y / B, sp = blockIdx.y % B;
+  const uint32_t s = gl::rev_bits(sp, rate_bits);
+  const uint64_t N = (uint64_t)n << rate_bits;
+  const uint64_t *src = vals + blockIdx.z * v_bstride + c * N + ((uint64_t)sp << log_n);
+  uint64_t *dst = out + blockIdx.z * o_bstride + ((uint64_t)c << rate_bits) * n + (uint64_t)s * n;
+  for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += gridDim.x * blockDim.x)
+    dst[i] = src[gl::rev_bits(i, log_n)];
+}
+
 // coset iNTT, stage 2: e_j = (1/2^r) sum_s C^s_k w_{2^r}^{-sj}; a_{k+jn} = e_j g^{-jn}
 __global__ void __launch_bounds__(256) k_qintt_radix(const uint64_t *__restrict__ cbuf, uint64_t *__restrict__ coeffs,
                                                      uint32_t log_n, uint32_t rate_bits, uint64_t c_bstride,
@@ -1296,6 +1323,9 @@ __global__ void __launch_bounds__(256) k_fri_compose(FriComposeArgs a) {
 
 // suffix-scan form of divide_by_linear: q_{k-1} = sum_{i>=k} c_i z^{i-k}
 //   = z^{-k} S_k with S_k = sum_{i>=k} c_i z^i; final = alpha^nc Q1 + Q2
+// MAXPER: n / blockDim.x values per thread (16 up to n = 2^14; 64 for the
+// degree-2^15/2^16 top aggregation circuits, whose arrays live in scratch)
+template <int MAXPER>
 __global__ void __launch_bounds__(1024) k_fri_divide(const uint64_t *__restrict__ comp, uint64_t *__restrict__ fin,
                                                      uint32_t log_n, const uint64_t *__restrict__ chal,
                                                      uint64_t f_bstride, uint64_t f_cstride) {
@@ -1304,14 +1334,14 @@ __global__ void __launch_bounds__(1024) k_fri_divide(const uint64_t *__restrict_
   const uint64_t *ch = chal + b * CHAL_STRIDE;
   const uint32_t T = blockDim.x, per = n / T;
   const uint32_t lo = threadIdx.x * per;
-  ext res[16];
+  ext res[MAXPER];
   for (int pass = 0; pass < 2; pass++) {
     const uint64_t *cc = comp + b * (4ull * n) + (uint64_t)pass * 2 * n;
     const ext z{ch[pass ? CH_ZETA_NEXT : CH_ZETA], ch[(pass ? CH_ZETA_NEXT : CH_ZETA) + 1]};
     const ext zi{ch[pass ? CH_ZETA_NEXT_INV : CH_ZETA_INV], ch[(pass ? CH_ZETA_NEXT_INV : CH_ZETA_INV) + 1]};
     // local suffix sums within [lo, lo+per) of d_i = c_i z^i
     ext zp = gl::ext_pow(z, lo);
-    ext d[16];
+    ext d[MAXPER];
     for (uint32_t i = 0; i < per; i++) {
       d[i] = gl::ext_mul(ext{cc[lo + i], cc[n + lo + i]}, zp);
       zp = gl::ext_mul(zp, z);
@@ -1363,6 +1393,8 @@ __global__ void __launch_bounds__(1024) k_fri_divide(const uint64_t *__restrict_
     o[f_cstride + n - 1] = 0;
   }
 }
+template __global__ void k_fri_divide<16>(const uint64_t *, uint64_t *, uint32_t, const uint64_t *, uint64_t, uint64_t);
+template __global__ void k_fri_divide<64>(const uint64_t *, uint64_t *, uint32_t, const uint64_t *, uint64_t, uint64_t);
 
 // FRI layer leaves: leaf i = 2^ab consecutive leaf-order ext values, interleaved c0,c1
 __global__ void __launch_bounds__(256) k_fri_leaf(const uint64_t *__restrict__ vals, uint64_t *__restrict__ dig,

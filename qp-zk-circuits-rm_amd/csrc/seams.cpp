@@ -274,8 +274,8 @@ int qp_fri_layer_commit(qp_ctx *ctx, const uint64_t *coeffs, uint32_t log_coeffs
     }
   uint32_t lc = 1;
   while ((1ull << lc) < nz) lc++;
-  if (lc > 14) {  // the coset LDE's sizes (degree-2^14 aggregation circuits' layer 0)
-    ctx->err = "qp_fri_layer_commit: more than 2^14 nonzero coefficients";
+  if (lc > qpk::BIG_LOG_MAX) {  // the coset LDE's sizes
+    ctx->err = "qp_fri_layer_commit: more than 2^16 nonzero coefficients";
     return QP_ERR_ARG;
   }
   lc = std::min(lc, log_coeffs);

@@ -153,8 +153,9 @@ class _LevelProver:
         return out
 
 
-# the GPU prover's largest circuit: LDS-resident NTTs of n <= 2^14 (prover.cpp setup)
-GPU_MAX_DEGREE_BITS = 14
+# the GPU prover's largest circuit (prover.cpp setup): n <= 2^15, its LDE of
+# 2^18 points within the twiddle tables (n > 2^14 runs the HBM-level NTTs)
+GPU_MAX_DEGREE_BITS = 15
 
 _circuits = {}
 _circuits_lock = threading.Lock()
@@ -252,8 +253,9 @@ def aggregate_to_tree(leaf_proofs, common_data: bytes, verifier_only: bytes,
     previous level's circuit data, down to one root proof.  Every leaf's public
     inputs are registered at every level, so circuits grow with the depth (the
     root of 2048 leaves registers 32,768 and needs 2^15 rows): a level whose
-    circuit exceeds the GPU prover's 2^14 raises CircuitTooLarge carrying the
-    proofs of the level below (not with a CPU backend)."""
+    circuit exceeds the GPU prover's 2^GPU_MAX_DEGREE_BITS raises
+    CircuitTooLarge carrying the proofs of the level below (not with a CPU
+    backend)."""
     config = config or TreeAggregationConfig.default()
 
     def check(inner_common, proofs):

@@ -132,6 +132,24 @@ def _device_vs_host(circ, vo, chunks, zk=None):
     return dev, host, vd
 
 
+def test_degree15_aggregation_gpu_equals_oracle(reference_leaves):
+    """A degree-2^15 circuit (aggregate_chunk of five leaves; the root of a
+    2048-leaf tree is 2^15 rows too): transforms beyond one workgroup's LDS run
+    their first level in HBM (ntt.hip dif_big), Z's scan, the quotient iNTT and
+    FRI's divide have large-n forms; proof bytes == the oracle's, verified."""
+    import qp_wormhole
+    cb, vo, leaves = reference_leaves
+    chunk = [leaves[i % 2] for i in range(5)]
+    circ = qp_wormhole.Circuit.aggregation(cb, 5)
+    assert circ.degree_bits == 15
+    agg = qp_wormhole.aggregate_chunk(chunk, cb, vo)
+    w = circ.commit_proofs(vo, chunk)
+    ob, ovd = oracle_prove(circ, w.wires(), w.public_inputs())
+    assert agg.proof.to_bytes() == ob
+    assert agg.circuit_data.verifier_data() == ovd
+    assert verify(ovd, ob) == 0
+
+
 def test_device_witness_equals_host_witness_levels_1_and_2(reference_leaves):
     """The recursive verifier's generators on the device (Poseidon with swap,
     arithmetic, BaseSum, wire split, extension division, RandomAccess): proof

@@ -46,7 +46,8 @@ def test_poseidon_permute(ctx):
     assert len(bad) == 0, bad[:10]
 
 
-@pytest.mark.parametrize("log_n", [1, 3, 8, 10, 13, 14])
+# 15, 16: beyond one workgroup's LDS (HBM levels + 2^14-point LDS blocks)
+@pytest.mark.parametrize("log_n", [1, 3, 8, 10, 13, 14, 15, 16])
 def test_ifft(ctx, log_n):
     import qp_wormhole
     rng = np.random.default_rng(log_n)
@@ -58,7 +59,8 @@ def test_ifft(ctx, log_n):
         assert (got[c] == e).all()
 
 
-@pytest.mark.parametrize("log_n,rate_bits", [(2, 1), (5, 3), (10, 3), (13, 3), (12, 4), (11, 1), (11, 2), (13, 1), (10, 4), (14, 2)])
+@pytest.mark.parametrize("log_n,rate_bits", [(2, 1), (5, 3), (10, 3), (13, 3), (12, 4), (11, 1), (11, 2), (13, 1), (10, 4), (14, 2),
+                                            (15, 3), (16, 2), (15, 1)])
 def test_lde_leaf_order(ctx, log_n, rate_bits):
     import qp_wormhole
     rng = np.random.default_rng(100 + log_n)

@@ -89,6 +89,11 @@ for s in "$@"; do
              step coop_off 300 env QPGPU_WIT_COOP=0 python -u tools/agg_subtree.py 256 2 &&
              step coop_16 300 env QPGPU_WIT_COOP=16 python -u tools/agg_subtree.py 256 2 &&
              step coop_t512 300 env QPGPU_WIT_THREADS=512 python -u tools/agg_subtree.py 256 2 ;;
+    lde_mulk) for r in 1 2; do
+             step prof_lde86_def_$r 300 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/prof_lde86_def_$r -o run -- python3 tools/kbench.py 86 2 &&
+             step prof_lde86_mulk0_$r 300 env QPGPU_LIB=gpurun_ab/libqpgpu_mulk0.so rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/prof_lde86_mulk0_$r -o run -- python3 tools/kbench.py 86 2 &&
+             step prof_lde86_m1_$r 300 env QPGPU_LDE_MODE=1 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/prof_lde86_m1_$r -o run -- python3 tools/kbench.py 86 2 || exit 1
+           done ;;
     *) echo "unknown step $s" ;;
   esac
 done
