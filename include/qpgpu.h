@@ -309,11 +309,12 @@ int qp_prover_stage_times(qp_prover *p, double *ms, uint32_t n, int reset);
  * sequence).
  *
  * Shape limits (a call outside them returns QP_ERR_ARG with the reason in the
- * context's last error, never a wrong result): LDE domains up to 2^17 points
- * (log_n + rate_bits <= 17, i.e. circuits up to degree 2^14 at rate 3, the
- * aggregation circuits' size); qp_quotient: 2 challenges,
+ * context's last error, never a wrong result): commitments of up to 2^16
+ * values per polynomial with LDE domains up to 2^18 points (log_n + rate_bits
+ * <= 18, i.e. circuits up to degree 2^15 at rate 3, the top of a 2048-leaf
+ * aggregation tree); qp_quotient: degree <= 2^14, 2 challenges,
  * quotient_degree_factor == 2^rate_bits <= 16, at most 16 gates, unsalted
- * batches of one; qp_fri_layer_commit: at most 2^14 nonzero coefficients.                                                     */
+ * batches of one; qp_fri_layer_commit: at most 2^16 nonzero coefficients.                                                     */
 
 /* gate kinds of CommonCircuitData.gates (DefaultGateSerializer ids in brackets).
  * 0-5: the leaf circuits' gates (fast single-read quotient kernel); 6-13: the
@@ -364,7 +365,7 @@ int qp_quotient(qp_ctx *ctx, const qp_batch *cs, const qp_batch *wires, const qp
  * 2^arity_bits ext values, MerkleTree -> cap_out [2^cap_height][4].  coeffs are
  * ext coefficients as two rows [2][2^log_coeffs] (c0, c1); the reference keeps
  * them full length with a zero tail, so log_coeffs may equal log_values: only
- * the nonzero prefix (at most 2^14 coefficients) is transformed.  The caller
+ * the nonzero prefix (at most 2^16 coefficients) is transformed.  The caller
  * observes the cap, draws beta and calls qp_fri_fold; out (optional) keeps the
  * layer for qp_fri_layer_open in the query rounds.  A layer uses its context's
  * stream: free it (qp_fri_layer_free) before qp_ctx_destroy.                */

@@ -107,6 +107,7 @@ int qp_quotient(qp_ctx *ctx, const qp_batch *cs, const qp_batch *wires, const qp
   const uint32_t nterms = nc + nc * nchunks + g->num_gate_constraints;
   if (nc != 2 || g->num_gates == 0 || g->num_gates > QP_MAX_GATES || g->num_selectors == 0 ||
       g->num_selectors > QP_MAX_GATES || qdf != (1u << rb) || logN > qpk::TW_LOG || log_n < 6 ||
+      log_n > qpk::LDS_LOG_MAX ||
       nterms > qpk::APOW_STRIDE || wires->log_n != log_n || zs_pp->log_n != log_n || wires->rate_bits != rb ||
       zs_pp->rate_bits != rb || cs->nbat != 1 || wires->nbat != 1 || zs_pp->nbat != 1 ||
       cs->npolys != g->num_constants + R || wires->npolys != g->num_wires || zs_pp->npolys != nc * nchunks ||

@@ -94,6 +94,8 @@ for s in "$@"; do
              step prof_lde86_mulk0_$r 300 env QPGPU_LIB=gpurun_ab/libqpgpu_mulk0.so rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/prof_lde86_mulk0_$r -o run -- python3 tools/kbench.py 86 2 &&
              step prof_lde86_m1_$r 300 env QPGPU_LDE_MODE=1 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/prof_lde86_m1_$r -o run -- python3 tools/kbench.py 86 2 || exit 1
            done ;;
+    aggpmc_q) step pmc_agg_q 300 env QP_AGG_PROVERS=1 rocprofv3 --pmc SQ_WAVES SQ_INSTS_VALU SQ_ACTIVE_INST_VALU SQ_WAVE_CYCLES SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_BUSY_CYCLES SQ_WAIT_ANY --kernel-include-regex k_quotient --output-format csv -d gpurun_out/pmc_agg_q -o run -- python3 tools/agg_subtree.py 256 1 ;;
+    calib) step pmc_calib 600 bash tools/pmc_calib.sh ;;
     *) echo "unknown step $s" ;;
   esac
 done
