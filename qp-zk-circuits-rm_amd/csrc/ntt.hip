@@ -195,6 +195,14 @@ __global__ void __launch_bounds__(512) QP_NTT_OCC k_lde(const uint64_t *__restri
 // before and by the merged w_N^{t(s + B brev4(m))} (N words, 512 KiB at
 // n = 2^13, evicted by the streaming output) after the DFT.
 // The remaining levels run in LDS (ntt_lds_from); output rows in leaf order.
+// QP_LDE_MULK=0 (default): the coset LDE's twiddle products one at a time
+// rather than as interleaved triples (nt::mul_rows): fewer live temporaries at
+// the 128-VGPR cap (72 -> 48 B of spill per lane); 4.33 -> 4.18 ms per
+// 86-proof launch, while the iNTT keeps the triples (0.86 vs 0.93 ms;
+// profiles/r04_lde_ab.log)
+#ifndef QP_LDE_MULK
+#define QP_LDE_MULK 0
+#endif
 // MODE (QPGPU_LDE_MODE): 0 = MTW (default; measured 548 vs 701 us per
 // 64-column launch for mode 1 at n = 2^13, profiles/r04_lde_ab.log), 1 =
 // factored with both tables re-read per coset, 2 = factored with the coset
@@ -244,22 +252,22 @@ __global__ void __launch_bounds__(1 << LOG_T) QP_NTT_OCC k_lde_cosets(const uint
     if constexpr (MTW) {
 #pragma unroll
       for (int m = 0; m < 16; m++) r[m] = a[m];
-      nt::mul_rows(r, [&](int m) { return pw[16 * s + m]; });
+      nt::mul_rows<QP_LDE_MULK>(r, [&](int m) { return pw[16 * s + m]; });
       nt::dft16<false>(r);
       // merged twiddles w_N^{t(s + B brev4(m))}: row (s, m) of the table, lane t
       // (a product by w^0 = 1 returns its input unchanged)
       const uint64_t *ms = mtw + (uint64_t)16 * T * s + t;
       if (s) r[0] = nt::mul(r[0], ms[0]);
-      nt::mul_rows(r, [&](int m) { return ms[T * m]; });
+      nt::mul_rows<QP_LDE_MULK>(r, [&](int m) { return ms[T * m]; });
     } else {
       if (s) {
         // a_m w_N^{s(t+Tm)} from coset s - 1's registers
         if constexpr (MODE >= 2) {
           a[0] = nt::mul(a[0], hu[0]);
-          nt::mul_rows(a, [&](int m) { return hu[m]; });
+          nt::mul_rows<QP_LDE_MULK>(a, [&](int m) { return hu[m]; });
         } else {
           a[0] = nt::mul(a[0], ut[0]);
-          nt::mul_rows(a, [&](int m) { return ut[T * m]; });
+          nt::mul_rows<QP_LDE_MULK>(a, [&](int m) { return ut[T * m]; });
         }
       }
 #pragma unroll
@@ -267,9 +275,9 @@ __global__ void __launch_bounds__(1 << LOG_T) QP_NTT_OCC k_lde_cosets(const uint
       nt::dft16<false>(r);
       if (t) {
         if constexpr (MODE == 3)
-          nt::mul_rows(r, [&](int m) { return hp[m]; });
+          nt::mul_rows<QP_LDE_MULK>(r, [&](int m) { return hp[m]; });
         else
-          nt::mul_rows(r, [&](int m) { return p1[T * m]; });
+          nt::mul_rows<QP_LDE_MULK>(r, [&](int m) { return p1[T * m]; });
       }
     }
 #pragma unroll
@@ -282,7 +290,7 @@ __global__ void __launch_bounds__(1 << LOG_T) QP_NTT_OCC k_lde_cosets(const uint
     // the LDS passes (launched with T threads) leave exactly the G levels the
     // store loop runs
     static_assert(nt::lds_levels_left(LOG_N, LOG_T, T) == G, "LDS passes and the store loop disagree");
-    nt::ntt_lds_from<false, false>(lds, LOG_N, LOG_T, pt);
+    nt::ntt_lds_from<false, false, QP_LDE_MULK>(lds, LOG_N, LOG_T, pt);
     uint64_t *dst = dst0 + ((uint64_t)gl::rev_bits(s, rate_bits) << LOG_N);
     if constexpr (G == 0) {
 #pragma unroll

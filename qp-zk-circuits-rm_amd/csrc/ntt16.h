@@ -108,9 +108,9 @@ __device__ __forceinline__ uint64_t mul(uint64_t a, uint64_t b) {
 #ifndef QP_NTT_MULK
 #define QP_NTT_MULK 1
 #endif
-template <class TW>
+template <bool K = QP_NTT_MULK, class TW>
 __device__ __forceinline__ void mul_rows(uint64_t r[16], const TW &tw) {
-  if constexpr (QP_NTT_MULK) {
+  if constexpr (K) {
 #pragma unroll
     for (int m = 1; m < 16; m += 3) {
       const uint64_t a[3] = {r[m], r[m + 1], r[m + 2]}, b[3] = {tw(m), tw(m + 1), tw(m + 2)};
@@ -346,7 +346,9 @@ __host__ __device__ constexpr uint32_t lds_levels_left(uint32_t log_n, uint32_t 
   while (log_S >= 4) log_S = use_pass32(log_S, 1u << log_n, T) ? 1 : log_S - 4;
   return log_S;
 }
-template <bool INV, bool TAIL = true>
+// K: the pass twiddles as interleaved triples (mul_rows); the coset LDE uses
+// single products (QP_LDE_MULK)
+template <bool INV, bool TAIL = true, bool K = QP_NTT_MULK>
 __device__ __forceinline__ uint32_t ntt_lds_from(uint64_t *a, uint32_t log_n, uint32_t log_S, const uint64_t *__restrict__ pt) {
   const uint32_t n = 1u << log_n;
   const uint32_t T = blockDim.x;
@@ -367,7 +369,7 @@ __device__ __forceinline__ uint32_t ntt_lds_from(uint64_t *a, uint32_t log_n, ui
       dft16<INV>(r);
       if (t) {
         const uint64_t *ptS = pt + qpk::pt_offset(log_S) + t;
-        mul_rows(r, [&](int m) { return ptS[m * q]; });
+        mul_rows<K>(r, [&](int m) { return ptS[m * q]; });
       }
 #pragma unroll
       for (int m = 0; m < 16; m++) base[lp(m * q)] = r[m];

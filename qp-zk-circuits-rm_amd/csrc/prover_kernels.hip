@@ -316,6 +316,15 @@ __device__ __forceinline__ void poseidon_gate(const uint64_t *__restrict__ wl, u
   WireRead rd{wl, N, nullptr, 0};
   poseidon_gate_rd(rd, A);
 }
+// the generic kernel's Poseidon gate as a call (QP_QGEN_POS_CALL=1): its
+// permutation-sized live state gets its own register allocation instead of
+// adding to the gate loop's (inlined, k_quotient<2> spills 432 B per lane)
+#ifndef QP_QGEN_POS_CALL
+#define QP_QGEN_POS_CALL 0
+#endif
+__device__ __noinline__ void poseidon_gate_call(const uint64_t *__restrict__ wl, uint64_t N, TermAcc &A) {
+  poseidon_gate(wl, N, A);
+}
 
 template <class RD>
 __device__ __forceinline__ void poseidon_gate_rd(const RD &WR, TermAcc &A) {
@@ -643,7 +652,8 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(QP_QGE
     A.i = pre;
     const uint64_t *gc = cs + (uint64_t)nsel * N;
     if (kind == GK_POSEIDON) {
-      poseidon_gate(wl, N, A);
+      if constexpr (QP_QGEN_POS_CALL) poseidon_gate_call(wl, N, A);
+      else poseidon_gate(wl, N, A);
     } else {
       switch (kind) {
         case GK_CONSTANT:

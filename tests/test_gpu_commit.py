@@ -131,6 +131,8 @@ def test_commit_full_size_wires(ctx):
 
 
 def test_bad_shape_is_an_error(ctx):
+    """Beyond the twiddle tables (2^16 values at rate 3 = 2^19 points > 2^18):
+    an error with the reason, not a wrong result."""
     import qp_wormhole
     with pytest.raises(qp_wormhole.QpError):
-        qp_wormhole.PolynomialBatch.from_values(ctx, np.zeros((2, 1 << 15), np.uint64), 3, 4)
+        qp_wormhole.PolynomialBatch.from_values(ctx, np.zeros((2, 1 << 16), np.uint64), 3, 4)

@@ -96,6 +96,11 @@ for s in "$@"; do
            done ;;
     aggpmc_q) step pmc_agg_q 300 env QP_AGG_PROVERS=1 rocprofv3 --pmc SQ_WAVES SQ_INSTS_VALU SQ_ACTIVE_INST_VALU SQ_WAVE_CYCLES SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_BUSY_CYCLES SQ_WAIT_ANY --kernel-include-regex k_quotient --output-format csv -d gpurun_out/pmc_agg_q -o run -- python3 tools/agg_subtree.py 256 1 ;;
     calib) step pmc_calib 600 bash tools/pmc_calib.sh ;;
+    qgen_ab) for r in 1 2; do
+             step qgen_def_$r 300 python -u tools/agg_subtree.py 256 2 &&
+             step qgen_qpc_$r 300 env QPGPU_LIB=gpurun_ab/libqpgpu_qpc.so python -u tools/agg_subtree.py 256 2 &&
+             step qgen_qpc3_$r 300 env QPGPU_LIB=gpurun_ab/libqpgpu_qpc3.so python -u tools/agg_subtree.py 256 2 || exit 1
+           done ;;
     *) echo "unknown step $s" ;;
   esac
 done
