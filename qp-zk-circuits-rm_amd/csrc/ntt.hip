@@ -203,6 +203,9 @@ __global__ void __launch_bounds__(512) QP_NTT_OCC k_lde(const uint64_t *__restri
 #ifndef QP_LDE_MULK
 #define QP_LDE_MULK 0
 #endif
+#ifndef QP_LDE_ALDS
+#define QP_LDE_ALDS 0
+#endif
 // MODE (QPGPU_LDE_MODE): 0 = MTW (default; measured 548 vs 701 us per
 // 64-column launch for mode 1 at n = 2^13, profiles/r04_lde_ab.log), 1 =
 // factored with both tables re-read per coset, 2 = factored with the coset
@@ -237,6 +240,14 @@ __global__ void __launch_bounds__(1 << LOG_T) QP_NTT_OCC k_lde_cosets(const uint
   // first pass's twiddles w_n^{t brev4(m)}
   const uint64_t *ut = mtw + t, *p1 = pt + pt_offset(LOG_N) + t;
   constexpr bool MTW = MODE == 0;
+  // QP_LDE_ALDS = K > 0: the last K shifted coefficients live in LDS past the
+  // transform's words instead of VGPRs across the coset loop (fewer spills;
+  // the launch adds K*T*8 bytes of LDS)
+  uint64_t *alds = lds + ntt_lds_words(1u << LOG_N);
+  if constexpr (QP_LDE_ALDS > 0) {
+#pragma unroll
+    for (int m = 16 - QP_LDE_ALDS; m < 16; m++) alds[(m - (16 - QP_LDE_ALDS)) * T + t] = a[m];
+  }
   // coset-independent tables held in registers (modes 2 and 3)
   uint64_t hu[16], hp[16];
   if constexpr (MODE >= 2) {
@@ -251,7 +262,8 @@ __global__ void __launch_bounds__(1 << LOG_T) QP_NTT_OCC k_lde_cosets(const uint
     uint64_t r[16];
     if constexpr (MTW) {
 #pragma unroll
-      for (int m = 0; m < 16; m++) r[m] = a[m];
+      for (int m = 0; m < 16; m++)
+        r[m] = m >= 16 - QP_LDE_ALDS ? alds[(m - (16 - QP_LDE_ALDS)) * T + t] : a[m];
       nt::mul_rows<QP_LDE_MULK>(r, [&](int m) { return pw[16 * s + m]; });
       nt::dft16<false>(r);
       // merged twiddles w_N^{t(s + B brev4(m))}: row (s, m) of the table, lane t
@@ -511,7 +523,7 @@ void lde(const Twiddles &t, const uint64_t *coeffs, uint64_t c_stride, uint64_t 
       log_n + rate_bits <= TW_LOG &&
       !getenv_flag("QPGPU_LDE_PERCOSET")) {
     dim3 g(ncols, nbat);
-    const size_t lds_bytes = (size_t)8 * qpk::ntt_lds_words(1u << log_n);
+    const size_t lds_bytes = (size_t)8 * (qpk::ntt_lds_words(1u << log_n) + QP_LDE_ALDS * (1u << (log_n - 4)));
     if (QP_LDE_RADIX8 && log_n == 13) {
       const uint64_t shift_T8 = gl::pow(shift, 1u << (log_n - 3));
       k_lde_cosets8<10><<<g, 1024, lds_bytes, s>>>(coeffs, c_stride, c_bstride, out, o_stride, o_bstride, rate_bits,

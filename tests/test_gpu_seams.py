@@ -201,8 +201,8 @@ def test_fri_layer_matches_oracle(ctx, lnz, lbuf, lv, shift, ab, cap_h):
 def test_fri_layer_errors(ctx):
     import qp_wormhole
     rng = np.random.default_rng(5)
-    with pytest.raises(qp_wormhole.QpError, match="more than 2\\^14 nonzero coefficients"):
-        qp_wormhole.FriLayer(ctx, rand_felts(rng, 2, 1 << 15), 17, G, 2, 4)
+    with pytest.raises(qp_wormhole.QpError, match="more than 2\\^16 nonzero coefficients"):
+        qp_wormhole.FriLayer(ctx, rand_felts(rng, 2, 1 << 17), 18, G, 2, 4)
     with pytest.raises(qp_wormhole.QpError, match="QP_ERR_ARG"):
         qp_wormhole.FriLayer(ctx, rand_felts(rng, 2, 1 << 8), 7, G, 2, 4)  # values shorter than coeffs
     layer = qp_wormhole.FriLayer(ctx, rand_felts(rng, 2, 1 << 8), 10, G, 2, 4)

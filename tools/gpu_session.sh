@@ -101,6 +101,12 @@ for s in "$@"; do
              step qgen_qpc_$r 300 env QPGPU_LIB=gpurun_ab/libqpgpu_qpc.so python -u tools/agg_subtree.py 256 2 &&
              step qgen_qpc3_$r 300 env QPGPU_LIB=gpurun_ab/libqpgpu_qpc3.so python -u tools/agg_subtree.py 256 2 || exit 1
            done ;;
+    lde_alds) for r in 1 2; do
+             step prof_lde86b_def_$r 300 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/prof_lde86b_def_$r -o run -- python3 tools/kbench.py 86 2 &&
+             step prof_lde86b_alds3_$r 300 env QPGPU_LIB=gpurun_ab/libqpgpu_alds3.so rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/prof_lde86b_alds3_$r -o run -- python3 tools/kbench.py 86 2 &&
+             step prof_lde86b_alds2_$r 300 env QPGPU_LIB=gpurun_ab/libqpgpu_alds2.so rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/prof_lde86b_alds2_$r -o run -- python3 tools/kbench.py 86 2 || exit 1
+           done &&
+           step test_alds3 300 env QPGPU_LIB=gpurun_ab/libqpgpu_alds3.so python -u -m pytest tests/test_gpu_commit.py -x -q --timeout 120 --timeout-method thread ;;
     *) echo "unknown step $s" ;;
   esac
 done
