@@ -203,8 +203,12 @@ __global__ void __launch_bounds__(512) QP_NTT_OCC k_lde(const uint64_t *__restri
 #ifndef QP_LDE_MULK
 #define QP_LDE_MULK 0
 #endif
+// QP_LDE_ALDS=3 (default): the last 3 shifted coefficients in LDS past the
+// transform (12 KB per 8192-point workgroup: 2 still fit per CU); spill
+// 48 -> 12 B per lane, 4.11 -> 4.06 ms per 86-proof launch
+// (profiles/r04_lde_ab.log)
 #ifndef QP_LDE_ALDS
-#define QP_LDE_ALDS 0
+#define QP_LDE_ALDS 3
 #endif
 // MODE (QPGPU_LDE_MODE): 0 = MTW (default; measured 548 vs 701 us per
 // 64-column launch for mode 1 at n = 2^13, profiles/r04_lde_ab.log), 1 =
