@@ -107,6 +107,7 @@ for s in "$@"; do
              step prof_lde86b_alds2_$r 300 env QPGPU_LIB=gpurun_ab/libqpgpu_alds2.so rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/prof_lde86b_alds2_$r -o run -- python3 tools/kbench.py 86 2 || exit 1
            done &&
            step test_alds3 300 env QPGPU_LIB=gpurun_ab/libqpgpu_alds3.so python -u -m pytest tests/test_gpu_commit.py -x -q --timeout 120 --timeout-method thread ;;
+    agglog) step agg_subtree 300 python -u tools/agg_subtree.py 256 3 ;;
     *) echo "unknown step $s" ;;
   esac
 done
