@@ -128,6 +128,7 @@ struct qp_prover {
   uint32_t wg_nslots = 0, wg_nin = 0, wg_nlev = 0;
   bool quotient_rereads = false;
   bool quotient_fused = false;  // A/B: QPGPU_QUOTIENT=fused selects k_quotient_fused where it applies
+  bool quotient_onepass = false;  // A/B: QPGPU_QUOTIENT=onepass keeps k_quotient<2> for generic gate lists
   bool has_poseidon_gate = false;
   bool has_random_access = false;
   bool generic_quotient = false;  // a gate outside k_quotient_1r's set (the recursive verifier's RandomAccess)
@@ -419,6 +420,9 @@ int setup(qp_prover *P) {
     const char *qv = getenv("QPGPU_QUOTIENT");
     P->quotient_rereads = qv && !strcmp(qv, "rereads");
     P->quotient_fused = qv && !strcmp(qv, "fused");
+    // QPGPU_QUOTIENT=onepass: the generic gate list in one k_quotient<2> pass
+    // (A/B) instead of the per-gate launches
+    P->quotient_onepass = qv && !strcmp(qv, "onepass");
     const char *pv = getenv("QPGPU_PP_GENERIC");
     P->pp_generic = pv && pv[0] && pv[0] != '0';
   }
@@ -667,7 +671,23 @@ int prove_batch(qp_prover *P, const uint64_t *d_wires, const uint64_t *const *wi
     a.num_constants = P->NC;
     a.g = P->gdesc;
     kt_begin(P, 3);
-    if (P->quotient_rereads || P->generic_quotient)  // generic gate list (or A/B: QPGPU_QUOTIENT=rereads)
+    if (P->generic_quotient && !P->quotient_onepass && !P->quotient_rereads) {
+      // generic gate list: the permutation terms, then one launch per gate
+      // (k_quotient_part: each streams only its gate's columns), the last
+      // multiplying by 1/Z_H
+      const dim3 qg(cdiv(N, 256), nb);
+      int lastg = -1;
+      for (uint32_t gi = 0; gi < a.g.ngates; gi++)
+        if (a.g.kind[gi] != qpk::GK_NOOP) lastg = (int)gi;
+      qpk::k_quotient_part<0><<<qg, 256, 0, s>>>(a, 0, lastg < 0);
+      for (uint32_t gi = 0; gi < a.g.ngates; gi++) {
+        if (a.g.kind[gi] == qpk::GK_NOOP) continue;
+        if (a.g.kind[gi] == qpk::GK_POSEIDON)
+          qpk::k_quotient_part<2><<<qg, 256, 0, s>>>(a, gi, (int)gi == lastg);
+        else
+          qpk::k_quotient_part<1><<<qg, 256, 0, s>>>(a, gi, (int)gi == lastg);
+      }
+    } else if (P->quotient_rereads || P->generic_quotient)  // generic gate list (or A/B: QPGPU_QUOTIENT=rereads/onepass)
       qpk::k_quotient<2><<<dim3(cdiv(N, 256), nb), 256, 0, s>>>(a);
     else if (P->R == 80 && P->qdf == 8 && P->has_poseidon_gate && P->quotient_fused && !P->has_random_access)
       qpk::k_quotient_fused<<<dim3(cdiv(N, 256), nb), 256, 0, s>>>(a);

@@ -76,6 +76,8 @@ __global__ void k_quotient_1r(QuotientArgs a);
 // k_quotient_1r for R = 80 routed wires in chunks of 8 with the Poseidon gate:
 // the sweep rides on the gate's wire reads (every wire read once)
 __global__ void k_quotient_fused(QuotientArgs a);
+template <int PART>
+__global__ void k_quotient_part(QuotientArgs a, uint32_t gi, uint32_t last);
 __global__ void k_qintt_gather_big(const uint64_t *vals, uint64_t *out, uint32_t log_n, uint32_t rate_bits,
                                    uint64_t v_bstride, uint64_t o_bstride);
 __global__ void k_qintt_blocks(const uint64_t *vals, uint64_t *out, uint32_t log_n, uint32_t rate_bits,

@@ -1188,6 +1188,123 @@ k_quotient_fused(QuotientArgs a) {
   q[N + t] = gfn::canon(gfn::mul(acc1, zh_inv));
 }
 
+// ---- per-gate form of the generic quotient (QPGPU_QUOTIENT unset: the
+// default for gate lists outside the leaf set, i.e. the aggregation circuits).
+// The one-pass kernel above evaluates every gate per point and re-reads the
+// wires gate after gate: with 135 wires x 8 B per point and 1,024 points in
+// flight per CU the working set is far beyond L2, so every gate's reads come
+// from HBM again (30 GB per 32-proof level-1 launch, 6.6x the distinct
+// values, 432 B of spill per lane; profiles/r04_pmc_hbm_b128.json).  Here one
+// launch writes the L_0 and partial-product terms, then one launch per gate
+// streams only that gate's columns and adds its filtered alpha sum to the
+// point's accumulators; the last one multiplies by 1/Z_H.  Same sums (the
+// alpha-weighted terms do not depend on evaluation order), so the output is
+// bit-identical.  PART 0: permutation terms; 1: one non-Poseidon gate; 2: the
+// Poseidon gate.
+template <int PART>
+__global__ void __launch_bounds__(256) k_quotient_part(QuotientArgs a, uint32_t gi, uint32_t last) {
+  const uint32_t logN = a.log_n + a.rate_bits;
+  const uint64_t N = 1ull << logN;
+  const uint32_t t = blockIdx.x * blockDim.x + threadIdx.x;
+  if (t >= N) return;
+  const uint32_t b = blockIdx.y;
+  const uint64_t *ch = a.chal + b * CHAL_STRIDE;
+  const uint64_t *cs = a.cs_lde + t;
+  const uint64_t *wl = a.w_lde + b * a.w_bstride + t;
+  const uint64_t *zl = a.z_lde + b * a.z_bstride;
+  uint64_t *q = a.q_out + b * a.q_bstride;
+  TermAcc A;
+  A.p0 = a.apow + (uint64_t)b * 2 * APOW_STRIDE;
+  A.p1 = A.p0 + APOW_STRIDE;
+  A.s0 = A.s1 = 0;
+  A.i = 0;
+  const uint32_t R = a.R, qdf = a.qdf, nchunks = (R + qdf - 1) / qdf, npp = nchunks - 1;
+  uint64_t acc0, acc1;
+  if constexpr (PART == 0) {
+    const uint32_t j = gl::rev_bits(t, logN);
+    const uint32_t tn = gl::rev_bits((j + (1u << a.rate_bits)) & (uint32_t)(N - 1), logN);
+    const uint64_t x = a.xtab[t];
+    const uint64_t l0 = a.l0tab[t];
+    for (uint32_t c = 0; c < 2; c++) A.emit(gfn::mul(l0, gfn::sub(zl[(uint64_t)c * N + t], 1)));
+    for (uint32_t c = 0; c < 2; c++) {
+      const uint64_t beta = ch[CH_BETA + c], gamma = ch[CH_GAMMA + c];
+      uint64_t bkx = gfn::mul(beta, x);
+      for (uint32_t k = 0; k < nchunks; k++) {
+        uint64_t num = 1, den = 1;
+        for (uint32_t jj = k * qdf; jj < (k + 1) * qdf && jj < R; jj++) {
+          const uint64_t wv = WV(jj);
+          const uint64_t wg = gfn::add_c(wv, gamma);
+          num = gfn::mul(num, gfn::add(wg, bkx));
+          den = gfn::mul(den, gfn::add(wg, gfn::mul(beta, cs[(uint64_t)(a.num_constants + jj) * N])));
+          bkx = gfn::mul(bkx, gl::GEN);
+        }
+        const uint64_t prev = k == 0 ? zl[(uint64_t)c * N + t] : zl[((uint64_t)2 + c * npp + k - 1) * N + t];
+        const uint64_t next = k == nchunks - 1 ? zl[(uint64_t)c * N + tn] : zl[((uint64_t)2 + c * npp + k) * N + t];
+        A.emit(gfn::sub(gfn::mul(prev, num), gfn::mul(next, den)));
+      }
+    }
+    acc0 = A.s0;
+    acc1 = A.s1;
+  } else {
+    const uint32_t kind = a.g.kind[gi];
+    const uint32_t si = a.g.sel_index[gi], nsel = a.g.nsel;
+    const uint64_t sv = cs[(uint64_t)si * N];
+    uint64_t f = 1;
+    for (uint32_t jj = a.g.grp_lo[si]; jj < a.g.grp_hi[si]; jj++)
+      if (jj != gi) f = gfn::mul(f, gfn::sub(jj, sv));
+    if (nsel > 1) f = gfn::mul(f, gfn::sub(0xFFFFFFFFull, sv));
+    A.i = 2 * (1 + nchunks);
+    const uint64_t *gc = cs + (uint64_t)nsel * N;
+    if constexpr (PART == 2) {
+      poseidon_gate(wl, N, A);
+    } else {
+      switch (kind) {
+        case GK_CONSTANT:
+          for (uint32_t i = 0; i < a.g.param[gi]; i++) A.emit(gfn::sub(gc[(uint64_t)i * N], WV(i)));
+          break;
+        case GK_PUBLIC_INPUT:
+          for (uint32_t i = 0; i < 4; i++) A.emit(gfn::sub(WV(i), ch[CH_PIH + i]));
+          break;
+        case GK_BASE_SUM: {
+          const uint32_t L = a.g.param[gi];
+          uint64_t acc = 0;
+          for (uint32_t i = L; i-- > 0;) acc = gfn::add(gfn::add(acc, acc), WV(1 + i));
+          A.emit(gfn::sub(acc, WV(0)));
+          for (uint32_t i = 0; i < L; i++) {
+            const uint64_t l = WV(1 + i);
+            A.emit(gfn::mul(l, gfn::sub(l, 1)));
+          }
+          break;
+        }
+        case GK_ARITHMETIC:
+          for (uint32_t i = 0; i < a.g.param[gi]; i++) {
+            const uint64_t comp = gfn::add(gfn::mul(gfn::mul(WV(4 * i), WV(4 * i + 1)), gc[0]),
+                                           gfn::mul(WV(4 * i + 2), gc[N]));
+            A.emit(gfn::sub(WV(4 * i + 3), comp));
+          }
+          break;
+        default:
+          recursion_gate(kind, a.g.param[gi], a.g.param2[gi], a.g.param3[gi], wl, gc, N, A);
+          break;
+      }
+    }
+    acc0 = gfn::add(q[t], gfn::mul(f, A.s0));
+    acc1 = gfn::add(q[N + t], gfn::mul(f, A.s1));
+  }
+  if (last) {
+    const uint32_t j = gl::rev_bits(t, logN);
+    const uint64_t zh_inv = a.zh_inv[j & ((1u << a.rate_bits) - 1)];
+    q[t] = gfn::canon(gfn::mul(acc0, zh_inv));
+    q[N + t] = gfn::canon(gfn::mul(acc1, zh_inv));
+  } else {
+    q[t] = acc0;
+    q[N + t] = acc1;
+  }
+}
+template __global__ void k_quotient_part<0>(QuotientArgs, uint32_t, uint32_t);
+template __global__ void k_quotient_part<1>(QuotientArgs, uint32_t, uint32_t);
+template __global__ void k_quotient_part<2>(QuotientArgs, uint32_t, uint32_t);
+
 template __global__ void k_quotient<0>(QuotientArgs);
 template __global__ void k_quotient<1>(QuotientArgs);
 template __global__ void k_quotient<2>(QuotientArgs);

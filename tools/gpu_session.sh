@@ -108,6 +108,10 @@ for s in "$@"; do
            done &&
            step test_alds3 300 env QPGPU_LIB=gpurun_ab/libqpgpu_alds3.so python -u -m pytest tests/test_gpu_commit.py -x -q --timeout 120 --timeout-method thread ;;
     agglog) step agg_subtree 300 python -u tools/agg_subtree.py 256 3 ;;
+    qpart_ab) for r in 1 2; do
+             step qpart_def_$r 300 python -u tools/agg_subtree.py 256 2 &&
+             step qpart_onepass_$r 300 env QPGPU_QUOTIENT=onepass python -u tools/agg_subtree.py 256 2 || exit 1
+           done ;;
     *) echo "unknown step $s" ;;
   esac
 done
