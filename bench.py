@@ -86,11 +86,12 @@ def pmc_traffic(kernel, ncols, log_n, proofs, lanes_per_proof=None):
 
 def mix_ceiling(ceil):
     """k_leaf_hash's issue ceiling (tools/issue_ceiling.py): its instruction mix at
-    the measured per-class costs, re-priced at the kernel's own clock when the
-    profile has it."""
+    the measured per-class costs, at the calibration streams' clock (≈2.38 GHz;
+    the bench's HIP-event rate has no clock reading, and the kernel runs near
+    that clock outside counter passes)."""
     if not ceil:
         return None
-    return ceil.get("ceiling_at_leaf_clock_wave_instr_per_s") or ceil["ceiling_wave_instr_per_s"]
+    return ceil["ceiling_wave_instr_per_s"]
 
 
 def profile_stamp(path):
@@ -127,7 +128,8 @@ def segregate_profile_fields(rec):
     check(PMC_FILE, rec.get("valu_kernels"), ["quotient_hbm_bytes_per_launch"], "valu_kernels")
     dk = rec.get("dominant_kernel")
     check(PMC_SQ_FILE, dk, ["instr_per_perm", "achieved", "frac", "frac_of_mix_ceiling"], "dominant_kernel")
-    check(CEIL_FILE, dk, ["mix_ceiling", "frac_of_mix_ceiling"], "dominant_kernel")
+    check(CEIL_FILE, dk, ["mix_ceiling", "frac_of_mix_ceiling", "frac_of_mix_ceiling_at_own_clock",
+                          "own_clock_ghz_in_counter_pass"], "dominant_kernel")
     check(KSUM1_FILE, dk, ["share_of_kernel_time"], "dominant_kernel")
     check(KSUM_FILE, rec.get("gpu_busy_frac"), ["value"], "gpu_busy_frac")
     rec["profile_build"] = {"lib_sha16": mine, "all_profiles_of_this_build": not moved}
@@ -596,10 +598,12 @@ def main():
                 "achieved": ach, "peak": VALU_PEAK_WAVE_INSTR_S, "unit": "wave-instructions/s",
                 "frac": ach / VALU_PEAK_WAVE_INSTR_S, "instr_per_perm": ipp,
                 "mix_ceiling": mix_ceiling(ceil),
-                "mix_ceiling_priced_at": ("the leaf hash's own clock (GRBM_GUI_ACTIVE per dispatch)"
-                                          if ceil and ceil.get("ceiling_at_leaf_clock_wave_instr_per_s")
-                                          else "the calibration kernels' clocks") if ceil else None,
+                "mix_ceiling_priced_at": "the calibration streams' clock" if ceil else None,
                 "frac_of_mix_ceiling": ach / mix_ceiling(ceil) if ceil else None,
+                # clock-consistent: the kernel's VALU rate and its ceiling re-priced
+                # at its own clock, both from the same counter-pass dispatches
+                "frac_of_mix_ceiling_at_own_clock": ceil.get("frac_of_ceiling_in_counter_pass") if ceil else None,
+                "own_clock_ghz_in_counter_pass": ceil.get("leaf_hash_clock_ghz") if ceil else None,
                 "sources": {"instr_per_perm": os.path.relpath(PMC_SQ_FILE, ROOT),
                             "mix_ceiling": os.path.relpath(CEIL_FILE, ROOT) if ceil else None,
                             "share": os.path.relpath(KSUM1_FILE, ROOT) if ksum1 else None,

@@ -9,7 +9,11 @@ kernel's static instruction mix (one permutation = the absorb-loop body) is
 read from its gfx950 assembly; the ceiling is the mix's issue time with every
 instruction at its class cost, plus its hazard s_nops at their measured cost.
 With a counter pass of tools/kbench.py (third argument) the class costs are
-re-priced at the leaf hash's own clock (GRBM_GUI_ACTIVE per dispatch).
+re-priced at the leaf hash's own clock (GRBM_GUI_ACTIVE per dispatch), and the
+kernel's own VALU rate in that pass (same dispatches, same clock) gives the
+clock-consistent fraction of the ceiling.  The counter pass itself runs the
+kernel at a lower clock than the bench (≈2.0 vs ≈2.4 GHz), so the bench's
+HIP-event rate is compared with the ceiling at the calibration clock.
 Usage: python tools/issue_ceiling.py gpurun_out/calib_isa out.json [gpurun_out/calib_kb]"""
 import collections
 import csv
@@ -68,15 +72,27 @@ def class_costs(d):
             "s_nop": c["mad_nop"] - c["mad"], "measured": c, "clock_ghz": clk}
 
 
+def leaf_dispatches(d):
+    xs = [x for x in dispatches(d).values() if x["k"].endswith("k_leaf_hash")]
+    if not xs:
+        return []
+    g = max(x["grid"] for x in xs)
+    return [x for x in xs if x["grid"] == g and clock_ghz(x)]
+
+
 def leaf_clock(d):
     """Clock of the k_leaf_hash dispatches (the wires leaf hash: the largest grid)
     in a counter pass of tools/kbench.py with the same GRBM counters."""
-    xs = [x for x in dispatches(d).values() if x["k"].endswith("k_leaf_hash")]
-    if not xs:
-        return None
-    g = max(x["grid"] for x in xs)
-    ck = [clock_ghz(x) for x in xs if x["grid"] == g and clock_ghz(x)]
+    ck = [clock_ghz(x) for x in leaf_dispatches(d)]
     return sum(ck) / len(ck) if ck else None
+
+
+def leaf_rate_in_pass(d):
+    """The same dispatches' VALU issue rate (SQ_INSTS_VALU wave-instructions
+    over their duration): measured at the clock leaf_clock reports, so it
+    compares with the ceiling priced at that clock with no clock assumption."""
+    xs = [x for x in leaf_dispatches(d) if x.get("SQ_INSTS_VALU")]
+    return sum(x["SQ_INSTS_VALU"] / (x["ns"] * 1e-9) for x in xs) / len(xs) if xs else None
 
 
 def static_mix():
@@ -110,6 +126,7 @@ def main():
     # it at the leaf hash's own clock (cycles are what an instruction costs;
     # the clock under DVFS differs between kernels, MI355X_MICROARCH.md)
     lclk = leaf_clock(sys.argv[3]) if len(sys.argv) > 3 else None
+    lrate = leaf_rate_in_pass(sys.argv[3]) if len(sys.argv) > 3 else None
     t_leaf = None
     if lclk:
         ck = cost["clock_ghz"]
@@ -128,6 +145,10 @@ def main():
         "ceiling_wave_instr_per_s": n_valu / (t * 1e-9) * 1024,
         "leaf_hash_clock_ghz": lclk,
         "ceiling_at_leaf_clock_wave_instr_per_s": n_valu / (t_leaf * 1e-9) * 1024 if t_leaf else None,
+        # the kernel's own rate in the same counter pass (same clock as the
+        # line above): the clock-consistent fraction of its ceiling
+        "leaf_rate_in_counter_pass_wave_instr_per_s": lrate,
+        "frac_of_ceiling_in_counter_pass": lrate / (n_valu / (t_leaf * 1e-9) * 1024) if (lrate and t_leaf) else None,
         "sources": {"class costs": "tools/pmc_calib.sh counter pass over tools/isa_chains (8 waves/SIMD)",
                     "mix": "hipcc -S of csrc/merkle.hip (this tree)",
                     "s_nop": "mad+s_nop 0 block minus mad block (same pass)"},
