@@ -112,6 +112,8 @@ for s in "$@"; do
              step qpart_def_$r 300 python -u tools/agg_subtree.py 256 2 &&
              step qpart_onepass_$r 300 env QPGPU_QUOTIENT=onepass python -u tools/agg_subtree.py 256 2 || exit 1
            done ;;
+    qpart_prof) step prof_qpart 300 env QP_AGG_PROVERS=1 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/prof_qpart -o run -- python3 tools/agg_subtree.py 256 1 &&
+                step prof_qone 300 env QP_AGG_PROVERS=1 QPGPU_QUOTIENT=onepass rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/prof_qone -o run -- python3 tools/agg_subtree.py 256 1 ;;
     *) echo "unknown step $s" ;;
   esac
 done
