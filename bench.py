@@ -74,7 +74,10 @@ def pmc_traffic(kernel, ncols, log_n, proofs, lanes_per_proof=None):
     except (OSError, ValueError):
         return None
     for r in recs:
-        if r.get("kernel") != kernel or not r.get("hbm_bytes"):
+        # template arguments beyond the first (e.g. k_lde_cosets<9, 0>'s twiddle mode) do not matter
+        name = r.get("kernel") or ""
+        if (name != kernel and not (kernel.endswith(">") and name.startswith(kernel[:-1] + ","))) \
+                or not r.get("hbm_bytes"):
             continue
         if lanes_per_proof is None:
             lanes_per_proof = ncols * (1 << log_n) // 16  # one 2^(log_n - 4)-lane workgroup per column
