@@ -119,6 +119,27 @@ def test_deep_subtree_root_carries_every_leaf_public_input(reference_leaves):
     assert root.proof.public_inputs == want
 
 
+def test_tree_of_2048_leaves_reaches_a_degree15_root(reference_leaves):
+    """configs[3] at N = 8 on one GPU: 2048 leaves (the reference's two proofs)
+    through 11 levels to one root; the top circuit registers 32,768 public
+    inputs and is 2^15 rows (the large-transform path), the root verifies and
+    carries every leaf's public inputs in order."""
+    import struct
+    import qp_wormhole
+    from qp_wormhole.aggregator import TreeAggregationConfig
+    from qp_wormhole.prover import _common_degree_bits
+    cb, vo, leaves = reference_leaves
+    ls = [leaves[k % 2] for k in range(2048)]
+    root = qp_wormhole.aggregate_to_tree(ls, cb, vo, TreeAggregationConfig.new(2, 11))
+    assert _common_degree_bits(root.circuit_data.common) == 15
+    assert verify(root.circuit_data.verifier_data(), root.proof.to_bytes()) == 0
+    pis = root.proof.public_inputs
+    assert len(pis) == 32768
+    for k in (0, 1, 2047):
+        pf = ls[k]
+        assert pis[16 * k:16 * k + 16] == list(struct.unpack_from("<16Q", pf, len(pf) - 128))
+
+
 def _device_vs_host(circ, vo, chunks, zk=None):
     """qp_prover_prove_aggregation (witness generated on the device) vs the host
     witness path (qp_aggregation_commit + qp_prover_prove) of the same chunks."""
