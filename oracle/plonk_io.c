@@ -295,7 +295,7 @@ int or_parse_proof(const uint8_t *buf, size_t len, const or_common_t *c, or_proo
     for (unsigned i = 0; i < d.final_poly_len; i++) p->final_poly[i] = rd_fx(&r);
     p->pow_witness = rd_fe(&r);
     p->num_pis = rd_u64(&r);
-    if (p->num_pis > 4096) r.err = 7;
+    if (p->num_pis > (1u << 20)) r.err = 7;  /* sanity bound (a 2048-leaf root carries 32,768) */
     if (!r.err) {
         free(p->pis);
         p->pis = xcalloc(p->num_pis, 8);
