@@ -157,6 +157,15 @@ int qp_circuit_info(const qp_circuit *c, uint32_t *info);
  * per device-witness level, info word 8 levels) = the generators of each
  * dependency level by kind.  Test/diagnostic entry point.                   */
 int qp_circuit_census(const qp_circuit *c, uint32_t *gens, uint32_t *rows, uint32_t *level_gens);
+/* the device witness's host part: gens[k] (14 words, GenKind order as above)
+ * = generators the host runs before the device schedule (Poseidon chains over
+ * inputs alone at least 64 permutations deep -- the public-input hashes and
+ * the transcript sponges behind them -- with the constants they read);
+ * *slots = value slots set on the host (commit()'s inputs and those chains'
+ * outputs); *chains (may be null) = independent chains among them (a batch
+ * smaller than the host pool runs them in parallel).  Test/diagnostic entry
+ * point.                                                                      */
+int qp_circuit_host_chains(const qp_circuit *c, uint32_t *gens, uint32_t *slots, uint32_t *chains);
 /* CommonCircuitData::to_bytes (plonky2 util/serialization.rs) */
 int qp_circuit_common_data(const qp_circuit *c, uint8_t *out, size_t cap, size_t *len);
 /* preprocessed constants||sigmas values over H, [num_constants+num_routed][n] */

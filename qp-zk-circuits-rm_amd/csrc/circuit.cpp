@@ -12,6 +12,8 @@
 #include <algorithm>
 #include <numeric>
 #include <stdexcept>
+#include <unordered_map>
+#include <stdlib.h>
 #include <string.h>
 #include "field.h"
 #include "poseidon.h"
@@ -661,20 +663,11 @@ CircuitData CircuitBuilder::build() {
           cd.input_slots.push_back(s);
         }
       }
-      std::sort(cd.input_slots.begin(), cd.input_slots.end());
-      const uint32_t INF = 0xFFFFFFFFu;
-      std::vector<uint32_t> avail(nslots, INF);
-      avail[0] = 0;
-      for (uint32_t s : cd.input_slots) avail[s] = 0;
-      std::vector<uint32_t> lvl(cd.schedule.size());
-      uint32_t nlev = 0;
-      // writers per slot (saturating at 2): host-set slots count as one
-      std::vector<uint8_t> nwr(nslots, 0);
-      for (uint32_t s : cd.input_slots) nwr[s] = 1;
-      for (uint32_t s : cd.zk_slots) nwr[s] = 1;
-      for (size_t i = 0; i < cd.schedule.size(); i++) {
+      const size_t ng = cd.schedule.size();
+      std::vector<std::vector<uint32_t>> rds(ng), wrs(ng);
+      for (size_t i = 0; i < ng; i++) {
         const Gen &g = cd.schedule[i];
-        std::vector<uint32_t> rd, wr;
+        std::vector<uint32_t> &rd = rds[i], &wr = wrs[i];
         switch (g.kind) {
           case GEN_CONSTANT: wr = {g.s[0], g.s[1]}; break;
           case GEN_ARITH: rd = {g.s[0], g.s[1], g.s[2]}; wr = {g.s[3]}; break;
@@ -711,14 +704,117 @@ CircuitData CircuitBuilder::build() {
             break;
           }
         }
+      }
+      // host chains (CircuitData::host_gens): forward, the Poseidon (and
+      // constant) generators computable from inputs alone with their chain
+      // depth in permutations; backward, those at least tmin deep and every
+      // such generator feeding one
+      uint32_t tmin = HOST_CHAIN_MIN;
+      if (const char *e = getenv("QPGPU_HOST_CHAIN")) tmin = (uint32_t)strtoul(e, nullptr, 10);
+      std::vector<uint8_t> on_host(ng, 0);
+      if (tmin) {
+        std::vector<uint8_t> hostable(ng, 0), hw(nslots, 0), need(nslots, 0);
+        std::vector<uint32_t> depth(ng, 0), sdepth(nslots, 0);
+        for (size_t i = 0; i < ng; i++) {
+          const uint32_t k = cd.schedule[i].kind;
+          if (k != GEN_POSEIDON && k != GEN_CONSTANT) continue;
+          bool ok = true;
+          uint32_t d = 0;
+          for (uint32_t s : rds[i]) {
+            if (s && !is_in[s] && !hw[s]) {
+              ok = false;
+              break;
+            }
+            d = std::max(d, sdepth[s]);
+          }
+          if (!ok) continue;
+          hostable[i] = 1;
+          depth[i] = d + (k == GEN_POSEIDON ? 1 : 0);
+          for (uint32_t s : wrs[i])
+            if (s) {
+              hw[s] = 1;
+              sdepth[s] = std::max(sdepth[s], depth[i]);
+            }
+        }
+        for (size_t i = ng; i-- > 0;) {
+          if (!hostable[i]) continue;
+          bool take = depth[i] >= tmin;
+          for (uint32_t s : wrs[i]) take = take || (s && need[s]);
+          if (!take) continue;
+          on_host[i] = 1;
+          for (uint32_t s : rds[i]) need[s] = 1;
+        }
+        // segments: the constants first (every chain reads them), then the
+        // independent chains -- union-find over slots one host generator
+        // writes and another reads or writes -- each in schedule order
+        std::vector<uint32_t> uf(ng), writer(nslots, UINT32_MAX);
+        std::iota(uf.begin(), uf.end(), 0u);
+        auto find = [&](uint32_t x) {
+          while (uf[x] != x) x = uf[x] = uf[uf[x]];
+          return x;
+        };
+        std::vector<uint32_t> cons;
+        for (size_t i = 0; i < ng; i++) {
+          if (!on_host[i]) continue;
+          for (uint32_t s : wrs[i])
+            if (s && !is_in[s]) {
+              is_in[s] = 1;
+              cd.input_slots.push_back(s);
+            }
+          if (cd.schedule[i].kind == GEN_CONSTANT) {
+            cons.push_back((uint32_t)i);
+            continue;
+          }
+          for (uint32_t s : rds[i])
+            if (s && writer[s] != UINT32_MAX) uf[find((uint32_t)i)] = find(writer[s]);
+          for (uint32_t s : wrs[i])
+            if (s) {
+              if (writer[s] != UINT32_MAX) uf[find((uint32_t)i)] = find(writer[s]);
+              writer[s] = (uint32_t)i;
+            }
+        }
+        cd.host_gens = cons;
+        cd.host_seg_off = {0, (uint32_t)cons.size()};
+        std::vector<uint32_t> roots;
+        std::vector<std::vector<uint32_t>> segs;
+        std::unordered_map<uint32_t, uint32_t> seg_of;
+        for (size_t i = 0; i < ng; i++) {
+          if (!on_host[i] || cd.schedule[i].kind == GEN_CONSTANT) continue;
+          const uint32_t r = find((uint32_t)i);
+          auto it = seg_of.find(r);
+          if (it == seg_of.end()) {
+            it = seg_of.emplace(r, (uint32_t)segs.size()).first;
+            segs.emplace_back();
+          }
+          segs[it->second].push_back((uint32_t)i);
+        }
+        for (auto &sg : segs) {
+          cd.host_gens.insert(cd.host_gens.end(), sg.begin(), sg.end());
+          cd.host_seg_off.push_back((uint32_t)cd.host_gens.size());
+        }
+        if (cd.host_gens.empty()) cd.host_seg_off.clear();
+      }
+      std::sort(cd.input_slots.begin(), cd.input_slots.end());
+      const uint32_t INF = 0xFFFFFFFFu;
+      std::vector<uint32_t> avail(nslots, INF);
+      avail[0] = 0;
+      for (uint32_t s : cd.input_slots) avail[s] = 0;
+      std::vector<uint32_t> lvl(ng, INF);
+      uint32_t nlev = 0;
+      // writers per slot (saturating at 2): host-set slots count as one
+      std::vector<uint8_t> nwr(nslots, 0);
+      for (uint32_t s : cd.input_slots) nwr[s] = 1;
+      for (uint32_t s : cd.zk_slots) nwr[s] = 1;
+      for (size_t i = 0; i < ng; i++) {
+        if (on_host[i]) continue;
         uint32_t l = 0;
-        for (uint32_t s : rd) {
+        for (uint32_t s : rds[i]) {
           if (avail[s] == INF) throw std::runtime_error("device witness schedule: input not available");
           l = std::max(l, avail[s]);
         }
         lvl[i] = l;
         nlev = std::max(nlev, l + 1);
-        for (uint32_t s : wr) {
+        for (uint32_t s : wrs[i]) {
           if (s) avail[s] = std::min(avail[s], l + 1);
           if (nwr[s] < 2) nwr[s]++;
         }
@@ -732,14 +828,16 @@ CircuitData CircuitBuilder::build() {
       cd.dev_wslot.resize(cd.wire_slot.size());
       for (size_t i = 0; i < cd.wire_slot.size(); i++) cd.dev_wslot[i] = flag(cd.wire_slot[i]);
       cd.level_off.assign(nlev + 1, 0);
-      for (uint32_t l : lvl) cd.level_off[l + 1]++;
+      for (uint32_t l : lvl)
+        if (l != INF) cd.level_off[l + 1]++;
       for (uint32_t l = 0; l < nlev; l++) cd.level_off[l + 1] += cd.level_off[l];
       std::vector<uint32_t> fill(cd.level_off.begin(), cd.level_off.end() - 1);
-      cd.dev_gens.resize(cd.schedule.size());
+      cd.dev_gens.resize(ng - cd.host_gens.size());
       // within a level, generators of one kind are contiguous (a wave then runs
       // one switch arm instead of serialising several)
-      std::vector<uint32_t> order(cd.schedule.size());
-      for (size_t i = 0; i < order.size(); i++) order[i] = (uint32_t)i;
+      std::vector<uint32_t> order;
+      for (size_t i = 0; i < ng; i++)
+        if (!on_host[i]) order.push_back((uint32_t)i);
       std::stable_sort(order.begin(), order.end(), [&](uint32_t x, uint32_t y) {
         return lvl[x] != lvl[y] ? lvl[x] < lvl[y] : cd.schedule[x].kind < cd.schedule[y].kind;
       });
@@ -885,17 +983,8 @@ Witness::Witness(const CircuitData &cd, F *vals) : cd_(cd), known_(cd.num_slots,
 
 bool Witness::set_slot(uint32_t s, F v) {
   v = gl::canon(v);
-  if (!s) {  // the shared zero slot is never settable
-    conflict_ = true;
-    return false;
-  }
-  if (known_[s]) {
-    if (vals_[s] != v) {
-      conflict_ = true;
-      return false;
-    }
-    return true;
-  }
+  if (!s) return false;  // the shared zero slot is never settable
+  if (known_[s]) return vals_[s] == v;
   known_[s] = 1;
   vals_[s] = v;
   return true;
@@ -971,11 +1060,26 @@ inline F inv_diff(F x, F y) {
 }  // namespace
 
 bool Witness::generate(std::string &err) {
+  for (const Gen &g : cd_.schedule)
+    if (!run(g, err)) return false;
+  return true;
+}
+
+bool Witness::generate_host_chains(std::string &err, int seg) {
+  const auto &off = cd_.host_seg_off;
+  if (off.empty()) return true;
+  const uint32_t lo = seg < 0 ? 0 : off[seg], hi = seg < 0 ? off.back() : off[seg + 1];
+  for (uint32_t k = lo; k < hi; k++)
+    if (!run(cd_.schedule[cd_.host_gens[k]], err)) return false;
+  return true;
+}
+
+bool Witness::run(const Gen &g, std::string &err) {
   const uint32_t W = cd_.config.num_wires;
   const uint32_t L = cd_.config.num_routed_wires - 1 < 63 ? cd_.config.num_routed_wires - 1 : 63;
   const uint32_t zslot = cd_.zero_const_slot;
   F *v = vals_;
-  for (const Gen &g : cd_.schedule) {
+  {
     bool ok = true;
     switch (g.kind) {
       case GEN_CONSTANT:

@@ -155,6 +155,10 @@ struct Gen {
 // slot ids in DevGen and CircuitData::dev_wslot carry DEV_MULTI when the slot
 // has more than one writer (or is the shared zero slot)
 constexpr uint32_t DEV_MULTI = 0x80000000u;
+// device witness: Poseidon chains over inputs alone at least this many
+// permutations deep run on the host (CircuitData::host_gens; the environment
+// variable QPGPU_HOST_CHAIN overrides, 0 = none)
+constexpr uint32_t HOST_CHAIN_MIN = 64;
 struct DevGen {
   uint32_t kind, row;
   uint32_t s[4];
@@ -190,7 +194,21 @@ struct CircuitData {
   std::vector<uint32_t> pi_slots;       // public input slots (in order)
   std::vector<uint32_t> virt_slot;      // virtual target index -> slot
   uint32_t zero_const_slot = 0;         // slot of builder.zero() (0 if the circuit has none)
-  std::vector<uint32_t> input_slots;    // distinct slots of the targets commit() sets
+  // distinct slots set on the host before the device schedule runs: the
+  // targets commit() sets, then the outputs of host_gens
+  std::vector<uint32_t> input_slots;
+  // generators the host runs for the device witness (schedule indices, in
+  // schedule order): Poseidon chains over inputs alone (with the constants they
+  // read) at least HOST_CHAIN_MIN permutations deep, and what leads into them
+  // -- the public-input hashes and the transcript sponges behind them.  A
+  // one-lane permutation chain is ~10x slower on one GPU wave than on a host
+  // core, and these chains set the device schedule's depth (a 32,768-input
+  // aggregation root: 4,097 levels without them)
+  std::vector<uint32_t> host_gens;
+  // host_gens segments [host_seg_off[k], host_seg_off[k + 1]): segment 0 the
+  // constants the chains read, then each independent chain (they can run in
+  // parallel once segment 0 has); empty if host_gens is
+  std::vector<uint32_t> host_seg_off;
   // zk config: the PublicInputGate row's unused wires 4..num_wires-1, which
   // plonky2's build() hands to RandomValueGenerators (randomize_unused_pi_wires,
   // plonk/circuit_builder.rs).  Here they are commit() inputs (zk randomness is an
@@ -366,6 +384,11 @@ class Witness {
   const F *slot_values() const { return vals_; }
   // run the generator schedule; returns false (and a message) on conflict / missing input
   bool generate(std::string &err);
+  // run CircuitData::host_gens (the device witness's host part): segment seg
+  // (0 = the constants, then one per independent chain), or all if seg < 0
+  bool generate_host_chains(std::string &err, int seg = -1);
+  // one generator of the schedule
+  bool run(const Gen &g, std::string &err);
   // full wire matrix, column-major [num_wires][n]
   void wires_matrix(F *out) const;
   std::vector<F> public_inputs() const;
@@ -377,7 +400,6 @@ class Witness {
   std::vector<F> own_;
   F *vals_;
   std::vector<uint8_t> known_;
-  bool conflict_ = false;
 };
 
 }  // namespace qc

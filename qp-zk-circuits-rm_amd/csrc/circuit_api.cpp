@@ -250,6 +250,16 @@ int qp_circuit_census(const qp_circuit *c, uint32_t *gens, uint32_t *rows, uint3
   return QP_OK;
 }
 
+int qp_circuit_host_chains(const qp_circuit *c, uint32_t *gens, uint32_t *slots, uint32_t *chains) {
+  if (!c || !gens || !slots) return QP_ERR_ARG;
+  memset(gens, 0, 14 * sizeof(uint32_t));
+  for (uint32_t i : c->cd.host_gens)
+    if (c->cd.schedule[i].kind < 14) gens[c->cd.schedule[i].kind]++;
+  *slots = (uint32_t)c->cd.input_slots.size();
+  if (chains) *chains = c->cd.host_seg_off.size() > 1 ? (uint32_t)c->cd.host_seg_off.size() - 2 : 0;
+  return QP_OK;
+}
+
 int qp_circuit_common_data(const qp_circuit *c, uint8_t *out, size_t cap, size_t *len) {
   if (!c) return QP_ERR_ARG;
   auto b = c->cd.common_bytes();

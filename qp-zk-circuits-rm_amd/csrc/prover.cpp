@@ -134,6 +134,7 @@ struct qp_prover {
   bool generic_quotient = false;  // a gate outside k_quotient_1r's set (the recursive verifier's RandomAccess)
   bool pp_generic = false;  // QPGPU_PP_GENERIC=1: the runtime-shape k_pp_rows (A/B)
   uint64_t *h_in = nullptr;  // pinned [max_batch][wg_nin] commit() values
+  std::vector<std::vector<uint64_t>> wscratch;  // per-proof slot values when host chains run split
   std::vector<uint32_t> h_werr;
   std::vector<uint64_t> h_wpis;
   ~qp_prover() {
@@ -1105,12 +1106,8 @@ int prove_inputs(qp_prover *P, FillFn fill, const uint8_t *inputs, size_t in_siz
     std::vector<std::string> msgs(nb);
     std::vector<int> codes(nb, QP_OK);
     auto T0 = Clock::now();
-    P->pool->parallel_for(nb, [&](size_t b) {
-      thread_local std::vector<uint64_t> scratch;
-      if (scratch.size() < cd.num_slots) scratch.resize(cd.num_slots);
-      qc::Witness w(cd, scratch.data());
-      int code = QP_OK;
-      std::string e = fill(P->circuit, inputs + (done + b) * in_size, w, &code);
+    // commit() values (and the host chains' outputs) into the pinned input rows
+    auto finish = [&](size_t b, const qc::Witness &w, std::string e, int code) {
       uint64_t *row = P->h_in + b * (size_t)P->wg_nin;
       if (e.empty())
         for (uint32_t i = 0; i < P->wg_nin; i++) {
@@ -1129,7 +1126,52 @@ int prove_inputs(qp_prover *P, FillFn fill, const uint8_t *inputs, size_t in_siz
         while (b < cur && !first_bad.compare_exchange_weak(cur, (uint32_t)b)) {
         }
       }
-    });
+    };
+    // the long input-only Poseidon chains (CircuitData::host_gens) run on the
+    // host after commit(); a batch smaller than the pool runs its proofs'
+    // independent chains in parallel (a 32,768-input root: chains of 4,096
+    // and twice ~2,150 permutations)
+    const uint32_t nseg = cd.host_seg_off.empty() ? 0 : (uint32_t)cd.host_seg_off.size() - 1;
+    if (nseg > 2 && nb <= P->pool->size()) {
+      const uint32_t nch = nseg - 1;
+      if (P->wscratch.size() < nb) P->wscratch.resize(nb);
+      std::vector<std::unique_ptr<qc::Witness>> wv(nb);
+      std::vector<std::string> em((size_t)nb * nch);
+      P->pool->parallel_for(nb, [&](size_t b) {
+        auto &sc = P->wscratch[b];
+        if (sc.size() < cd.num_slots) sc.resize(cd.num_slots);
+        wv[b].reset(new qc::Witness(cd, sc.data()));
+        codes[b] = QP_OK;
+        msgs[b] = fill(P->circuit, inputs + (done + b) * in_size, *wv[b], &codes[b]);
+        if (msgs[b].empty() && !wv[b]->generate_host_chains(msgs[b], 0)) codes[b] = QP_ERR_WITNESS;
+      });
+      P->pool->parallel_for((size_t)nb * nch, [&](size_t k) {
+        const size_t b = k / nch;
+        if (msgs[b].empty()) wv[b]->generate_host_chains(em[k], 1 + (int)(k % nch));
+      });
+      P->pool->parallel_for(nb, [&](size_t b) {
+        std::string e = msgs[b];
+        int code = codes[b];
+        for (uint32_t c = 0; c < nch && e.empty(); c++)
+          if (!em[b * nch + c].empty()) {
+            e = em[b * nch + c];
+            code = QP_ERR_WITNESS;
+          }
+        msgs[b].clear();
+        codes[b] = QP_OK;
+        finish(b, *wv[b], e, code);
+      });
+    } else {
+      P->pool->parallel_for(nb, [&](size_t b) {
+        thread_local std::vector<uint64_t> scratch;
+        if (scratch.size() < cd.num_slots) scratch.resize(cd.num_slots);
+        qc::Witness w(cd, scratch.data());
+        int code = QP_OK;
+        std::string e = fill(P->circuit, inputs + (done + b) * in_size, w, &code);
+        if (e.empty() && nseg && !w.generate_host_chains(e)) code = QP_ERR_WITNESS;
+        finish(b, w, e, code);
+      });
+    }
     if (first_bad.load() != UINT32_MAX) {
       const uint32_t b = first_bad.load();
       P->ctx->err = "proof " + std::to_string(done + b) + ": " + msgs[b];

@@ -106,6 +106,8 @@ def lib():
         "qp_wormhole_circuit_new": (ctypes.c_int, [ctypes.c_int, PP]),
         "qp_circuit_free": (None, [VP]),
         "qp_circuit_info": (ctypes.c_int, [VP, ctypes.POINTER(ctypes.c_uint32)]),
+        "qp_circuit_host_chains": (ctypes.c_int, [VP, ctypes.POINTER(ctypes.c_uint32), ctypes.POINTER(ctypes.c_uint32),
+                                                   ctypes.POINTER(ctypes.c_uint32)]),
         "qp_circuit_census": (ctypes.c_int, [VP, ctypes.POINTER(ctypes.c_uint32), ctypes.POINTER(ctypes.c_uint32),
                                               ctypes.POINTER(ctypes.c_uint32)]),
         "qp_circuit_common_data": (ctypes.c_int, [VP, ctypes.c_char_p, ctypes.c_size_t,

@@ -220,6 +220,16 @@ class Circuit:
                      for l in range(self.witness_levels)],)
         return out
 
+    def host_chains(self):
+        """({generator kind: count} the host runs before the device schedule,
+        value slots set on the host, independent chains among those
+        generators) -- qp_circuit_host_chains."""
+        g, n, ch = (ctypes.c_uint32 * 14)(), ctypes.c_uint32(), ctypes.c_uint32()
+        rc = lib().qp_circuit_host_chains(self.h, g, ctypes.byref(n), ctypes.byref(ch))
+        if rc:
+            raise QpError(rc, "qp_circuit_host_chains")
+        return {k: v for k, v in zip(self.GEN_KINDS, g) if v}, n.value, ch.value
+
     @classmethod
     def wormhole(cls, zero_knowledge=False):
         h = ctypes.c_void_p()

@@ -98,6 +98,29 @@ def test_aggregation_circuit_shape(agg_circuit):
         assert cb.count(struct.pack("<I", tag) + struct.pack(f"<{len(params)}Q", *params)) == 1
 
 
+def test_host_chains_cut_the_device_schedule(ref, agg_circuit, monkeypatch):
+    """The device witness's host part (CircuitData::host_gens): Poseidon chains
+    over inputs alone at least 64 permutations deep -- here the inner proofs'
+    transcript sponges -- and the constants they read run on the host, the
+    rest of the schedule on the device, 149 dependency levels down to 55;
+    QPGPU_HOST_CHAIN=0 keeps every generator on the device.  The leaf circuits
+    have no such chain.  (Device == host-witness bytes either way:
+    test_gpu_aggregation.)"""
+    import qp_wormhole
+    g, nslots, chains = agg_circuit.host_chains()
+    assert set(g) <= {"poseidon", "constant"} and g["poseidon"] >= 2 * 64
+    assert chains == 2  # the two inner proofs' transcripts
+    assert agg_circuit.witness_levels == 55
+    monkeypatch.setenv("QPGPU_HOST_CHAIN", "0")
+    c0 = qp_wormhole.Circuit.aggregation(ref[0], 2)
+    g0, n0, ch0 = c0.host_chains()
+    assert g0 == {} and ch0 == 0 and c0.witness_levels == 149 and n0 < nslots
+    assert c0.num_generators == agg_circuit.num_generators
+    monkeypatch.delenv("QPGPU_HOST_CHAIN")
+    for circ in (qp_wormhole.Circuit.wormhole(False), qp_wormhole.Circuit.voting()):
+        assert circ.host_chains()[0] == {}
+
+
 def test_reference_proofs_verify_in_circuit(ref, agg_circuit):
     cb, vo, leaves = ref
     w = agg_circuit.commit_proofs(vo, leaves)
