@@ -3,7 +3,8 @@ tool): `leaves` leaf proofs (the reference's own two, alternating) -> one root
 through aggregate_to_tree (branching 2), one untimed pass that builds and
 caches the level circuits, then `reps` timed passes with per-level seconds and
 the device stage times of the level provers.  Variants come from the
-environment (QP_AGG_PROVERS, QP_AGG_WITNESS, QPGPU_QUOTIENT, QPGPU_LDE_MODE).
+environment (QP_AGG_PROVERS, QP_AGG_WITNESS, QPGPU_QUOTIENT, QPGPU_LDE_MODE,
+QPGPU_HOST_CHAIN).
 python tools/agg_subtree.py [leaves] [reps]"""
 import json
 import os
@@ -56,7 +57,8 @@ def main():
             for k, v in p.stage_times().items():
                 stages[k] = stages.get(k, 0.0) + v / reps
     rvd, rp = root.circuit_data.verifier_data(), root.proof.to_bytes()
-    env = {k: os.environ.get(k) for k in ("QP_AGG_PROVERS", "QP_AGG_WITNESS", "QPGPU_QUOTIENT", "QPGPU_LDE_MODE")}
+    env = {k: os.environ.get(k) for k in ("QP_AGG_PROVERS", "QP_AGG_WITNESS", "QPGPU_QUOTIENT", "QPGPU_LDE_MODE",
+                                        "QPGPU_HOST_CHAIN")}
     print(json.dumps({"leaves": nl, "env": env, "warm_s": round(warm, 2), "runs": res,
                       "stage_ms_per_run_all_provers": {k: round(v, 1) for k, v in stages.items()},
                       "root_verified": olib().ora_verify(rvd, len(rvd), rp, len(rp)) == 0}), flush=True)
