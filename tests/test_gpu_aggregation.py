@@ -193,6 +193,28 @@ def test_device_witness_equals_host_witness_levels_1_and_2(reference_leaves):
     assert dev2 == host2 and verify(vd2, dev2[0]) == 0
 
 
+def test_host_chains_off_gives_the_same_proofs(reference_leaves, monkeypatch):
+    """The device witness with the input-only Poseidon chains on the host
+    (default) and with every generator on the device (QPGPU_HOST_CHAIN=0, a
+    circuit built under it: 149 dependency levels instead of 55) prove the
+    same bytes, which verify."""
+    import qp_wormhole
+    cb, vo, leaves = reference_leaves
+    chunks = [leaves, leaves[::-1]]
+    c1 = qp_wormhole.Circuit.aggregation(cb, 2)
+    monkeypatch.setenv("QPGPU_HOST_CHAIN", "0")
+    c0 = qp_wormhole.Circuit.aggregation(cb, 2)
+    monkeypatch.delenv("QPGPU_HOST_CHAIN")
+    assert c1.host_chains()[0] and not c0.host_chains()[0] and c0.witness_levels > c1.witness_levels
+    out = []
+    for c in (c1, c0):
+        p = qp_wormhole.Prover(qp_wormhole.Context(0), c, max_batch=2)
+        out.append((p.prove_aggregation(vo, chunks), p.verifier_data()))
+        p.free()
+    (a, vd1), (b, vd0) = out
+    assert a == b and vd1 == vd0 and all(verify(vd1, x) == 0 for x in a)
+
+
 def test_device_witness_zk_aggregation(reference_leaves):
     """Under the zk config the PublicInputGate row's cells are explicit inputs
     (device == host for the same values) or, when not given, OS randomness
