@@ -408,9 +408,12 @@ __device__ __forceinline__ void alg_mul(uint64_t a0, uint64_t a1, uint64_t b0, u
   r1 = gfn::add(gfn::mul(a0, b1), gfn::mul(a1, b0));
 }
 
-__device__ __noinline__ void recursion_gate(uint32_t kind, uint32_t q0, uint32_t q1, uint32_t q2,
-                                            const uint64_t *__restrict__ wl, const uint64_t *__restrict__ gc,
-                                            uint64_t N, TermAcc &A) {
+// (inlined into the per-gate kernel, so TermAcc stays in registers and the
+// alpha-power reads are uniform scalar loads; called out of line by the
+// one-pass generic kernel to bound its size)
+__device__ __forceinline__ void recursion_gate_body(uint32_t kind, uint32_t q0, uint32_t q1, uint32_t q2,
+                                                    const uint64_t *__restrict__ wl,
+                                                    const uint64_t *__restrict__ gc, uint64_t N, TermAcc &A) {
   switch (kind) {
     case GK_ARITH_EXT:  // per op: multiplicand_0, multiplicand_1, addend, output
       for (uint32_t i = 0; i < q0; i++) {
@@ -433,20 +436,37 @@ __device__ __noinline__ void recursion_gate(uint32_t kind, uint32_t q0, uint32_t
       break;
     case GK_REDUCING:
     case GK_REDUCING_EXT: {
-      // output 0..2, alpha 2..4, old_acc 4..6, coeffs from 6, then accumulators
+      // output 0..2, alpha 2..4, old_acc 4..6, coeffs from 6, then accumulators;
+      // a chunk's coefficients and accumulators are loaded before its Horner
+      // steps (eight steps' reads in flight instead of one)
       const uint32_t cw = kind == GK_REDUCING ? 1 : 2, start_accs = 6 + cw * q0;
       uint64_t a0 = WV(4), a1 = WV(5);
       const uint64_t al0 = WV(2), al1 = WV(3);
-      for (uint32_t i = 0; i < q0; i++) {
-        uint64_t m0, m1;
-        alg_mul(a0, a1, al0, al1, m0, m1);
-        m0 = gfn::add(m0, WV(6 + cw * i));
-        if (cw == 2) m1 = gfn::add(m1, WV(7 + 2 * i));
-        const uint32_t ai = i == q0 - 1 ? 0 : start_accs + 2 * i;
-        a0 = WV(ai);
-        a1 = WV(ai + 1);
-        A.emit(gfn::sub(m0, a0));
-        A.emit(gfn::sub(m1, a1));
+      constexpr uint32_t CH = 8;
+      for (uint32_t i0 = 0; i0 < q0; i0 += CH) {
+        const uint32_t n = q0 - i0 < CH ? q0 - i0 : CH;
+        uint64_t c0[CH], c1[CH], x0[CH], x1[CH];
+#pragma unroll
+        for (uint32_t k = 0; k < CH; k++)
+          if (k < n) {
+            const uint32_t i = i0 + k, ai = i == q0 - 1 ? 0 : start_accs + 2 * i;
+            c0[k] = WV(6 + cw * i);
+            c1[k] = cw == 2 ? WV(7 + 2 * i) : 0;
+            x0[k] = WV(ai);
+            x1[k] = WV(ai + 1);
+          }
+#pragma unroll
+        for (uint32_t k = 0; k < CH; k++)
+          if (k < n) {
+            uint64_t m0, m1;
+            alg_mul(a0, a1, al0, al1, m0, m1);
+            m0 = gfn::add(m0, c0[k]);
+            if (cw == 2) m1 = gfn::add(m1, c1[k]);
+            a0 = x0[k];
+            a1 = x1[k];
+            A.emit(gfn::sub(m0, a0));
+            A.emit(gfn::sub(m1, a1));
+          }
       }
       break;
     }
@@ -463,19 +483,24 @@ __device__ __noinline__ void recursion_gate(uint32_t kind, uint32_t q0, uint32_t
       A.emit(gfn::sub(WV(1 + q0), WV(2 + q0 + q0 - 1)));
       break;
     }
-    case GK_POSEIDON_MDS:  // inputs 0..24, outputs 24..48 (ext pairs)
-      for (uint32_t r = 0; r < 12; r++) {
-        uint64_t a0 = 0, a1 = 0;
-        for (uint32_t i = 0; i < 12; i++) {
-          const uint32_t e = (i + r) % 12;
-          const uint64_t m = ps::mds_circ(i) + (r == 0 && i == 0 ? 8 : 0);
-          a0 = gfn::add(a0, gfn::mul(WV(2 * e), m));
-          a1 = gfn::add(a1, gfn::mul(WV(2 * e + 1), m));
-        }
-        A.emit(gfn::sub(WV(24 + 2 * r), a0));
-        A.emit(gfn::sub(WV(25 + 2 * r), a1));
+    case GK_POSEIDON_MDS: {  // inputs 0..24, outputs 24..48 (ext pairs)
+      // the permutation's MDS layer (circulant + diagonal) on each coordinate
+      // of the 12 extension inputs, each input read once
+      uint64_t a[12], b[12];
+#pragma unroll
+      for (int i = 0; i < 12; i++) {
+        a[i] = WV(2 * i);
+        b[i] = WV(2 * i + 1);
+      }
+      pf::mds<0, -1>(a);
+      pf::mds<0, -1>(b);
+#pragma unroll
+      for (int r = 0; r < 12; r++) {
+        A.emit(gfn::sub(WV(24 + 2 * r), a[r]));
+        A.emit(gfn::sub(WV(25 + 2 * r), b[r]));
       }
       break;
+    }
     case GK_RANDOM_ACCESS: {  // q0 bits, q1 copies, q2 extra constants
       const uint32_t vec = 1u << q0, routed = (2 + vec) * q1 + q2;
       for (uint32_t cp = 0; cp < q1; cp++) {
@@ -565,6 +590,12 @@ __device__ __noinline__ void recursion_gate(uint32_t kind, uint32_t q0, uint32_t
     default:
       break;
   }
+}
+
+__device__ __noinline__ void recursion_gate(uint32_t kind, uint32_t q0, uint32_t q1, uint32_t q2,
+                                            const uint64_t *__restrict__ wl, const uint64_t *__restrict__ gc,
+                                            uint64_t N, TermAcc &A) {
+  recursion_gate_body(kind, q0, q1, q2, wl, gc, N, A);
 }
 
 // Two phases with separate register allocation (the Poseidon gate alone is
@@ -1201,6 +1232,9 @@ k_quotient_fused(QuotientArgs a) {
 // alpha-weighted terms do not depend on evaluation order), so the output is
 // bit-identical.  PART 0: permutation terms; 1: one non-Poseidon gate; 2: the
 // Poseidon gate.
+#ifndef QP_QPART_INLINE
+#define QP_QPART_INLINE 1
+#endif
 template <int PART>
 __global__ void __launch_bounds__(256) k_quotient_part(QuotientArgs a, uint32_t gi, uint32_t last) {
   const uint32_t logN = a.log_n + a.rate_bits;
@@ -1266,14 +1300,29 @@ __global__ void __launch_bounds__(256) k_quotient_part(QuotientArgs a, uint32_t 
           for (uint32_t i = 0; i < 4; i++) A.emit(gfn::sub(WV(i), ch[CH_PIH + i]));
           break;
         case GK_BASE_SUM: {
-          const uint32_t L = a.g.param[gi];
+          // each limb read once, high limb first in chunks: the sum by Horner
+          // and the limb's boolean check at its own alpha index (i0 + 1 + i)
+          const uint32_t L = a.g.param[gi], i0 = A.i;
+          constexpr uint32_t CH = 8;
           uint64_t acc = 0;
-          for (uint32_t i = L; i-- > 0;) acc = gfn::add(gfn::add(acc, acc), WV(1 + i));
-          A.emit(gfn::sub(acc, WV(0)));
-          for (uint32_t i = 0; i < L; i++) {
-            const uint64_t l = WV(1 + i);
-            A.emit(gfn::mul(l, gfn::sub(l, 1)));
+          for (uint32_t hi = L; hi > 0;) {
+            const uint32_t n = hi < CH ? hi : CH;
+            uint64_t l[CH];
+#pragma unroll
+            for (uint32_t k = 0; k < CH; k++)
+              if (k < n) l[k] = WV(hi - k);  // limb hi - 1 - k is wire hi - k
+#pragma unroll
+            for (uint32_t k = 0; k < CH; k++)
+              if (k < n) {
+                acc = gfn::add(gfn::add(acc, acc), l[k]);
+                A.i = i0 + hi - k;
+                A.emit(gfn::mul(l[k], gfn::sub(l[k], 1)));
+              }
+            hi -= n;
           }
+          A.i = i0;
+          A.emit(gfn::sub(acc, WV(0)));
+          A.i = i0 + 1 + L;
           break;
         }
         case GK_ARITHMETIC:
@@ -1284,7 +1333,10 @@ __global__ void __launch_bounds__(256) k_quotient_part(QuotientArgs a, uint32_t 
           }
           break;
         default:
-          recursion_gate(kind, a.g.param[gi], a.g.param2[gi], a.g.param3[gi], wl, gc, N, A);
+          if constexpr (QP_QPART_INLINE)
+            recursion_gate_body(kind, a.g.param[gi], a.g.param2[gi], a.g.param3[gi], wl, gc, N, A);
+          else
+            recursion_gate(kind, a.g.param[gi], a.g.param2[gi], a.g.param3[gi], wl, gc, N, A);
           break;
       }
     }
