@@ -71,7 +71,9 @@ class AggregatedProof:
 
 class _LevelProver:
     """One aggregation circuit (inner common data, branching) with its device
-    provers: QP_AGG_PROVERS (default 2) contexts, each with its own HIP stream
+    provers: QP_AGG_PROVERS (default 2; 3 raises a level's throughput but not the
+    256-leaf subtree inside bench.py, profiles/r04_agg_provers_ab.log) contexts,
+    each with its own HIP stream
     and workspace, so one prover's host phases (transcript, query assembly)
     overlap the other's kernels, as the leaf bench's provers do."""
 
