@@ -221,6 +221,8 @@ def cpu_baseline(circuit, inputs, sample, min_seconds):
     L = olib()
     L.ora_prove.argtypes = [ctypes.c_char_p, ctypes.c_size_t, U64P, U64P, U64P, ctypes.c_size_t, ctypes.c_char_p,
                             ctypes.c_size_t, ctypes.POINTER(ctypes.c_size_t), U64P, U64P]
+    cores = int(os.environ.get("OMP_NUM_THREADS") or host_cpu_share())
+    L.ora_set_threads(cores)
     cb = circuit.common_data()
     cs = circuit.constants_sigmas()
     out = ctypes.create_string_buffer(400000)
@@ -240,14 +242,37 @@ def cpu_baseline(circuit, inputs, sample, min_seconds):
         assert rc == 0
         done += 1
     dt = time.perf_counter() - t
-    cores = int(os.environ.get("OMP_NUM_THREADS", os.cpu_count() or 1))
-    return {"value": done / dt, "unit": "proofs/s", "cores": cores, "kind": "port",
+    nproc = os.cpu_count() or 1
+    value = done / dt
+    return {"value": value, "unit": "proofs/s", "cores": cores, "kind": "port",
+            "per_core": value / cores,
             "sample": f"{done} {circuit.kind} proofs (deg {circuit.degree_bits}, standard_recursion_config) from the "
                       f"bench's CircuitInputs, {dt:.1f} s: commit + witness generation {t_wit:.2f} s (host C++, one "
-                      f"thread), prove {dt - t_wit:.1f} s (oracle/prover.c, C + OpenMP)",
-            "host": {"nproc": os.cpu_count(), "cpu_model": cpu_model(), "omp_threads": cores},
-            "note": "the GPU line's work (commit, witness generation, prove) on the host cores; a C restatement "
-                    "of plonky2, not the Rust reference (no cargo here): quote no GPU/CPU ratio"}
+                      f"thread), prove {dt - t_wit:.1f} s (oracle/prover.c, C + OpenMP, {cores} threads)",
+            "host": {"nproc": nproc, "cpu_model": cpu_model(), "omp_threads": cores,
+                     "affinity": len(os.sched_getaffinity(0)), "cgroup_cpus": cgroup_cpu_quota(),
+                     # the box gives one GPU's job a share of the node's cores
+                     # (OMP_NUM_THREADS); all nproc at the measured per-core rate,
+                     # an upper bound (commit + witness run on one thread)
+                     "whole_node_linear_estimate": value / cores * nproc},
+            "note": "the GPU line's work (commit, witness generation, prove) on the host cores this job may use; "
+                    "a C restatement of plonky2, not the Rust reference (no cargo here): quote no GPU/CPU ratio"}
+
+
+def cgroup_cpu_quota():
+    """CPUs of this process's cgroup v2 cpu.max quota, or None if unlimited/unknown."""
+    try:
+        q, per = open("/sys/fs/cgroup/cpu.max").read().split()[:2]
+        return None if q == "max" else round(int(q) / int(per), 2)
+    except (OSError, ValueError):
+        return None
+
+
+def host_cpu_share():
+    """Cores this process may run on: the affinity mask, capped by the cgroup quota."""
+    n = len(os.sched_getaffinity(0))
+    q = cgroup_cpu_quota()
+    return max(1, min(n, int(q))) if q else n
 
 
 def reference_parity(qp_wormhole, device):

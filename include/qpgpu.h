@@ -173,6 +173,15 @@ int qp_circuit_constants_sigmas(const qp_circuit *c, uint64_t *out);
 /* their coefficients (PolynomialValues::ifft per column, host), the polynomials
  * of ProverOnlyCircuitData.constants_sigmas_commitment                     */
 int qp_circuit_constants_sigmas_coeffs(const qp_circuit *c, uint64_t *out);
+/* ProverOnlyCircuitData::to_bytes through DefaultGeneratorSerializer (the
+ * prover.bin of wormhole/circuit-builder/src/lib.rs:53-59, read by
+ * WormholeProver::new_from_bytes, prover/src/lib.rs:104-137) of a leaf circuit
+ * (Wormhole, voting; QP_ERR_ARG for an aggregation circuit), computed on the
+ * host: generators, watch index, the constants||sigmas PolynomialBatch with its
+ * Merkle tree, sigmas, subgroup, public inputs, representative map, fft root
+ * table, circuit digest.  out == NULL: *len = the size (the bytes are kept until
+ * the copying call).  Restated from upstream plonky2; parity unpinned.        */
+int qp_circuit_prover_only_bytes(const qp_circuit *c, uint8_t *out, size_t cap, size_t *len);
 /* WormholeProver::commit (lib.rs:209-225) + witness generation.  On a witness
  * conflict returns QP_ERR_WITNESS with the reference's message in err.     */
 int qp_wormhole_commit(const qp_circuit *c, const qp_wormhole_inputs *in, qp_witness **out, char *err,
@@ -321,9 +330,12 @@ int qp_prover_stage_times(qp_prover *p, double *ms, uint32_t n, int reset);
  * context's last error, never a wrong result): commitments of up to 2^16
  * values per polynomial with LDE domains up to 2^18 points (log_n + rate_bits
  * <= 18, i.e. circuits up to degree 2^15 at rate 3, the top of a 2048-leaf
- * aggregation tree); qp_quotient: degree <= 2^14, 2 challenges,
- * quotient_degree_factor == 2^rate_bits <= 16, at most 16 gates, unsalted
- * batches of one; qp_fri_layer_commit: at most 2^16 nonzero coefficients.                                                     */
+ * aggregation tree, and the level-1 circuits of 5- to 7-ary trees);
+ * qp_quotient: 2^6 <= degree <= 2^15 (the same kernels as the whole-circuit
+ * prover; above 2^14 the coset iNTT runs its first levels in HBM), 2
+ * challenges, quotient_degree_factor == 2^rate_bits <= 16, at most 16 gates,
+ * unsalted batches of one; qp_fri_layer_commit: at most 2^16 nonzero
+ * coefficients.                                                             */
 
 /* gate kinds of CommonCircuitData.gates (DefaultGateSerializer ids in brackets).
  * 0-5: the leaf circuits' gates (fast single-read quotient kernel); 6-13: the

@@ -8,6 +8,7 @@
 #include "fft.h"
 #include "merkle.h"
 #include "challenger.h"
+#include <omp.h>
 #include <stdlib.h>
 #include <string.h>
 
@@ -67,6 +68,12 @@ int ora_merkle(const uint64_t *leaves, unsigned log_n, size_t width, unsigned ca
 }
 
 /* full verification of a proof against verifier-only + common data bytes */
+/* OpenMP threads of the prover/verifier loops (bench.py's cpu_baseline sizes
+ * them to the host cores the job may use) */
+void ora_set_threads(int n) {
+  if (n > 0) omp_set_num_threads(n);
+}
+
 int ora_verify(const uint8_t *vd, size_t vlen, const uint8_t *pb, size_t plen) {
     or_common_t c;
     or_verifier_only_t v;

@@ -218,6 +218,7 @@ Target CircuitBuilder::is_equal(Target x, Target y) {
   g.kind = GEN_EQUALITY;
   g.a = x; g.b = y; g.c = equal; g.d = inv;
   gens_.push_back(g);
+  simple_gens_.push_back(g);
   Target diff = sub(x, y);
   Target not_equal_check = mul(equal, diff);
   Target diff_normalized = mul(diff, inv);
@@ -251,16 +252,16 @@ std::vector<Target> CircuitBuilder::split_le(Target x, uint32_t num_bits) {
   F base = gl::pow(2, L);
   for (size_t i = gates.size(); i-- > 0;) acc = mul_const_add(base, acc, Target::wire(gates[i], 0));
   connect(acc, x);
-  if (k > 1) {
-    // WireSplitGenerator: the integer's L-bit chunks into the gates' sum wires
-    // (with one gate the sum wire is the integer itself)
-    Gen g{};
-    g.kind = GEN_WIRE_SPLIT;
-    g.a = x;
-    g.row = gates[0];
-    g.op = k;
-    gens_.push_back(g);
-  }
+  // WireSplitGenerator: the integer's L-bit chunks into the gates' sum wires
+  // (with one gate the sum wire is the integer itself, so the schedule skips
+  // it; upstream's generator list has it either way)
+  Gen g{};
+  g.kind = GEN_WIRE_SPLIT;
+  g.a = x;
+  g.row = gates[0];
+  g.op = k;
+  if (k > 1) gens_.push_back(g);
+  simple_gens_.push_back(g);
   return bits;
 }
 
@@ -364,6 +365,10 @@ CircuitData CircuitBuilder::build() {
   CircuitData cd;
   cd.config = cfg_;
   cd.n = (uint32_t)n;
+  cd.simple_gens = simple_gens_;
+  cd.copies = copies_;
+  cd.num_virtual_targets = nvirt_;
+  cd.public_input_targets = public_inputs_;
   cd.degree_bits = 0;
   while ((1u << cd.degree_bits) < n) cd.degree_bits++;
   cd.rows = rows_;

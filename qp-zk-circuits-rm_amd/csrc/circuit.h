@@ -220,6 +220,15 @@ struct CircuitData {
   std::vector<uint32_t> dev_wslot;      // wire_slot with DEV_MULTI flags (device witness)
   std::vector<uint32_t> level_off;      // [levels + 1] offsets into dev_gens
   std::vector<uint32_t> level_pos;      // [levels][2]: first Poseidon generator of the level, count
+  // what upstream's ProverOnlyCircuitData records beyond the above (prover.bin,
+  // prover_bin.cpp): the simple generators the gadgets added, in call order
+  // (EqualityGenerator, WireSplitGenerator -- every split_le, also of one gate),
+  // the copy constraints in connect() order, the virtual target count and the
+  // public-input targets
+  std::vector<Gen> simple_gens;
+  std::vector<std::pair<Target, Target>> copies;
+  uint32_t num_virtual_targets = 0;
+  std::vector<Target> public_input_targets;
   // commitments (filled by the prover backend at setup)
   F constants_sigmas_cap[64 * 4] = {0};
   F circuit_digest[4] = {0};
@@ -346,6 +355,7 @@ class CircuitBuilder {
   uint32_t nvirt_ = 0;
   std::vector<std::pair<Target, Target>> copies_;
   std::vector<Gen> gens_;
+  std::vector<Gen> simple_gens_;  // CircuitData::simple_gens
   std::vector<Target> public_inputs_;
   std::vector<Target> inputs_;
   std::unordered_map<F, Target> const_to_target_;

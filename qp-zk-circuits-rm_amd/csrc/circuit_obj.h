@@ -1,6 +1,7 @@
 // circuit_obj.h — definitions behind qp_circuit / qp_witness handles.
 #pragma once
 #include <stdint.h>
+#include <vector>
 #include "circuit.h"
 #include "recursion.h"
 #include "voting.h"
@@ -13,6 +14,8 @@ struct qp_circuit {
   qv::VoteTargets voting;
   qr::AggregationTargets aggregation;
   uint32_t gates_used = 0;
+  // upstream-format prover.bin between qp_circuit_prover_only_bytes' size and copy calls
+  mutable std::vector<uint8_t> prover_bin;
 };
 
 // commit(): the fragments' fill_targets into w (no generation); "" on success,

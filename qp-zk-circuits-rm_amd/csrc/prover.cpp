@@ -672,50 +672,15 @@ int prove_batch(qp_prover *P, const uint64_t *d_wires, const uint64_t *const *wi
     a.num_constants = P->NC;
     a.g = P->gdesc;
     kt_begin(P, 3);
-    if (P->generic_quotient && !P->quotient_onepass && !P->quotient_rereads) {
-      // generic gate list: the permutation terms, then one launch per gate
-      // (k_quotient_part: each streams only its gate's columns), the last
-      // multiplying by 1/Z_H
-      const dim3 qg(cdiv(N, 256), nb);
-      int lastg = -1;
-      for (uint32_t gi = 0; gi < a.g.ngates; gi++)
-        if (a.g.kind[gi] != qpk::GK_NOOP) lastg = (int)gi;
-      qpk::k_quotient_part<0><<<qg, 256, 0, s>>>(a, 0, lastg < 0);
-      for (uint32_t gi = 0; gi < a.g.ngates; gi++) {
-        if (a.g.kind[gi] == qpk::GK_NOOP) continue;
-        if (a.g.kind[gi] == qpk::GK_POSEIDON)
-          qpk::k_quotient_part<2><<<qg, 256, 0, s>>>(a, gi, (int)gi == lastg);
-        else
-          qpk::k_quotient_part<1><<<qg, 256, 0, s>>>(a, gi, (int)gi == lastg);
-      }
-    } else if (P->quotient_rereads || P->generic_quotient)  // generic gate list (or A/B: QPGPU_QUOTIENT=rereads/onepass)
-      qpk::k_quotient<2><<<dim3(cdiv(N, 256), nb), 256, 0, s>>>(a);
+    qpk::QuotientKernel qk = qpk::QK_1R;
+    if (P->generic_quotient && !P->quotient_onepass && !P->quotient_rereads) qk = qpk::QK_PARTS;
+    else if (P->quotient_rereads || P->generic_quotient) qk = qpk::QK_ONEPASS;  // A/B: QPGPU_QUOTIENT=rereads/onepass
     else if (P->R == 80 && P->qdf == 8 && P->has_poseidon_gate && P->quotient_fused && !P->has_random_access)
-      qpk::k_quotient_fused<<<dim3(cdiv(N, 256), nb), 256, 0, s>>>(a);
-    else
-      qpk::k_quotient_1r<<<dim3(cdiv(N, 256), nb), 256, 0, s>>>(a);
+      qk = qpk::QK_FUSED;
+    qpk::quotient_values(a, qk, nb, s);
     kt_end(P, 3, (double)nb * N);
-    const uint64_t n_inv = gl::inv(n);
-    if (P->log_n <= qpk::LDS_LOG_MAX) {
-      qpk::k_qintt_blocks<<<dim3(B, nc, nb), 512, 8u * qpk::ntt_lds_words(1u << P->log_n), s>>>(
-          P->qvals.p, P->cbuf.p, P->log_n, P->rate_bits, (uint64_t)nc * N, (uint64_t)nc * N, c->tw.fwd, c->tw.pt_inv,
-          n_inv, gl::inv(gl::GEN));
-    } else {
-      // n > 2^14: gather each coset block into natural order, inverse DIF in
-      // place, then per coset the bit-reversal scaled by (g w_N^s)^-k / n
-      qpk::k_qintt_gather_big<<<dim3(64, nc * B, nb), 256, 0, s>>>(P->qvals.p, P->cbuf.p, P->log_n, P->rate_bits,
-                                                                  (uint64_t)nc * N, (uint64_t)nc * N);
-      qpk::dif_big(c->tw, P->cbuf.p, (uint64_t)B * n, nc, B, n, P->log_n, true, nb, (uint64_t)nc * N, s);
-      const uint64_t wN = gl::root_of_unity(logN), ginv = gl::inv(gl::GEN);
-      for (uint32_t sc = 0; sc < B; sc++)
-        qpk::bitrev_scale(P->cbuf.p + (uint64_t)sc * n, (uint64_t)B * n, nc, P->log_n, n_inv,
-                          gl::mul(ginv, gl::inv(gl::pow(wN, sc))), nb, (uint64_t)nc * N, s);
-    }
-    const uint64_t winv_r = gl::inv(gl::root_of_unity(P->rate_bits));
-    const uint64_t gninv = gl::inv(gl::pow(gl::GEN, n));
-    qpk::k_qintt_radix<<<dim3(cdiv(n, 256), nc, nb), 256, 0, s>>>(P->cbuf.p, P->quot.coeffs.p, P->log_n, P->rate_bits,
-                                                                 (uint64_t)nc * N, P->quot.cbs(), winv_r,
-                                                                 gl::inv(B), gninv);
+    qpk::quotient_coeffs(c->tw, P->qvals.p, P->cbuf.p, P->quot.coeffs.p, P->log_n, P->rate_bits, nc, nb,
+                         (uint64_t)nc * N, (uint64_t)nc * N, P->quot.cbs(), s);
     P->quot.build(c, nb);
     TRY(hipGetLastError());
   }

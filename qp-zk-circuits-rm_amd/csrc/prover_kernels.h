@@ -85,6 +85,22 @@ __global__ void k_qintt_blocks(const uint64_t *vals, uint64_t *out, uint32_t log
                                uint64_t n_inv, uint64_t ginv);
 __global__ void k_qintt_radix(const uint64_t *cbuf, uint64_t *coeffs, uint32_t log_n, uint32_t rate_bits,
                               uint64_t c_bstride, uint64_t o_bstride, uint64_t winv_r, uint64_t r_inv, uint64_t gninv);
+// compute_quotient_polys (plonk/prover.rs) as launches, shared by the prover's
+// stage 3 and the qp_quotient seam: the vanishing-polynomial values at every
+// LDE point of nb proofs with the chosen kernel(s) ...
+enum QuotientKernel : uint32_t {
+  QK_1R,       // k_quotient_1r: the leaf gate set, every column read once
+  QK_FUSED,    // k_quotient_fused (A/B)
+  QK_ONEPASS,  // k_quotient<2>: any gate list in one pass (A/B)
+  QK_PARTS     // k_quotient_part: permutation terms, then one launch per gate (any gate list)
+};
+void quotient_values(const QuotientArgs &a, QuotientKernel k, uint32_t nb, hipStream_t s);
+// ... and their coset iNTT into nc * qdf * n coefficients per proof (qvals
+// [nb][nc][N] leaf order -> coeffs [nb][nc][qdf * n]; cbuf: scratch of the
+// size of qvals); LDS form up to n = 2^LDS_LOG_MAX, HBM levels above
+void quotient_coeffs(const Twiddles &tw, const uint64_t *qvals, uint64_t *cbuf, uint64_t *coeffs, uint32_t log_n,
+                     uint32_t rate_bits, uint32_t nc, uint32_t nb, uint64_t v_bstride, uint64_t c_bstride,
+                     uint64_t o_bstride, hipStream_t s);
 constexpr int OPEN_PB = 8;  // polys per k_openings block
 __global__ void k_openings(const uint64_t *coeffs, uint64_t c_bstride, uint32_t npolys, uint32_t log_n,
                            const uint64_t *pts, uint32_t pt_off, uint64_t *out, uint32_t out_off);

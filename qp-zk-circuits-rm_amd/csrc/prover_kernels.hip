@@ -1433,6 +1433,58 @@ __global__ void __launch_bounds__(256) k_qintt_radix(const uint64_t *__restrict_
   }
 }
 
+// ---- compute_quotient_polys as launches, shared by the prover's stage 3 and
+// the qp_quotient seam (any 2^6 <= n <= 2^15: the coset iNTT takes its LDS or
+// its large-n form by size)
+void quotient_values(const QuotientArgs &a, QuotientKernel k, uint32_t nb, hipStream_t s) {
+  const uint64_t N = 1ull << (a.log_n + a.rate_bits);
+  const dim3 qg((unsigned)((N + 255) / 256), nb);
+  switch (k) {
+    case QK_PARTS: {
+      // the permutation terms, then one launch per gate (each streams only its
+      // gate's columns), the last multiplying by 1/Z_H
+      int lastg = -1;
+      for (uint32_t gi = 0; gi < a.g.ngates; gi++)
+        if (a.g.kind[gi] != GK_NOOP) lastg = (int)gi;
+      k_quotient_part<0><<<qg, 256, 0, s>>>(a, 0, lastg < 0);
+      for (uint32_t gi = 0; gi < a.g.ngates; gi++) {
+        if (a.g.kind[gi] == GK_NOOP) continue;
+        if (a.g.kind[gi] == GK_POSEIDON) k_quotient_part<2><<<qg, 256, 0, s>>>(a, gi, (int)gi == lastg);
+        else k_quotient_part<1><<<qg, 256, 0, s>>>(a, gi, (int)gi == lastg);
+      }
+      break;
+    }
+    case QK_ONEPASS: k_quotient<2><<<qg, 256, 0, s>>>(a); break;
+    case QK_FUSED: k_quotient_fused<<<qg, 256, 0, s>>>(a); break;
+    case QK_1R: k_quotient_1r<<<qg, 256, 0, s>>>(a); break;
+  }
+}
+
+void quotient_coeffs(const Twiddles &tw, const uint64_t *qvals, uint64_t *cbuf, uint64_t *coeffs, uint32_t log_n,
+                     uint32_t rate_bits, uint32_t nc, uint32_t nb, uint64_t v_bstride, uint64_t c_bstride,
+                     uint64_t o_bstride, hipStream_t s) {
+  const uint64_t n = 1ull << log_n;
+  const uint32_t B = 1u << rate_bits;
+  const uint64_t n_inv = gl::inv(n), ginv = gl::inv(gl::GEN);
+  if (log_n <= LDS_LOG_MAX) {
+    k_qintt_blocks<<<dim3(B, nc, nb), 512, 8u * ntt_lds_words(1u << log_n), s>>>(qvals, cbuf, log_n, rate_bits,
+                                                                                v_bstride, c_bstride, tw.fwd,
+                                                                                tw.pt_inv, n_inv, ginv);
+  } else {
+    // n > 2^14: gather each coset block into natural order, inverse DIF in
+    // place, then per coset the bit-reversal scaled by (g w_N^s)^-k / n
+    k_qintt_gather_big<<<dim3(64, nc * B, nb), 256, 0, s>>>(qvals, cbuf, log_n, rate_bits, v_bstride, c_bstride);
+    dif_big(tw, cbuf, (uint64_t)B * n, nc, B, n, log_n, true, nb, c_bstride, s);
+    const uint64_t wN = gl::root_of_unity(log_n + rate_bits);
+    for (uint32_t sc = 0; sc < B; sc++)
+      bitrev_scale(cbuf + (uint64_t)sc * n, (uint64_t)B * n, nc, log_n, n_inv, gl::mul(ginv, gl::inv(gl::pow(wN, sc))),
+                   nb, c_bstride, s);
+  }
+  k_qintt_radix<<<dim3((unsigned)((n + 255) / 256), nc, nb), 256, 0, s>>>(
+      cbuf, coeffs, log_n, rate_bits, c_bstride, o_bstride, gl::inv(gl::root_of_unity(rate_bits)), gl::inv(B),
+      gl::inv(gl::pow(gl::GEN, n)));
+}
+
 // ---------------------------------------------------------------- a10
 
 // value of each coefficient column at an extension point: out[b][poly].

@@ -107,13 +107,13 @@ int qp_quotient(qp_ctx *ctx, const qp_batch *cs, const qp_batch *wires, const qp
   const uint32_t nterms = nc + nc * nchunks + g->num_gate_constraints;
   if (nc != 2 || g->num_gates == 0 || g->num_gates > QP_MAX_GATES || g->num_selectors == 0 ||
       g->num_selectors > QP_MAX_GATES || qdf != (1u << rb) || logN > qpk::TW_LOG || log_n < 6 ||
-      log_n > qpk::LDS_LOG_MAX ||
+      log_n > qpk::BIG_LOG_MAX - 1 ||
       nterms > qpk::APOW_STRIDE || wires->log_n != log_n || zs_pp->log_n != log_n || wires->rate_bits != rb ||
       zs_pp->rate_bits != rb || cs->nbat != 1 || wires->nbat != 1 || zs_pp->nbat != 1 ||
       cs->npolys != g->num_constants + R || wires->npolys != g->num_wires || zs_pp->npolys != nc * nchunks ||
       wires->nsalt || zs_pp->nsalt || cs->nsalt || R > g->num_wires || rb > 4 ||
       g->num_constants < g->num_selectors) {
-    ctx->err = "qp_quotient: unsupported shape (2 challenges, qdf = 2^rate_bits <= 16, unsalted batches of one)";
+    ctx->err = "qp_quotient: unsupported shape (2 challenges, qdf = 2^rate_bits <= 16, 2^6 <= n <= 2^15, unsalted batches of one)";
     return QP_ERR_ARG;
   }
   // per-gate checks: known kind, selector in range, parameters inside the
@@ -237,15 +237,13 @@ int qp_quotient(qp_ctx *ctx, const qp_batch *cs, const qp_batch *wires, const qp
       a.g.grp_lo[i] = g->group_lo[i];
       a.g.grp_hi[i] = g->group_hi[i];
     }
-    if (fast) qpk::k_quotient_1r<<<dim3(cdiv(N, 256), 1), 256, 0, s>>>(a);
-    else qpk::k_quotient<2><<<dim3(cdiv(N, 256), 1), 256, 0, s>>>(a);  // any gate list
-    const uint64_t n_inv = gl::inv(n);
-    qpk::k_qintt_blocks<<<dim3(B, nc, 1), 512, 8u * qpk::ntt_lds_words(1u << log_n), s>>>(
-        d_q.p, d_cbuf.p, log_n, rb, 2 * N, 2 * N, ctx->tw.fwd, ctx->tw.pt_inv, n_inv, gl::inv(gl::GEN));
-    qpk::k_qintt_radix<<<dim3(cdiv(n, 256), nc, 1), 256, 0, s>>>(d_cbuf.p, d_out.p, log_n, rb, 2 * N,
-                                                                 (uint64_t)nc * qdf * n,
-                                                                 gl::inv(gl::root_of_unity(rb)), gl::inv(B),
-                                                                 gl::inv(gl::pow(gl::GEN, n)));
+    // the prover's kernels: the single-read one for the leaf gate set, else
+    // the permutation terms and one launch per gate (QPGPU_QUOTIENT=onepass:
+    // any gate list in one pass)
+    const qpk::QuotientKernel qk =
+        fast ? qpk::QK_1R : getenv_flag_eq("QPGPU_QUOTIENT", "onepass") ? qpk::QK_ONEPASS : qpk::QK_PARTS;
+    qpk::quotient_values(a, qk, 1, s);
+    qpk::quotient_coeffs(ctx->tw, d_q.p, d_cbuf.p, d_out.p, log_n, rb, nc, 1, 2 * N, 2 * N, (uint64_t)nc * qdf * n, s);
     QP_HIP_TRY(ctx, hipGetLastError());
     QP_HIP_TRY(ctx, hipMemcpyAsync(quotient_coeffs_out, d_out.p, (uint64_t)nc * qdf * n * 8, hipMemcpyDeviceToHost, s));
     QP_HIP_TRY(ctx, hipStreamSynchronize(s));

@@ -114,6 +114,8 @@ def lib():
                                                   ctypes.POINTER(ctypes.c_size_t)]),
         "qp_circuit_constants_sigmas": (ctypes.c_int, [VP, U64P]),
         "qp_circuit_constants_sigmas_coeffs": (ctypes.c_int, [VP, U64P]),
+        "qp_circuit_prover_only_bytes": (ctypes.c_int, [VP, ctypes.c_char_p, ctypes.c_size_t,
+                                                        ctypes.POINTER(ctypes.c_size_t)]),
         "qp_wormhole_commit": (ctypes.c_int, [VP, VP, PP, ctypes.c_char_p, ctypes.c_size_t]),
         "qp_voting_circuit_new": (ctypes.c_int, [ctypes.c_int, PP]),
         "qp_voting_commit": (ctypes.c_int, [VP, VP, PP, ctypes.c_char_p, ctypes.c_size_t]),

@@ -84,6 +84,10 @@ class _LevelProver:
         if max_batch == 1:
             nprov = 1
         self.provers = [Prover(Context(device), self.circuit, max_batch=max_batch) for _ in range(nprov)]
+        # the provers split the process's host budget (qp_prover_set_host_threads:
+        # each would otherwise take min(hardware threads, 16))
+        for p in self.provers:
+            p.set_host_threads(max(1, _host_budget() // nprov))
         self.prover = self.provers[0]
         vd = self.prover.verifier_data()
         common = self.circuit.common_data()
@@ -176,14 +180,19 @@ def aggregation_circuit(inner_common: bytes, branching: int) -> Circuit:
 _pool = None
 
 
+def _host_budget() -> int:
+    """Host threads aggregation may use: QP_AGG_THREADS, else the process's CPU
+    budget (OMP_NUM_THREADS on the GPU boxes), at most 16."""
+    n = int(os.environ.get("QP_AGG_THREADS") or os.environ.get("OMP_NUM_THREADS") or min(os.cpu_count() or 4, 16))
+    return max(1, min(n, 16))
+
+
 def _witness_pool():
-    """Host threads for aggregation witnesses: QP_AGG_THREADS, else the
-    process's CPU budget (OMP_NUM_THREADS on the GPU boxes), at most 16."""
+    """Host threads for aggregation witnesses (the host-witness path)."""
     global _pool
     if _pool is None:
         import concurrent.futures
-        n = int(os.environ.get("QP_AGG_THREADS") or os.environ.get("OMP_NUM_THREADS") or min(os.cpu_count() or 4, 16))
-        _pool = concurrent.futures.ThreadPoolExecutor(max_workers=max(1, min(n, 16)))
+        _pool = concurrent.futures.ThreadPoolExecutor(max_workers=_host_budget())
     return _pool
 
 
@@ -261,8 +270,13 @@ def aggregate_to_tree(leaf_proofs, common_data: bytes, verifier_only: bytes,
     config = config or TreeAggregationConfig.default()
 
     def check(inner_common, proofs):
-        if backend is None and len(proofs) >= config.tree_branching_factor:
-            c = aggregation_circuit(inner_common, config.tree_branching_factor)
+        # every circuit the level builds: full chunks of k and a shorter tail
+        if backend is not None:
+            return None
+        k = config.tree_branching_factor
+        sizes = ([k] if len(proofs) >= k else []) + ([len(proofs) % k] if len(proofs) % k else [])
+        for size in sizes:
+            c = aggregation_circuit(inner_common, size)
             if c.degree_bits > GPU_MAX_DEGREE_BITS:
                 return c.degree_bits
         return None

@@ -307,6 +307,19 @@ class Circuit:
             raise QpError(rc, "qp_circuit_constants_sigmas_coeffs")
         return out
 
+    def prover_only_bytes(self):
+        """Upstream ProverOnlyCircuitData::to_bytes of this leaf circuit
+        (DefaultGeneratorSerializer; csrc/prover_bin.cpp, host only)."""
+        ln = ctypes.c_size_t()
+        rc = lib().qp_circuit_prover_only_bytes(self.h, None, 0, ctypes.byref(ln))
+        if rc:
+            raise QpError(rc, "qp_circuit_prover_only_bytes")
+        buf = ctypes.create_string_buffer(ln.value)
+        rc = lib().qp_circuit_prover_only_bytes(self.h, buf, ln.value, ctypes.byref(ln))
+        if rc:
+            raise QpError(rc, "qp_circuit_prover_only_bytes")
+        return buf.raw[:ln.value]
+
     def commit(self, inputs) -> Witness:
         """WormholeProver::commit (CircuitInputs) or VoteCircuitData::fill_targets
         (VoteCircuitData) followed by witness generation."""

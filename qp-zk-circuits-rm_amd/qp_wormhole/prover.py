@@ -202,26 +202,26 @@ def _shared(config, device):
 
 CONFIGS = ("standard_recursion_config", "standard_recursion_zk_config")
 
-# prover.bin of this backend.  plonky2's ProverOnlyCircuitData::to_bytes
-# (generators through DefaultGeneratorSerializer, the constants||sigmas
-# PolynomialBatch, fft root table, ...) has no fixture in the reference
-# (generated-bins/ is empty) and would be rebuilt by the device preprocessing
-# anyway, so the file records the circuit identity and its preprocessed
-# commitment: magic, version, circuit kind, zk flag, degree bits, SHA-256 of
-# common.bin, then the VerifierOnlyCircuitData bytes (constants||sigmas cap +
-# circuit digest).  Loading rebuilds the native circuit for that identity and
-# refuses data whose commitment differs.
+# prover.bin.  By default generate_circuit_binaries writes upstream plonky2's
+# ProverOnlyCircuitData::to_bytes through DefaultGeneratorSerializer, as the
+# reference's circuit-builder does (circuit-builder/src/lib.rs:53-59; read back
+# by WormholeProver::new_from_bytes, prover/src/lib.rs:104-137): the native
+# writer qp_circuit_prover_only_bytes (csrc/prover_bin.cpp, host only) emits the
+# generators with their tags and bodies, the watch index, the constants||sigmas
+# PolynomialBatch with its Merkle tree, the sigmas' transpose, the subgroup,
+# the public-input targets, the representative map, the fft root table and the
+# circuit digest.  read_upstream_prover_only walks that layout field by field
+# (restated from upstream plonky2's util/serialization; parity unpinned: the
+# reference commits no prover.bin -- what IS pinned is the commitment, equal to
+# the reference's verifier data), and upstream_prover_layout checks a walked
+# file against a circuit.
 #
-# An upstream prover.bin (ProverOnlyCircuitData::to_bytes of the reference's
-# generate_circuit_binaries, circuit-builder/src/lib.rs:54-60; read back by
-# WormholeProver::new_from_bytes, prover/src/lib.rs:105-137) is walked by
-# upstream_prover_layout: the framing is restated from upstream plonky2's
-# write_prover_only_circuit_data (parity unpinned: the reference commits no
-# such file) and the walk checks the CONTENT the preprocessing fixes, so a
-# truncated or foreign blob is refused even if it ends like one.  The native
-# circuit IS the reference's (same constants||sigmas columns, cap and circuit
-# digest: tests/test_reference_layout.py), so a file of the reference's circuit
-# passes; its generators are not needed (witness generation is native).
+# This backend's own, smaller prover.bin (prover_format="backend") records the
+# circuit identity and its preprocessed commitment: magic, version, circuit
+# kind, zk flag, degree bits, SHA-256 of common.bin, then the
+# VerifierOnlyCircuitData bytes (constants||sigmas cap + circuit digest).
+# Loading either rebuilds the native circuit and refuses data whose
+# preprocessing differs from it.
 PROVER_MAGIC = b"QPGPU-PROVER-ONLY\0"
 PROVER_VERSION = 1
 _KINDS = {"wormhole": 0, "voting": 1}
@@ -256,8 +256,14 @@ def _verifier_only(circuit, prover):
     return full[:len(full) - len(common)]
 
 
-def prover_only_bytes(circuit, prover):
-    """This backend's prover.bin for a built circuit and its device prover."""
+def prover_only_bytes(circuit, prover=None, prover_format="upstream"):
+    """prover.bin of a built leaf circuit: upstream ProverOnlyCircuitData::to_bytes
+    (default; host only) or, with prover_format="backend", this backend's
+    identity + commitment blob (needs the circuit's device prover)."""
+    if prover_format == "upstream":
+        return circuit.prover_only_bytes()
+    if prover_format != "backend":
+        raise ValueError(f"unknown prover.bin format {prover_format!r}")
     common = circuit.common_data()
     head = PROVER_MAGIC + struct.pack("<IBBI", PROVER_VERSION, _KINDS[circuit.kind], int(circuit.zk),
                                       circuit.degree_bits)
@@ -266,6 +272,7 @@ def prover_only_bytes(circuit, prover):
 
 # plonky2 Goldilocks POWER_OF_TWO_GENERATOR: w_{2^k} = TWO_ADIC_GEN^(2^(32-k))
 TWO_ADIC_GEN = 7277203076849721926
+_P = 0xFFFFFFFF00000001
 
 
 def _goldilocks_powers(w, n):
@@ -273,129 +280,288 @@ def _goldilocks_powers(w, n):
     x = 1
     for i in range(n):
         out[i] = x
-        x = x * w % 0xFFFFFFFF00000001
+        x = x * w % _P
     return out
 
 
-def upstream_prover_layout(data, circuit, cap=None):
-    """Walk an upstream ProverOnlyCircuitData::to_bytes file of `circuit` and
-    return its circuit digest (4 ints), or raise ValueError naming what is
-    missing.  Restated framing (plonky2 util/serialization write_prover_only_
-    circuit_data), in file order:
-      generators.len() u64, the generators (tag u32 + body each),
-      generator_indices_by_watches, then the constants||sigmas PolynomialBatch:
-      polynomials.len() u64 and per polynomial its coefficients as a field vec
-      (u64 length + values), the MerkleTree (leaves, digests, cap: u64 length +
-      16 hashes), degree_log, rate_bits, blinding; sigmas.len() u64 and the
-      sigma value vectors; the subgroup (powers of w_n); public-input targets;
-      representative_map; the fft root table (optional); circuit_digest
-      (4 u64); lookup_rows and lut_to_lookups (empty: two u64 zeros).
-    What is checked is what the preprocessing fixes: this circuit's
-    constants||sigmas coefficients (every column, consecutive), the cap
-    (when given: the caller's device-computed one), the 80 sigma value
-    columns, the subgroup, and the empty lookup tail.  The generator bodies and
-    the Merkle leaves/digests are skipped by search, so only their presence is
-    restated, not their layout."""
+# DefaultGeneratorSerializer (plonky2 util/serialization/generator_serialization.rs):
+# tag = index in its generator list; the leaf circuits' kinds and the fields of
+# their serialize() bodies (u: usize, f: field, t: target, U: usize vec)
+UPSTREAM_GENERATORS = {
+    0: ("ArithmeticBaseGenerator", "uffu"),   # row, const_0, const_1, i
+    2: ("BaseSplitGenerator", "uu"),          # row, num_limbs
+    4: ("ConstantGenerator", "uuuf"),         # row, constant_index, wire_index, constant
+    7: ("EqualityGenerator", "tttt"),         # x, y, equal, inv
+    15: ("PoseidonGenerator", "u"),           # row
+    19: ("RandomValueGenerator", "t"),        # target
+    23: ("WireSplitGenerator", "tUu"),        # integer, gates, num_limbs
+}
+
+
+class _Walk:
+    """Cursor over upstream plonky2 serialization (little-endian; usize = u64;
+    every vector = u64 length + elements)."""
+
+    def __init__(self, data):
+        self.d = data
+        self.p = 0
+
+    def need(self, k, what):
+        if k < 0 or self.p + k > len(self.d):
+            raise ValueError(f"truncated in {what} at offset {self.p}")
+
+    def u8(self, what="u8"):
+        self.need(1, what)
+        self.p += 1
+        return self.d[self.p - 1]
+
+    def u32(self, what="u32"):
+        self.need(4, what)
+        (v,) = struct.unpack_from("<I", self.d, self.p)
+        self.p += 4
+        return v
+
+    def u64(self, what="usize"):
+        self.need(8, what)
+        (v,) = struct.unpack_from("<Q", self.d, self.p)
+        self.p += 8
+        return v
+
+    def u64s(self, n, what):
+        if n > (len(self.d) - self.p) // 8:
+            raise ValueError(f"truncated in {what} at offset {self.p} ({n} words announced)")
+        a = np.frombuffer(self.d, np.uint64, n, self.p)
+        self.p += 8 * n
+        return a
+
+    def vec(self, what):
+        return self.u64s(self.u64(what), what)
+
+    def fields(self, n, what):
+        a = self.u64s(n, what)
+        if (a >= _P).any():
+            raise ValueError(f"non-canonical field element in {what}")
+        return a
+
+    def field_vec(self, what):
+        return self.fields(self.u64(what), what)
+
+    def target(self, what="target"):
+        b = self.u8(what)
+        if b == 1:
+            return ("wire", self.u64(what), self.u64(what))
+        if b == 0:
+            return ("virtual", self.u64(what))
+        raise ValueError(f"malformed target in {what} at offset {self.p - 1}")
+
+
+def read_upstream_prover_only(data):
+    """Walk an upstream ProverOnlyCircuitData::to_bytes file (plonky2
+    write_prover_only_circuit_data, restated; parity unpinned) of a lookup-free
+    leaf circuit and return its fields, or raise ValueError naming the first
+    thing that does not parse: a truncation, a foreign generator tag, a
+    non-canonical element, a malformed section, bytes past the end."""
     data = bytes(data)
     if data[:len(PROVER_MAGIC)] == PROVER_MAGIC:
         raise ValueError("this backend's prover.bin, not an upstream one")
-    if len(data) < 8 + 48 or data[-16:] != bytes(16):
-        raise ValueError("does not end with the circuit digest and empty lookup tables")
-    (ngen,) = struct.unpack_from("<Q", data, 0)
-    dig = struct.unpack_from("<4Q", data, len(data) - 48)
-    if not 0 < ngen < len(data) // 8 or any(x >= 0xFFFFFFFF00000001 for x in dig):
-        raise ValueError("implausible generator count or non-canonical digest")
+    w = _Walk(data)
+    out = {}
+    ngen = w.u64("generators")
+    if not 0 < ngen <= len(data) // 8:
+        raise ValueError(f"implausible generator count {ngen}")
+    gens = []
+    for i in range(ngen):
+        tag = w.u32("generator tag")
+        if tag not in UPSTREAM_GENERATORS:
+            raise ValueError(f"generator {i}: tag {tag} is not one of the leaf circuits' generator kinds "
+                             f"(foreign generator)")
+        name, body = UPSTREAM_GENERATORS[tag]
+        fields = []
+        for k in body:
+            if k == "u":
+                fields.append(w.u64(name))
+            elif k == "f":
+                f = w.u64(name)
+                if f >= _P:
+                    raise ValueError(f"generator {i} ({name}): non-canonical field element")
+                fields.append(f)
+            elif k == "t":
+                fields.append(w.target(name))
+            else:
+                fields.append([int(x) for x in w.vec(name)])
+        gens.append((name, fields))
+    out["generators"] = gens
+    nw = w.u64("generator_indices_by_watches")
+    watches, last = {}, -1
+    for _ in range(nw):
+        key = w.u64("watch key")
+        if key <= last:
+            raise ValueError("generator_indices_by_watches keys out of order")
+        idx = w.vec("watch indices")
+        if len(idx) == 0 or (idx >= ngen).any():
+            raise ValueError("generator_indices_by_watches names no or unknown generators")
+        watches[key] = idx
+        last = key
+    out["watches"] = watches
+    # constants_sigmas_commitment: PolynomialBatch
+    npoly = w.u64("polynomials")
+    if not 0 < npoly <= 1024:
+        raise ValueError(f"implausible polynomial count {npoly}")
+    polys = [w.field_vec(f"polynomial {c}") for c in range(npoly)]
+    if len({len(p) for p in polys}) != 1:
+        raise ValueError("constants||sigmas polynomials of different lengths")
+    out["coeffs"] = np.stack(polys)
+    nleaves = w.u64("merkle leaves")
+    width = w.u64("merkle leaf") if nleaves else 0
+    w.p -= 8 if nleaves else 0
+    rows = w.u64s(nleaves * (1 + width), "merkle leaves").reshape(nleaves, 1 + width) if nleaves else None
+    if nleaves and ((rows[:, 0] != width).any() or width != npoly):
+        raise ValueError("merkle leaves of the wrong width")
+    if nleaves and (rows[:, 1:] >= _P).any():
+        raise ValueError("non-canonical field element in merkle leaves")
+    out["leaves"] = rows[:, 1:] if nleaves else np.zeros((0, 0), np.uint64)
+    nd = w.u64("merkle digests")
+    out["digests"] = w.fields(4 * nd, "merkle digests").reshape(nd, 4)
+    cap_h = w.u64("merkle cap height")
+    if cap_h > 20:
+        raise ValueError(f"implausible cap height {cap_h}")
+    out["cap"] = w.fields(4 << cap_h, "merkle cap")
+    if nd != 2 * (nleaves - (1 << cap_h)) if nleaves >= (1 << cap_h) else nd != 0:
+        raise ValueError(f"{nd} digests for {nleaves} leaves under a height-{cap_h} cap")
+    out["degree_log"] = w.u64("degree_log")
+    out["rate_bits"] = w.u64("rate_bits")
+    out["blinding"] = w.u8("blinding")
+    if out["blinding"] > 1:
+        raise ValueError("malformed blinding flag")
+    n = 1 << out["degree_log"] if out["degree_log"] < 32 else 0
+    if out["coeffs"].shape[1] != n or nleaves != n << out["rate_bits"]:
+        raise ValueError("polynomial / leaf counts disagree with degree_log and rate_bits")
+    # sigmas: the transpose of the sigma polynomials, n rows
+    nrows = w.u64("sigmas")
+    if nrows != n:
+        raise ValueError(f"{nrows} sigma rows for degree {n}")
+    r0 = w.u64("sigma row")
+    w.p -= 8
+    sg = w.u64s(nrows * (1 + r0), "sigmas").reshape(nrows, 1 + r0)
+    if (sg[:, 0] != r0).any() or (sg[:, 1:] >= _P).any():
+        raise ValueError("malformed sigma rows")
+    out["sigmas"] = sg[:, 1:]
+    out["subgroup"] = w.field_vec("subgroup")
+    npi = w.u64("public inputs")
+    if npi > len(data):
+        raise ValueError("implausible public-input count")
+    out["public_inputs"] = [w.target("public inputs") for _ in range(npi)]
+    rep = w.vec("representative_map")
+    if len(rep) < n * 1 or (rep >= len(rep)).any() or (rep[rep] != rep).any():
+        raise ValueError("representative_map is not a compressed forest")
+    out["representative_map"] = rep
+    has = w.u8("fft_root_table")
+    table = None
+    if has == 1:
+        table = [w.field_vec("fft_root_table row") for _ in range(w.u64("fft_root_table"))]
+    elif has != 0:
+        raise ValueError("malformed fft_root_table flag")
+    out["fft_root_table"] = table
+    out["circuit_digest"] = tuple(int(x) for x in w.fields(4, "circuit digest"))
+    if w.u64("lookup_rows") != 0 or w.u64("lut_to_lookups") != 0:
+        raise ValueError("lookup tables present (the leaf circuits have none)")
+    if w.p != len(data):
+        raise ValueError(f"{len(data) - w.p} bytes past lut_to_lookups")
+    return out
+
+
+def _hash(v):
+    from ._native import hash_no_pad
+    return hash_no_pad(np.asarray(v, np.uint64))
+
+
+def _merkle_subtree_ok(leaves, digests, cap, k, ncap):
+    """hash/merkle_tree.rs fill_subtree layout of cap subtree k: rebuild its
+    digests from its leaves and compare them and the cap entry."""
+    nl = len(leaves) // ncap
+    nd = len(digests) // ncap
+    L = leaves[k * nl:(k + 1) * nl]
+    D = digests[k * nd:(k + 1) * nd]
+
+    def fill(lo, nleaves, dlo, nd_):
+        if nd_ == 0:
+            row = L[lo]
+            return _hash(row) if len(row) > 4 else [int(x) for x in row] + [0] * (4 - len(row))
+        half = nd_ // 2
+        left = fill(lo, nleaves // 2, dlo, half - 1)
+        right = fill(lo + nleaves // 2, nleaves // 2, dlo + half + 1, half - 1)
+        if [int(x) for x in D[dlo + half - 1]] != left or [int(x) for x in D[dlo + half]] != right:
+            raise ValueError(f"merkle digests of cap subtree {k} do not hash up from its leaves")
+        return _hash(left + right)
+    if fill(0, nl, 0, nd) != [int(x) for x in cap[4 * k:4 * k + 4]]:
+        raise ValueError(f"cap entry {k} is not the root of its subtree")
+
+
+def upstream_prover_layout(data, circuit, cap=None, check_subtrees=1):
+    """Walk an upstream prover.bin (read_upstream_prover_only) and check it
+    against `circuit`; return its circuit digest (4 ints), or raise ValueError.
+    Checked: the generators are the circuit's kinds and counts (one
+    PoseidonGenerator per Poseidon row, num_ops ArithmeticBaseGenerators per
+    arithmetic row, one BaseSplitGenerator per BaseSum row, the PublicInputGate
+    row's RandomValueGenerators), the constants||sigmas coefficients, degree,
+    rate and blinding, the sigmas, the subgroup, the public-input count, the
+    fft root table; the Merkle cap (against `cap` when given: the caller's
+    device-computed or reference one), the first `check_subtrees` cap subtrees
+    rebuilt from their leaves, the leaves' first row against the coefficients'
+    value at g (the coset LDE's first leaf), and the digest as
+    hash_no_pad(cap || hash_pad([]) || degree_bits)."""
+    f = read_upstream_prover_only(data)
     n = circuit.n
-    N = struct.pack("<Q", n)
-    coeffs = circuit.constants_sigmas_coeffs()
+    if f["degree_log"] != circuit.degree_bits or f["rate_bits"] != 3 or f["blinding"]:
+        raise ValueError("degree, rate or blinding differ from this circuit's")
+    co = circuit.constants_sigmas_coeffs()
+    if f["coeffs"].shape != co.shape:
+        raise ValueError("constants||sigmas polynomial count differs from this circuit's")
+    for c in range(co.shape[0]):
+        if not np.array_equal(f["coeffs"][c], co[c]):
+            raise ValueError(f"constants||sigmas coefficient column {c} differs from this circuit's")
     vals = circuit.constants_sigmas()
-    ncs = coeffs.shape[0]
-
-    def column(pos, arr, what):
-        blob = N + arr.tobytes()
-        if data[pos:pos + len(blob)] != blob:
-            raise ValueError(f"{what} does not follow at offset {pos}")
-        return pos + len(blob)
-
-    # the PolynomialBatch's coefficient columns: located by column 0, then every
-    # column must follow at the same gap (0 or 8 extra bytes per polynomial)
-    p0 = data.find(N + coeffs[0].tobytes(), 8 + 8 * ngen)
-    if p0 < 0:
-        raise ValueError("constants||sigmas coefficients of this circuit not found")
-    if struct.pack("<Q", ncs) not in data[max(0, p0 - 16):p0]:
-        raise ValueError("polynomial count missing before the coefficients")
-    e = p0 + 8 + 8 * n
-    gap = None
-    for g in (0, 8):
-        if data[e + g:e + g + 8 + 8 * n] == N + coeffs[1].tobytes():
-            gap = g
-            break
-    if gap is None:
-        raise ValueError("constants||sigmas coefficient column 1 does not follow column 0")
-    for c in range(1, ncs):
-        e = column(e + gap, coeffs[c], f"coefficient column {c}")
-    # the Merkle tree's cap (the leaves and digests precede it)
-    pos = e
-    if cap is not None:
-        cb = struct.pack("<Q", len(cap) // 4) + np.ascontiguousarray(cap, dtype=np.uint64).tobytes()
-        pc = data.find(cb, e)
-        if pc < 0:
-            raise ValueError("constants||sigmas Merkle cap differs from this circuit's")
-        pos = pc + len(cb)
-    # sigmas: count, then the value vectors
-    nsig = ncs - circuit.num_constants
-    ps = data.find(struct.pack("<Q", nsig) + N + vals[circuit.num_constants].tobytes(), pos)
-    if ps < 0:
-        raise ValueError("sigma columns of this circuit not found")
-    e = ps + 8
-    for j in range(nsig):
-        e = column(e, vals[circuit.num_constants + j], f"sigma column {j}")
-    # subgroup: powers of w_n
-    w = pow(TWO_ADIC_GEN, 1 << (32 - circuit.degree_bits), 0xFFFFFFFF00000001)
-    e = column(e, _goldilocks_powers(w, n), "subgroup")
-    # public_inputs: target vec (write_target: bool Wire? + row, column | index)
-    end = len(data) - 48
-    try:
-        (npi,) = struct.unpack_from("<Q", data, e)
-        if npi != circuit.num_public_inputs:
-            raise ValueError(f"{npi} public-input targets, the circuit has {circuit.num_public_inputs}")
-        e += 8
-        for _ in range(npi):
-            e += 17 if data[e] == 1 else 9 if data[e] == 0 else 1 << 62
-        # representative_map: one entry per wire target and virtual target
-        (nrep,) = struct.unpack_from("<Q", data, e)
-        if nrep < n * circuit.num_wires:
-            raise ValueError(f"representative_map of {nrep} entries for {n} x {circuit.num_wires} wires")
-        e += 8 + 8 * nrep
-        # fft_root_table: Option<Vec<Vec<F>>>
-        if data[e] == 1:
-            (k,) = struct.unpack_from("<Q", data, e + 1)
-            e += 9
-            for _ in range(k):
-                (m,) = struct.unpack_from("<Q", data, e)
-                e += 8 + 8 * m
-        elif data[e] == 0:
-            e += 1
-        else:
-            raise ValueError("malformed fft_root_table")
-    except (struct.error, IndexError):
-        raise ValueError("truncated after the subgroup") from None
-    if e != end:
-        raise ValueError(f"{end - e} bytes between the fft root table and the circuit digest")
-    return dig
-
-
-def upstream_prover_digest(data):
-    """Circuit digest of a blob that ENDS like an upstream prover.bin (no
-    structural walk; upstream_prover_layout does that), or None."""
-    data = bytes(data)
-    if data[:len(PROVER_MAGIC)] == PROVER_MAGIC or len(data) < 8 + 48 or data[-16:] != bytes(16):
-        return None
-    (ngen,) = struct.unpack_from("<Q", data, 0)
-    dig = struct.unpack_from("<4Q", data, len(data) - 48)
-    if not 0 < ngen < len(data) or any(x >= 0xFFFFFFFF00000001 for x in dig):
-        return None
-    return dig
+    sig = vals[circuit.num_constants:]
+    if f["sigmas"].shape != (n, sig.shape[0]) or not np.array_equal(f["sigmas"], sig.T):
+        raise ValueError("sigma rows differ from this circuit's sigma columns")
+    wn = pow(TWO_ADIC_GEN, 1 << (32 - circuit.degree_bits), _P)
+    if not np.array_equal(f["subgroup"], _goldilocks_powers(wn, n)):
+        raise ValueError("subgroup is not the powers of w_n")
+    if len(f["public_inputs"]) != circuit.num_public_inputs:
+        raise ValueError(f"{len(f['public_inputs'])} public-input targets, the circuit has "
+                         f"{circuit.num_public_inputs}")
+    gk, rows = circuit.census()
+    count = {}
+    for name, _ in f["generators"]:
+        count[name] = count.get(name, 0) + 1
+    want = {"PoseidonGenerator": rows["poseidon"], "BaseSplitGenerator": rows["base_sum"],
+            "ArithmeticBaseGenerator": rows["arithmetic"] * (circuit.num_routed_wires // 4),
+            "RandomValueGenerator": circuit.num_wires - 4}
+    for name, k in want.items():
+        if count.get(name, 0) != k:
+            raise ValueError(f"{count.get(name, 0)} {name}s, the circuit needs {k}")
+    tab = f["fft_root_table"]
+    if tab is None or [len(r) for r in tab] != [max(1 << (m - 1), 2) for m in range(1, len(tab) + 1)]:
+        raise ValueError("fft_root_table missing or of the wrong shape")
+    fcap = f["cap"]
+    if cap is not None and not np.array_equal(fcap, np.asarray(cap, np.uint64)):
+        raise ValueError("constants||sigmas Merkle cap differs from this circuit's")
+    # leaf 0 is the LDE at g (rev(0) = 0): each column's polynomial at the shift
+    g0 = [0] * co.shape[0]
+    for c in range(co.shape[0]):
+        acc = 0
+        for x in reversed([int(v) for v in co[c]]):
+            acc = (acc * 0xC65C18B67785D900 + x) % _P
+        g0[c] = acc
+    if [int(x) for x in f["leaves"][0]] != g0:
+        raise ValueError("merkle leaf 0 is not the constants||sigmas LDE at the coset shift")
+    ncap = len(fcap) // 4
+    for k in range(min(check_subtrees, ncap)):
+        _merkle_subtree_ok(f["leaves"], f["digests"], fcap, k, ncap)
+    dsep = _hash([1, 0, 0, 0, 0, 0, 0, 1])
+    if tuple(_hash(list(fcap) + dsep + [circuit.degree_bits])) != f["circuit_digest"]:
+        raise ValueError("circuit digest is not the hash of the cap and degree")
+    return f["circuit_digest"]
 
 
 def _parse_prover_only(data, common_bytes, circuit=None, vo=None):
@@ -405,7 +571,10 @@ def _parse_prover_only(data, common_bytes, circuit=None, vo=None):
     cap of its VerifierOnlyCircuitData bytes `vo`."""
     data = bytes(data)
     n = len(PROVER_MAGIC)
-    if data[:n] != PROVER_MAGIC and upstream_prover_digest(data) is not None:
+    if data[:n] != PROVER_MAGIC:
+        if len(data) < 8 + 48 or data[-16:] != bytes(16):
+            raise ValueError("neither this backend's prover.bin (bad magic) nor an upstream plonky2 "
+                             "ProverOnlyCircuitData::to_bytes file of a lookup-free circuit")
         if circuit is None:
             raise ValueError("an upstream prover.bin needs the circuit to be checked against")
         cap = None
@@ -413,9 +582,8 @@ def _parse_prover_only(data, common_bytes, circuit=None, vo=None):
             (h,) = struct.unpack_from("<Q", vo, 0)
             cap = np.frombuffer(vo, np.uint64, 4 << h, 8)
         return None, None, upstream_prover_layout(data, circuit, cap)
-    if len(data) < n + 10 + 32 or data[:n] != PROVER_MAGIC:
-        raise ValueError("neither this backend's prover.bin (bad magic) nor an upstream plonky2 "
-                         "ProverOnlyCircuitData::to_bytes file of a lookup-free circuit")
+    if len(data) < n + 10 + 32:
+        raise ValueError("truncated prover.bin header")
     version, kind, zk, degree_bits = struct.unpack_from("<IBBI", data, n)
     if version != PROVER_VERSION:
         raise ValueError(f"unsupported version {version}")
@@ -459,18 +627,20 @@ def _common_degree_bits(cb):
         return None
 
 
-def generate_circuit_binaries(output_dir, include_prover=True, config="standard_recursion_config", device=0):
+def generate_circuit_binaries(output_dir, include_prover=True, config="standard_recursion_config", device=0,
+                              prover_format="upstream"):
     """wormhole/circuit-builder/src/lib.rs:11-66: build the circuit and write
     common.bin (CommonCircuitData::to_bytes), verifier.bin
-    (VerifierOnlyCircuitData::to_bytes) and, if asked, prover.bin (this
-    backend's format, see PROVER_MAGIC)."""
+    (VerifierOnlyCircuitData::to_bytes) and, if asked, prover.bin: upstream
+    ProverOnlyCircuitData::to_bytes (default) or this backend's identity +
+    commitment blob (prover_format="backend", see PROVER_MAGIC)."""
     ctx, circ, prover, lock = _shared(config, device)
     os.makedirs(output_dir, exist_ok=True)
     with open(os.path.join(output_dir, "common.bin"), "wb") as f:
         f.write(circ.common_data())
     with lock:
         vd = _verifier_only(circ, prover)
-        pb = prover_only_bytes(circ, prover) if include_prover else None
+        pb = prover_only_bytes(circ, prover, prover_format) if include_prover else None
     with open(os.path.join(output_dir, "verifier.bin"), "wb") as f:
         f.write(vd)
     if include_prover:

@@ -209,3 +209,16 @@ def test_unsupported_inner_circuit_is_an_error(ref):
     cb[-4 - 4] ^= 0xFF  # corrupt the last gate's tag
     with pytest.raises(QpError):
         Circuit.aggregation(bytes(cb), 2)
+
+
+def test_too_large_level_is_refused_before_proving(ref):
+    """aggregate_to_tree sizes every circuit a level builds -- also a lone short
+    chunk (fewer proofs than the branching factor): 9 leaf proofs in one chunk
+    need 2^16 rows, past the GPU prover's 2^15, so CircuitTooLarge is raised
+    before any proving (no GPU needed to see it)."""
+    import qp_wormhole
+    from qp_wormhole.aggregator import CircuitTooLarge, TreeAggregationConfig
+    cb, vo, leaves = ref
+    with pytest.raises(CircuitTooLarge, match="2\\^16") as e:
+        qp_wormhole.aggregate_to_tree([leaves[0]] * 9, cb, vo, TreeAggregationConfig.new(10, 1))
+    assert e.value.proofs == []

@@ -140,6 +140,28 @@ def test_tree_of_2048_leaves_reaches_a_degree15_root(reference_leaves):
         assert pis[16 * k:16 * k + 16] == list(struct.unpack_from("<16Q", pf, len(pf) - 128))
 
 
+@pytest.mark.parametrize("k", [3, 4, 5, 6, 7])
+def test_k_ary_depth_two_trees(reference_leaves, k):
+    """The reference's tree shapes TreeAggregationConfig::new(k, 2), k = 3..7
+    (benches/aggregator.rs:119-123): k^2 of the reference's own leaf proofs
+    through k level-1 proofs (degree 2^14 for k = 3, 4; 2^15 for k >= 5) to a
+    root (2^14 / 2^15) that verifies and carries every leaf's public inputs in
+    order."""
+    import struct
+    import qp_wormhole
+    from qp_wormhole.aggregator import TreeAggregationConfig
+    from qp_wormhole.prover import _common_degree_bits
+    cb, vo, leaves = reference_leaves
+    ls = [leaves[(i * 5 + i // 3) % 2] for i in range(k * k)]
+    root = qp_wormhole.aggregate_to_tree(ls, cb, vo, TreeAggregationConfig.new(k, 2))
+    assert _common_degree_bits(root.circuit_data.common) == (14 if k == 3 else 15)
+    assert verify(root.circuit_data.verifier_data(), root.proof.to_bytes()) == 0
+    want = []
+    for pf in ls:
+        want += list(struct.unpack_from("<16Q", pf, len(pf) - 128))
+    assert root.proof.public_inputs == want
+
+
 def _device_vs_host(circ, vo, chunks, zk=None):
     """qp_prover_prove_aggregation (witness generated on the device) vs the host
     witness path (qp_aggregation_commit + qp_prover_prove) of the same chunks."""

@@ -21,12 +21,21 @@ def bins(tmp_path_factory):
     return d
 
 
-def test_binaries_written(bins):
+def test_binaries_written(bins, tmp_path):
+    """prover.bin is upstream ProverOnlyCircuitData::to_bytes by default (its
+    commitment equal to the written verifier.bin's, i.e. the device prover's);
+    prover_format="backend" writes this backend's identity + commitment blob."""
+    import struct
     import qp_wormhole
+    from qp_wormhole.prover import read_upstream_prover_only
     common = open(bins / "common.bin", "rb").read()
     assert common == qp_wormhole.Circuit.wormhole().common_data()
-    assert len(open(bins / "verifier.bin", "rb").read()) == 8 + 16 * 32 + 32  # as bench-data/verifier.bin
-    assert open(bins / "prover.bin", "rb").read().startswith(b"QPGPU-PROVER-ONLY")
+    vo = open(bins / "verifier.bin", "rb").read()
+    assert len(vo) == 8 + 16 * 32 + 32  # as bench-data/verifier.bin
+    f = read_upstream_prover_only(open(bins / "prover.bin", "rb").read())
+    assert f["cap"].tobytes() == vo[8:8 + 512] and f["circuit_digest"] == struct.unpack_from("<4Q", vo, 8 + 512)
+    qp_wormhole.generate_circuit_binaries(str(tmp_path), prover_format="backend")
+    assert open(tmp_path / "prover.bin", "rb").read().startswith(b"QPGPU-PROVER-ONLY")
 
 
 def test_new_from_files_proves_and_verifies(bins):
@@ -49,37 +58,27 @@ def test_new_from_bytes_errors(bins):
     with pytest.raises(ValueError, match="Failed to deserialize prover only data"):
         WormholeProver.new_from_bytes(b"junk" + prover, common)
     bad = bytearray(prover)
-    bad[-1] ^= 1  # the stored commitment
-    with pytest.raises(ValueError, match="commitment differs"):
+    bad[-17] ^= 1  # the stored circuit digest
+    with pytest.raises(ValueError, match="Failed to deserialize prover only data"):
         WormholeProver.new_from_bytes(bytes(bad), common)
 
 
-def test_new_from_bytes_takes_an_upstream_prover_bin(bins):
-    """A ProverOnlyCircuitData::to_bytes-framed file carrying the Wormhole circuit
-    digest (the reference's generate_circuit_binaries output) loads, proves and
-    verifies; one with another digest is refused."""
-    import struct
-    import numpy as np
+def test_new_from_bytes_backend_blob_and_commitment(bins, tmp_path):
+    """This backend's prover.bin loads too; one whose stored commitment differs
+    from the circuit's is refused."""
     import qp_wormhole
     from qp_wormhole import WormholeProver
-    from upstream_prover_bin import upstream_prover_bin
     common = open(bins / "common.bin", "rb").read()
-    vo = open(bins / "verifier.bin", "rb").read()
-    dig = struct.unpack_from("<4Q", vo, len(vo) - 32)
-    circ = qp_wormhole.Circuit.wormhole()
-    up = upstream_prover_bin(circ, np.frombuffer(vo, np.uint64, 64, 8), dig)
-    wp = WormholeProver.new_from_bytes(up, common)
-    proof = wp.commit(WI.test_inputs()).prove()
-    vd = vo + common
-    from oracle_lib import lib as olib
-    pb = proof.to_bytes()
+    qp_wormhole.generate_circuit_binaries(str(tmp_path), prover_format="backend")
+    blob = open(tmp_path / "prover.bin", "rb").read()
+    wp = WormholeProver.new_from_bytes(blob, common)
+    pb = wp.commit(WI.test_inputs()).prove().to_bytes()
+    vd = open(bins / "verifier.bin", "rb").read() + common
     assert olib().ora_verify(vd, len(vd), pb, len(pb)) == 0
-    bad = upstream_prover_bin(circ, np.frombuffer(vo, np.uint64, 64, 8), [dig[0] ^ 1] + list(dig[1:]))
+    bad = bytearray(blob)
+    bad[-1] ^= 1  # the stored commitment
     with pytest.raises(ValueError, match="commitment differs"):
-        WormholeProver.new_from_bytes(bad, common)
-    foreign = struct.pack("<Q", 1500) + b"\x11" * 40000 + struct.pack("<4Q", *dig) + bytes(16)
-    with pytest.raises(ValueError, match="not found"):
-        WormholeProver.new_from_bytes(foreign, common)
+        WormholeProver.new_from_bytes(bytes(bad), common)
 
 
 def test_zk_binaries_and_default(bins, tmp_path, monkeypatch):
@@ -88,9 +87,17 @@ def test_zk_binaries_and_default(bins, tmp_path, monkeypatch):
     qp_wormhole.generate_circuit_binaries(str(tmp_path / "zk"), config="standard_recursion_zk_config")
     p = WormholeProver.new_from_files(tmp_path / "zk" / "prover.bin", tmp_path / "zk" / "common.bin")
     assert p.config == "standard_recursion_zk_config"
-    # prover.bin of one config does not load with the other's common data
+    # the two configs share their preprocessing (no salt, no blinding rows under
+    # no_random), so their upstream prover.bin is the same file; the common data
+    # decides the config.  This backend's blob names its common data and refuses
+    # the other config's
+    assert open(tmp_path / "zk" / "prover.bin", "rb").read() == open(bins / "prover.bin", "rb").read()
+    assert WormholeProver.new_from_files(tmp_path / "zk" / "prover.bin", bins / "common.bin").config == \
+        "standard_recursion_config"
+    qp_wormhole.generate_circuit_binaries(str(tmp_path / "zkb"), config="standard_recursion_zk_config",
+                                          prover_format="backend")
     with pytest.raises(ValueError, match="different common data"):
-        WormholeProver.new_from_files(tmp_path / "zk" / "prover.bin", bins / "common.bin")
+        WormholeProver.new_from_files(tmp_path / "zkb" / "prover.bin", bins / "common.bin")
     # default(): generated-bins/ in the working directory, else a fresh build
     monkeypatch.chdir(tmp_path)
     assert WormholeProver.default().config == "standard_recursion_config"

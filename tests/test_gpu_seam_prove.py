@@ -46,3 +46,31 @@ def test_seam_composed_voting_proof(ctx):
     whole = qp_wormhole.Prover(ctx, circ, 1)
     assert seam == whole.prove_witnesses([w])[0]
     assert verify(whole.verifier_data(), seam) == 0
+
+
+def test_seam_composed_degree15_aggregation_proof(ctx):
+    """tree.rs:136's CircuitData::prove at degree 2^15 through the seams: the
+    aggregation circuit of five of the reference's own leaf proofs (level 1 of a
+    5-ary tree, benches/aggregator.rs:119-123; a 2048-leaf root has this degree
+    too).  qp_quotient's coset iNTT and the commitments take their large-n forms;
+    bytes == the GPU whole-circuit prover's == the oracle's, and it verifies."""
+    import qp_wormhole
+    from current_circuit_vd import current_circuit_verifier_data
+    from oracle_lib import golden
+    from test_oracle_golden import current_common_bytes
+    cb = current_common_bytes()
+    vd = current_circuit_verifier_data(cb)[0]
+    vo = vd[:len(vd) - len(cb)]
+    leaves = [golden("dummy_proof.bin"), golden("dummy_proof_zk.bin")]
+    chunk = [leaves[i % 2] for i in range(5)]
+    circ = qp_wormhole.Circuit.aggregation(cb, 5)
+    assert circ.degree_bits == 15
+    w = circ.commit_proofs(vo, chunk)
+    wires, pis = w.wires(), w.public_inputs()
+    seam = prove(ctx, circ, wires, pis)
+    whole = qp_wormhole.Prover(ctx, circ, 1)
+    assert seam == whole.prove_witnesses([w])[0]
+    cpu, ovd = oracle_prove(circ, wires, pis)
+    assert seam == cpu
+    assert verify(ovd, seam) == 0
+    whole.free()

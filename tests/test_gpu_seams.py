@@ -101,11 +101,13 @@ RECURSION_GATES = [
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("log_n", [8, 10])
+@pytest.mark.parametrize("log_n", [8, 10, 15])
 def test_quotient_recursion_gate_set_matches_oracle(ctx, log_n):
     """qp_quotient over the aggregator circuits' gate list (generic kernel) vs the
     descriptor-driven oracle; random selector values make every gate's filter
-    nonzero, so every constraint of every gate reaches the quotient."""
+    nonzero, so every constraint of every gate reaches the quotient.  2^15: the
+    degree of a 5- to 7-ary level-1 circuit and of a 2048-leaf root (the coset
+    iNTT's large-n form)."""
     import ctypes
 
     import qp_wormhole

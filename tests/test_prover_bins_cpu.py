@@ -1,8 +1,9 @@
-"""prover.bin parsing on the host (no GPU): this backend's format, an upstream
-plonky2 ProverOnlyCircuitData file recognised by its circuit digest (the native
-circuit is the reference's, so the reference's digest matches), and clear errors
-for anything else or a header that disagrees with the common data
-(wormhole/prover/src/lib.rs:105-187)."""
+"""prover.bin on the host (no GPU): upstream plonky2 ProverOnlyCircuitData::to_bytes
+written by the native writer (csrc/prover_bin.cpp) and walked section by section
+by the reader (qp_wormhole.prover.read_upstream_prover_only), this backend's own
+format, and clear errors for anything else or a header that disagrees with the
+common data (wormhole/circuit-builder/src/lib.rs:53-59,
+wormhole/prover/src/lib.rs:105-187)."""
 import hashlib
 import struct
 
@@ -59,45 +60,97 @@ def test_host_coefficients_are_the_constants_sigmas_polynomials(circ):
             assert acc == int(vals[col][i])
 
 
-def test_upstream_prover_bin_walked_against_the_circuit(circ):
-    """A file framed as upstream ProverOnlyCircuitData::to_bytes carrying this
-    circuit's preprocessing (the reference's cap and digest, reconstructed from
-    its own proofs; the native circuit's columns) is accepted, with either
-    length-prefix gap; its digest is the reference's."""
-    from upstream_prover_bin import upstream_prover_bin
+@pytest.fixture(scope="module")
+def upstream(circ):
+    """The native writer's upstream prover.bin (qp_circuit_prover_only_bytes)."""
+    return circ.prover_only_bytes()
+
+
+def test_upstream_prover_bin_round_trip(circ, upstream):
+    """writer -> structural reader -> checks: every section parses in
+    write_prover_only_circuit_data order and ends exactly; the commitment inside
+    (constants||sigmas cap, computed on the host from the LDE rows, and the
+    circuit digest) equals the reference's own verifier data -- reconstructed
+    from the reference's proofs, so this part is pinned; the rest (generator
+    order and bodies, watch index, representative map) is restated from
+    upstream plonky2, parity unpinned."""
+    vo, dig = _reference_vd()
+    cap = np.frombuffer(vo, np.uint64, 64, 8)
+    f = P.read_upstream_prover_only(upstream)
+    assert np.array_equal(f["cap"], cap) and list(f["circuit_digest"]) == dig
+    assert f["degree_log"] == 13 and f["rate_bits"] == 3 and not f["blinding"]
+    assert f["leaves"].shape == (1 << 16, 84) and f["digests"].shape == (2 * ((1 << 16) - 16), 4)
+    assert f["sigmas"].shape == (circ.n, 80)
+    # write_merkle_cap: the cap is prefixed by its HEIGHT (log2 of 16 hashes), as
+    # in VerifierOnlyCircuitData (verifier.bin, a reference fixture)
+    k = upstream.find(cap.tobytes())
+    assert k > 0 and struct.unpack_from("<Q", upstream, k - 8)[0] == 4 == struct.unpack_from("<Q", vo, 0)[0]
+    names = {}
+    for name, _ in f["generators"]:
+        names[name] = names.get(name, 0) + 1
+    gens, rows = circ.census()
+    assert names["PoseidonGenerator"] == rows["poseidon"] and names["RandomValueGenerator"] == 131
+    assert names["EqualityGenerator"] == gens["equality"]
+    assert names["ArithmeticBaseGenerator"] == 20 * rows["arithmetic"]
+    # every generator's watched targets are indexed under their representatives
+    rep = f["representative_map"]
+    assert all(rep[key] == key for key in f["watches"])
+    assert P.upstream_prover_layout(upstream, circ, cap, check_subtrees=2) == tuple(dig)
+    nz = P._common_of("standard_recursion_config")
+    parsed = P._parse_prover_only(upstream, nz, circ, vo)
+    assert parsed[:2] == (None, None) and P._same_preprocessing(vo, parsed[2])
+
+
+def _gen_tag_offsets(data, count=3):
+    """Byte offsets of the first generators' u32 tags (walk of their bodies)."""
+    w = P._Walk(data)
+    w.u64()
+    offs = []
+    for _ in range(count):
+        offs.append(w.p)
+        _, body = P.UPSTREAM_GENERATORS[w.u32()]
+        for k in body:
+            if k in "uf":
+                w.u64()
+            elif k == "t":
+                w.target()
+            else:
+                w.vec("gates")
+    return offs
+
+
+def test_truncated_or_foreign_upstream_blobs_are_rejected(circ, upstream):
+    """The walk refuses truncations in every section, a foreign generator tag,
+    bytes past the end, a flipped coefficient, sigma, Merkle leaf or digest, a
+    different cap, and a blob that only ends like a prover.bin."""
     nz = P._common_of("standard_recursion_config")
     vo, dig = _reference_vd()
     cap = np.frombuffer(vo, np.uint64, 64, 8)
-    for gap in (0, 8):
-        data = upstream_prover_bin(circ, cap, dig, gap=gap)
-        parsed = P._parse_prover_only(data, nz, circ, vo)
-        assert parsed[:2] == (None, None) and P._same_preprocessing(vo, parsed[2])
-    other = [dig[0] ^ 1] + dig[1:]
-    assert not P._same_preprocessing(vo, P._parse_prover_only(upstream_prover_bin(circ, cap, other), nz, circ, vo)[2])
-
-
-def test_truncated_or_foreign_upstream_blobs_are_rejected(circ):
-    """The old tail check accepted anything ending in digest || 0 || 0; the walk
-    refuses truncations (at every section), a flipped coefficient or sigma, a
-    different cap, and a foreign blob with the right tail."""
-    from upstream_prover_bin import upstream_prover_bin
-    nz = P._common_of("standard_recursion_config")
-    vo, dig = _reference_vd()
-    cap = np.frombuffer(vo, np.uint64, 64, 8)
-    good = upstream_prover_bin(circ, cap, dig)
+    good = upstream
     tail = good[-48:]
     foreign = struct.pack("<Q", 1500) + b"\x11" * 40000 + tail
-    assert P.upstream_prover_digest(foreign) is not None  # what the tail check used to accept
-    with pytest.raises(ValueError, match="coefficients of this circuit not found"):
+    with pytest.raises(ValueError, match="foreign generator|truncated"):
         P._parse_prover_only(foreign, nz, circ, vo)
-    n = circ.n
-    for cut in (len(good) // 10, len(good) // 3, len(good) // 2, len(good) - 8 * n - 100, len(good) - 60):
+    for cut in (9, len(good) // 10, len(good) // 3, len(good) // 2, len(good) - 8 * circ.n - 100, len(good) - 60):
         with pytest.raises(ValueError):
             P._parse_prover_only(good[:cut] + tail, nz, circ, vo)
-    # one coefficient of column 40, one sigma value, one cap element
-    k = good.find(circ.constants_sigmas_coeffs()[40].tobytes())
-    for pos, what in ((k + 8 * 5, "coefficient column 40"), (good.find(circ.constants_sigmas()[10].tobytes()) + 16,
-                                                             "sigma")):
+    with pytest.raises(ValueError, match="past"):
+        P.read_upstream_prover_only(good + bytes(8))
+    # a generator kind the leaf circuits do not have (ArithmeticExtensionGenerator, tag 1)
+    t = _gen_tag_offsets(good)[1]
+    bad = bytearray(good)
+    bad[t:t + 4] = struct.pack("<I", 1)
+    with pytest.raises(ValueError, match="foreign generator"):
+        P.read_upstream_prover_only(bytes(bad))
+    # one coefficient of column 40, one sigma value, one leaf of cap subtree 0, one digest
+    co = circ.constants_sigmas_coeffs()
+    sig_row = np.ascontiguousarray(circ.constants_sigmas()[circ.num_constants:, 7])
+    f = P.read_upstream_prover_only(good)
+    leaf = good.find(struct.pack("<Q", 84) + f["leaves"][3].tobytes())
+    digk = good.find(f["digests"][5].tobytes())
+    for pos, what in ((good.find(co[40].tobytes()) + 8 * 5, "coefficient column 40"),
+                      (good.find(struct.pack("<Q", 80) + sig_row.tobytes()) + 8 + 16, "sigma"),
+                      (leaf + 8 + 8 * 2, "merkle"), (digk + 3, "merkle")):
         bad = bytearray(good)
         bad[pos] ^= 1
         with pytest.raises(ValueError, match=what):
@@ -109,6 +162,25 @@ def test_truncated_or_foreign_upstream_blobs_are_rejected(circ):
     # without the circuit an upstream file cannot be checked
     with pytest.raises(ValueError, match="needs the circuit"):
         P._parse_prover_only(good, nz)
+
+
+def test_upstream_prover_bin_of_the_voting_circuit():
+    """The second leaf circuit (configs[4]) through the same writer and walk."""
+    import qp_wormhole
+    v = qp_wormhole.Circuit.voting()
+    data = v.prover_only_bytes()
+    d = P.upstream_prover_layout(data, v, check_subtrees=16)
+    f = P.read_upstream_prover_only(data)
+    assert f["degree_log"] == v.degree_bits and d == f["circuit_digest"]
+    assert len(f["public_inputs"]) == v.num_public_inputs == 13
+
+
+def test_aggregation_circuits_have_no_upstream_writer():
+    """Only the leaf circuits' generator kinds are restated (QP_ERR_ARG)."""
+    import qp_wormhole
+    from test_oracle_golden import current_common_bytes
+    with pytest.raises(qp_wormhole.QpError):
+        qp_wormhole.Circuit.aggregation(current_common_bytes(), 2).prover_only_bytes()
 
 
 def test_header_must_agree_with_common_data():

@@ -114,6 +114,9 @@ for s in "$@"; do
            done ;;
     qpart_prof) step prof_qpart 300 env QP_AGG_PROVERS=1 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/prof_qpart -o run -- python3 tools/agg_subtree.py 256 1 &&
                 step prof_qone 300 env QP_AGG_PROVERS=1 QPGPU_QUOTIENT=onepass rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/prof_qone -o run -- python3 tools/agg_subtree.py 256 1 ;;
+    agglat) step agg_latency 300 python -u tools/agg_latency.py 1,2,4,8,16 5 ;;
+    agglatprof) step prof_agglat 300 rocprofv3 --kernel-trace --output-format csv -d gpurun_out/prof_agglat -o run -- python3 tools/agg_latency.py 1,16 3 ;;
+    test_seamprove) step pytest_seamprove 600 python -u -m pytest tests/test_gpu_seam_prove.py tests/test_gpu_seams.py -x -v --timeout 300 --timeout-method thread ;;
     *) echo "unknown step $s" ;;
   esac
 done
