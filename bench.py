@@ -165,6 +165,9 @@ def parse():
                          "cores (OMP_NUM_THREADS, else min(cores, 16)) between the provers")
     ap.add_argument("--agg-leaves", type=int, default=64,
                     help="leaf proofs aggregated (one level, pairs) after the timed region (0 = skip)")
+    ap.add_argument("--configs3-steps", type=int, default=4,
+                    help="configs[3] also as K batches back to back (leaves of batch k+1 overlapping the "
+                         "aggregation of batch k); 0 or 1: the single-batch record only")
     ap.add_argument("--configs3", type=int, default=1,
                     help="after the headline, time BASELINE configs[3] as one pipeline (every rank: its batch of "
                          "leaves -> its subtree root; roots gathered over RCCL; rank 0: the tree root); 0 = skip")
@@ -350,19 +353,53 @@ def configs3(args, circuit, prover, provers, cin, per, NP, B, dist, world, rank,
         tt = torch.tensor([dt], dtype=torch.float64, device=dev)
         dist.all_reduce(tt, op=dist.ReduceOp.MAX)
         dt = float(tt.item())
+    # the same as a stream of batches: batch k+1's leaves proved while batch k
+    # is aggregated (pipeline_aggregate_steps), K batches timed end to end
+    pipe = None
+    K = args.configs3_steps
+    if K > 1:
+        from qp_wormhole.distributed import pipeline_aggregate_steps
+        if dist is not None:
+            dist.barrier()
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        proots, ptms = pipeline_aggregate_steps(prove_leaves, K, cb, vo, 2, dist, device=dev, gpu=local)
+        torch.cuda.synchronize()
+        if dist is not None:
+            dist.barrier()
+        pdt = time.perf_counter() - t0
+        if dist is not None:
+            tt = torch.tensor([pdt], dtype=torch.float64, device=dev)
+            dist.all_reduce(tt, op=dist.ReduceOp.MAX)
+            pdt = float(tt.item())
+        pipe = (proots, ptms, pdt)
     if rank != 0:
         return None
     from oracle_lib import lib as olib
     from qp_wormhole.prover import _common_degree_bits
+
+    def verified(t):
+        vd_, pb = t.circuit_data.verifier_data(), t.proof.to_bytes()
+        return olib().ora_verify(vd_, len(vd_), pb, len(pb)) == 0
     tops = root if isinstance(root, list) else [root]
-    ok = all(olib().ora_verify(t.circuit_data.verifier_data(), len(t.circuit_data.verifier_data()),
-                               t.proof.to_bytes(), len(t.proof.to_bytes())) == 0 for t in tops)
+    ok = all(verified(t) for t in tops)
     leaves = world * ns
+    pipelined = None
+    if pipe is not None:
+        proots, ptms, pdt = pipe
+        flat = [t for r in proots for t in (r if isinstance(r, list) else [r])]
+        pipelined = {"steps": K, "seconds": pdt, "seconds_per_step": pdt / K, "value": K * leaves / pdt,
+                     "unit": "leaf proofs/s (each batch proved and aggregated into its root)",
+                     "roots_verified": len(proots) == K and all(verified(t) for t in flat),
+                     "stages_rank0_s": {k: [round(t[k], 4) for t in ptms] for k in ptms[0]},
+                     "note": "K batches back to back, batch k+1's leaves proved on the leaf provers' streams "
+                             "while batch k is aggregated on the level provers' (the subtree's narrow top "
+                             "levels are latency-bound); leaves_s overlaps the previous batch's subtree"}
     return {"workload": f"{leaves}_leaves_as_{world}x{ns}_per_gpu_subtrees_branching2",
             "value": leaves / dt, "unit": "leaf proofs/s (proved and aggregated into one root)"
             if len(tops) == 1 else f"leaf proofs/s (proved and aggregated into {len(tops)} top proofs)",
             "seconds": dt, "leaves": leaves, "aggregation_proofs": leaves - len(tops),
-            "stages_rank0_s": tm,
+            "stages_rank0_s": tm, "pipelined": pipelined,
             "root_verified" if len(tops) == 1 else "top_proofs_verified": ok,
             "top_circuit_degree_bits": _common_degree_bits(tops[0].circuit_data.common),
             "root_public_inputs": sum(len(t.proof.public_inputs) for t in tops),
@@ -501,11 +538,18 @@ def main():
         t1 = time.perf_counter()
         root = aggregate_to_tree(proofs[:8], cb, vo)
         tree_ms = (time.perf_counter() - t1) * 1e3
+        # one aggregation proof's latency (aggregate_chunk of 2 leaves, batch of one)
+        ts = []
+        for _ in range(5):
+            t1 = time.perf_counter()
+            aggregate_level(proofs[:2], cb, vo, cfg2)
+            ts.append((time.perf_counter() - t1) * 1e3)
+        one_ms = sorted(ts)[2]
         rvd = root.circuit_data.verifier_data()
         rp = root.proof.to_bytes()
         agg = {"level_leaves": nl, "level_aggregation_proofs": len(level),
                "aggregation_proofs_per_s": len(level) / lvl_s, "leaves_per_s_through_one_level": nl / lvl_s,
-               "tree8_root_ms": tree_ms, "root_verified": olib().ora_verify(rvd, len(rvd), rp, len(rp)) == 0,
+               "tree8_root_ms": tree_ms, "one_proof_ms": one_ms, "root_verified": olib().ora_verify(rvd, len(rvd), rp, len(rp)) == 0,
                "aggregation_circuit_degree_bits": _common_degree_bits(root.circuit_data.common),
                "proof_bytes": len(rp),
                "note": "aggregate_chunk circuits (recursive verifier of 2 proofs on upstream's gate set, degree "

@@ -50,6 +50,9 @@ const char *qp_ctx_last_error(const qp_ctx *ctx);
 /* run subsequent work on an external HIP stream (e.g. torch's); NULL = own stream */
 int qp_ctx_set_stream(qp_ctx *ctx, void *hip_stream);
 int qp_ctx_synchronize(qp_ctx *ctx);
+/* re-create the context's own stream at the device's greatest stream priority
+ * (high != 0) or the default one; call before any work is queued on it */
+int qp_ctx_set_priority(qp_ctx *ctx, int high);
 /* library build/version string */
 const char *qp_version(void);
 

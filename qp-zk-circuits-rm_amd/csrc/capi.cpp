@@ -51,6 +51,24 @@ int qp_ctx_set_stream(qp_ctx *c, void *s) {
   return QP_OK;
 }
 
+// the context's own stream re-created at the device's greatest (high != 0) or
+// default priority: the aggregation levels' latency-bound launches then
+// dispatch ahead of leaf-proof kernels queued on normal-priority streams
+int qp_ctx_set_priority(qp_ctx *c, int high) {
+  if (!c) return QP_ERR_ARG;
+  QP_HIP_TRY(c, hipSetDevice(c->device));
+  int least = 0, greatest = 0;
+  QP_HIP_TRY(c, hipDeviceGetStreamPriorityRange(&least, &greatest));
+  hipStream_t s = nullptr;
+  QP_HIP_TRY(c, hipStreamCreateWithPriority(&s, hipStreamNonBlocking, high ? greatest : least));
+  QP_HIP_TRY(c, hipStreamSynchronize(c->own_stream));
+  const bool own = c->stream == c->own_stream;
+  (void)hipStreamDestroy(c->own_stream);
+  c->own_stream = s;
+  if (own) c->stream = s;
+  return QP_OK;
+}
+
 int qp_ctx_synchronize(qp_ctx *c) {
   if (!c) return QP_ERR_ARG;
   QP_HIP_TRY(c, hipStreamSynchronize(c->stream));

@@ -88,6 +88,7 @@ def lib():
         "qp_ctx_destroy": (None, [VP]),
         "qp_ctx_last_error": (ctypes.c_char_p, [VP]),
         "qp_ctx_set_stream": (ctypes.c_int, [VP, VP]),
+        "qp_ctx_set_priority": (ctypes.c_int, [VP, ctypes.c_int]),
         "qp_ctx_synchronize": (ctypes.c_int, [VP]),
         "qp_commit_values": (ctypes.c_int, [VP, U64P, ctypes.c_uint32, ctypes.c_uint32, ctypes.c_uint32,
                                             ctypes.c_uint32, VP, ctypes.c_uint32, VP, U64P, PP]),
@@ -181,6 +182,10 @@ class Context:
     def check(self, rc, what=""):
         if rc:
             raise QpError(rc, f"{what}: {lib().qp_ctx_last_error(self.h).decode()}")
+
+    def set_priority(self, high=True):
+        """Own stream at the device's greatest (or the default) priority."""
+        self.check(lib().qp_ctx_set_priority(self.h, int(bool(high))), "set_priority")
 
     def close(self):
         if self.h:

@@ -83,7 +83,14 @@ class _LevelProver:
         nprov = max(1, int(os.environ.get("QP_AGG_PROVERS", "2")))
         if max_batch == 1:
             nprov = 1
-        self.provers = [Prover(Context(device), self.circuit, max_batch=max_batch) for _ in range(nprov)]
+        # QP_AGG_PRIORITY=1: the level provers' streams at the greatest priority,
+        # so their latency-bound launches dispatch ahead of concurrent leaf kernels
+        high = os.environ.get("QP_AGG_PRIORITY", "0") not in ("", "0")
+        ctxs = [Context(device) for _ in range(nprov)]
+        if high:
+            for c in ctxs:
+                c.set_priority(True)
+        self.provers = [Prover(c, self.circuit, max_batch=max_batch) for c in ctxs]
         # the provers split the process's host budget (qp_prover_set_host_threads:
         # each would otherwise take min(hardware threads, 16))
         for p in self.provers:

@@ -238,3 +238,59 @@ def pipeline_aggregate_step(prove_leaves, common: bytes, verifier_only: bytes, b
     root = aggregate_subtrees(leaves, common, verifier_only, branching, dist, device=device, gpu=gpu, dst=dst,
                               backend=backend, timings=tm)
     return root, tm
+
+
+def pipeline_aggregate_steps(prove_leaves, steps: int, common: bytes, verifier_only: bytes, branching: int,
+                             dist=None, device="cpu", gpu: int = 0, dst: int = 0, backend=None):
+    """configs[3] as a stream of batches: `steps` pipeline_aggregate_step's with
+    batch k+1's leaves proved (a leaf thread: prove_leaves() on the leaf
+    provers' own streams) while batch k is aggregated into its root (this
+    thread: the level provers' streams, the roots gather, rank dst's top
+    levels).  The subtree's narrow top levels are latency-bound (one proof's
+    sequential Poseidon chains), so the leaf proofs of the next batch fill the
+    GPU they leave idle.  At most one finished batch waits in between.  Only
+    this thread issues collectives, in the same order on every rank.  Returns
+    ([root per step on dst / None], [stage seconds per step])."""
+    import queue
+    import threading
+    import time
+    q = queue.Queue(maxsize=1)
+    errors = []
+    stop = threading.Event()
+
+    def leaf_worker():
+        try:
+            for _ in range(steps):
+                if stop.is_set():
+                    return
+                t = time.perf_counter()
+                leaves = prove_leaves()
+                q.put((leaves, time.perf_counter() - t))
+        except BaseException as e:  # re-raised on the calling thread
+            errors.append(e)
+            q.put(None)
+
+    th = threading.Thread(target=leaf_worker, daemon=True)
+    th.start()
+    roots, tms = [], []
+    try:
+        for _ in range(steps):
+            item = q.get()
+            if item is None:
+                break
+            leaves, lt = item
+            tm = {"leaves_s": lt}
+            roots.append(aggregate_subtrees(leaves, common, verifier_only, branching, dist, device=device, gpu=gpu,
+                                            dst=dst, backend=backend, timings=tm))
+            tms.append(tm)
+    finally:
+        stop.set()
+        while th.is_alive():
+            try:
+                q.get(timeout=0.1)
+            except queue.Empty:
+                pass
+        th.join()
+    if errors:
+        raise errors[0]
+    return roots, tms

@@ -307,3 +307,57 @@ def test_configs3_pipeline_step_world2_gloo():
     ok, pis_ok, stages = _run(_worker_pipeline, 2)
     assert ok and pis_ok
     assert stages == ["gather_s", "leaves_s", "subtree_s", "top_s"]
+
+
+def _worker_pipeline_steps(rank, world, port, q):
+    """configs[3] as a stream of batches (distributed.pipeline_aggregate_steps):
+    three batches, each rank's next leaves proved on a leaf thread while the
+    previous batch is aggregated; every batch's root verifies and carries its
+    own leaves' public inputs (the batches differ), in order."""
+    import struct
+
+    import torch.distributed as dist
+
+    from agg_oracle_backend import oracle_backend
+    from qp_wormhole.distributed import pipeline_aggregate_steps
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    from current_circuit_vd import current_circuit_verifier_data
+    from oracle_lib import golden, lib as olib
+    from test_oracle_golden import current_common_bytes
+    cb = current_common_bytes()
+    vd = current_circuit_verifier_data(cb)[0]
+    fx = [golden("dummy_proof.bin"), golden("dummy_proof_zk.bin")]
+    order = [[0, 1], [1, 0], [1, 1]]
+    calls = []
+
+    def prove_leaves():
+        k = len(calls)
+        calls.append(k)
+        o = order[(k + rank) % 3]
+        return [fx[i] for i in o]
+    roots, tms = pipeline_aggregate_steps(prove_leaves, 3, cb, vd[:len(vd) - len(cb)], 2, dist,
+                                          backend=oracle_backend)
+    if rank == 0:
+        res = []
+        for k, root in enumerate(roots):
+            rvd = root.circuit_data.verifier_data()
+            ok = olib().ora_verify(rvd, len(rvd), root.proof.to_bytes(), len(root.proof.to_bytes())) == 0
+            want = []
+            for r in range(world):
+                for i in order[(k + r) % 3]:
+                    pf = fx[i]
+                    want += list(struct.unpack_from("<16Q", pf, len(pf) - 128))
+            res.append(ok and [int(x) for x in root.proof.public_inputs] == want)
+        q.put((res, len(calls), [sorted(t) for t in tms]))
+    else:
+        assert roots == [None] * 3 and len(calls) == 3
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+def test_configs3_pipelined_steps_world2_gloo():
+    res, ncalls, stages = _run(_worker_pipeline_steps, 2)
+    assert res == [True] * 3 and ncalls == 3
+    assert stages == [["gather_s", "leaves_s", "subtree_s", "top_s"]] * 3

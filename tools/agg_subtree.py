@@ -33,10 +33,16 @@ def main():
     levels = []
     orig = A.aggregate_level
 
+    import resource
+
+    def cpu():
+        r = resource.getrusage(resource.RUSAGE_SELF)
+        return r.ru_utime + r.ru_stime
+
     def timed_level(proofs, *a, **k):
-        t = time.perf_counter()
+        t, c = time.perf_counter(), cpu()
         r = orig(proofs, *a, **k)
-        levels.append((len(proofs) // 2, time.perf_counter() - t))
+        levels.append((len(proofs) // 2, time.perf_counter() - t, cpu() - c))
         return r
     A.aggregate_level = timed_level
     t = time.perf_counter()
@@ -45,12 +51,22 @@ def main():
     for lp in A._levels.values():
         for p in lp.provers:
             p.stage_times(reset=True)
+    def throttle():
+        try:
+            d = dict(l.split() for l in open("/sys/fs/cgroup/cpu.stat"))
+            return int(d.get("nr_throttled", 0)), int(d.get("throttled_usec", 0))
+        except (OSError, ValueError):
+            return None
+    th0 = throttle()
     res = []
     for _ in range(reps):
         levels.clear()
         t = time.perf_counter()
         root = A.aggregate_to_tree(leaves, cb, vo, cfg)
-        res.append({"seconds": time.perf_counter() - t, "levels": [(n, round(s * 1e3, 1)) for n, s in levels]})
+        # per level: proofs, wall ms, process CPU ms (all threads; the box gives
+        # this job OMP_NUM_THREADS cores)
+        res.append({"seconds": time.perf_counter() - t,
+                    "levels": [(n, round(s * 1e3, 1), round(c * 1e3, 1)) for n, s, c in levels]})
     stages = {}
     for lp in A._levels.values():
         for p in lp.provers:
@@ -58,8 +74,12 @@ def main():
                 stages[k] = stages.get(k, 0.0) + v / reps
     rvd, rp = root.circuit_data.verifier_data(), root.proof.to_bytes()
     env = {k: os.environ.get(k) for k in ("QP_AGG_PROVERS", "QP_AGG_WITNESS", "QPGPU_QUOTIENT", "QPGPU_LDE_MODE",
-                                        "QPGPU_HOST_CHAIN")}
-    print(json.dumps({"leaves": nl, "env": env, "warm_s": round(warm, 2), "runs": res,
+                                        "QPGPU_HOST_CHAIN", "QP_AGG_THREADS", "OMP_NUM_THREADS")}
+    th1 = throttle()
+    cg = None
+    if th0 and th1:
+        cg = {"nr_throttled": th1[0] - th0[0], "throttled_ms": (th1[1] - th0[1]) / 1e3}
+    print(json.dumps({"leaves": nl, "env": env, "warm_s": round(warm, 2), "runs": res, "cgroup_throttling": cg,
                       "stage_ms_per_run_all_provers": {k: round(v, 1) for k, v in stages.items()},
                       "root_verified": olib().ora_verify(rvd, len(rvd), rp, len(rp)) == 0}), flush=True)
 

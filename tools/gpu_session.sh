@@ -117,6 +117,16 @@ for s in "$@"; do
     agglat) step agg_latency 300 python -u tools/agg_latency.py 1,2,4,8,16 5 ;;
     agglatprof) step prof_agglat 300 rocprofv3 --kernel-trace --output-format csv -d gpurun_out/prof_agglat -o run -- python3 tools/agg_latency.py 1,16 3 ;;
     test_seamprove) step pytest_seamprove 600 python -u -m pytest tests/test_gpu_seam_prove.py tests/test_gpu_seams.py -x -v --timeout 300 --timeout-method thread ;;
+    aggthr) step agg_thr_def 300 python -u tools/agg_subtree.py 256 2 &&
+            step agg_thr4 300 env QP_AGG_THREADS=4 python -u tools/agg_subtree.py 256 2 &&
+            step agg_thr8 300 env QP_AGG_THREADS=8 python -u tools/agg_subtree.py 256 2 &&
+            step agg_thr16_p1 300 env QP_AGG_PROVERS=1 python -u tools/agg_subtree.py 256 2 &&
+            cat /sys/fs/cgroup/cpu.max /sys/fs/cgroup/cpu.stat > gpurun_out/cgroup.txt ;;
+    c3q) step c3_q4 300 python -u bench.py --steps 2 --warmup 1 --cpu-sample 0 --agg-leaves 0 &&
+         step c3_q16 300 env GPU_MAX_HW_QUEUES=16 python -u bench.py --steps 2 --warmup 1 --cpu-sample 0 --agg-leaves 0 ;;
+    c3prio) step c3_prio0 300 python -u bench.py --steps 2 --warmup 1 --cpu-sample 0 --agg-leaves 0 &&
+            step c3_prio1 300 env QP_AGG_PRIORITY=1 python -u bench.py --steps 2 --warmup 1 --cpu-sample 0 --agg-leaves 0 ;;
+    aggtrace) step prof_aggsub 300 rocprofv3 --kernel-trace --output-format csv -d gpurun_out/prof_aggsub -o run -- python3 tools/agg_subtree.py 256 2 ;;
     *) echo "unknown step $s" ;;
   esac
 done
