@@ -201,9 +201,133 @@ __device__ __forceinline__ uint64_t mul_w16(uint64_t x) {
   else return mul_pow2<(192 - 12 * J) % 192>(x);
 }
 
+// QP_NTT_ILV=1 (default): a stage's butterflies four at a time, their adds and
+// subs interleaved in one asm block each (add4 / sub4): every carry is read
+// four instructions after it is written, so the gfx950 carry hazard needs no
+// s_nop (a 16-point DFT: 694 VALU + 387 s_nop -> 660 VALU + 113 s_nop, static)
+#ifndef QP_NTT_ILV
+#define QP_NTT_ILV 1
+#endif
+// 4 independent Goldilocks adds (non-canonical in and out, as nt::add),
+// interleaved in one asm block: every carry is read 4 instructions after it
+// is written, so no hazard pads
+__device__ __forceinline__ void add4(const uint64_t a[4], const uint64_t b[4], uint64_t s[4]) {
+  uint64_t c0, c1, c2, c3;
+  uint32_t e0, e1, e2, e3;
+  asm("v_lshl_add_u64 %0, %12, 0, %16\n\t"
+      "v_lshl_add_u64 %1, %13, 0, %17\n\t"
+      "v_lshl_add_u64 %2, %14, 0, %18\n\t"
+      "v_lshl_add_u64 %3, %15, 0, %19\n\t"
+      "v_cmp_lt_u64_e64 %8, %0, %16\n\t"
+      "v_cmp_lt_u64_e64 %9, %1, %17\n\t"
+      "v_cmp_lt_u64_e64 %10, %2, %18\n\t"
+      "v_cmp_lt_u64_e64 %11, %3, %19\n\t"
+      "v_cndmask_b32_e64 %4, 0, -1, %8\n\t"
+      "v_cndmask_b32_e64 %5, 0, -1, %9\n\t"
+      "v_cndmask_b32_e64 %6, 0, -1, %10\n\t"
+      "v_cndmask_b32_e64 %7, 0, -1, %11\n\t"
+      "v_mad_u64_u32 %0, %8, %4, 1, %0\n\t"
+      "v_mad_u64_u32 %1, %9, %5, 1, %1\n\t"
+      "v_mad_u64_u32 %2, %10, %6, 1, %2\n\t"
+      "v_mad_u64_u32 %3, %11, %7, 1, %3\n\t"
+      "v_cndmask_b32_e64 %4, 0, -1, %8\n\t"
+      "v_cndmask_b32_e64 %5, 0, -1, %9\n\t"
+      "v_cndmask_b32_e64 %6, 0, -1, %10\n\t"
+      "v_cndmask_b32_e64 %7, 0, -1, %11\n\t"
+      "v_mad_u64_u32 %0, %8, %4, 1, %0\n\t"
+      "v_mad_u64_u32 %1, %9, %5, 1, %1\n\t"
+      "v_mad_u64_u32 %2, %10, %6, 1, %2\n\t"
+      "v_mad_u64_u32 %3, %11, %7, 1, %3"
+      : "=&v"(s[0]), "=&v"(s[1]), "=&v"(s[2]), "=&v"(s[3]), "=&v"(e0), "=&v"(e1), "=&v"(e2), "=&v"(e3),
+        "=&s"(c0), "=&s"(c1), "=&s"(c2), "=&s"(c3)
+      : "v"(a[0]), "v"(a[1]), "v"(a[2]), "v"(a[3]), "v"(b[0]), "v"(b[1]), "v"(b[2]), "v"(b[3]));
+}
+
+// 4 independent Goldilocks subs (as nt::sub): d = a - b; on a borrow d - eps,
+// and on a second borrow (b > a + p) d - eps again
+__device__ __forceinline__ void sub4(const uint64_t a[4], const uint64_t b[4], uint64_t d[4]) {
+  uint32_t l0, l1, l2, l3, h0, h1, h2, h3, e0, e1, e2, e3;
+  uint64_t c0, c1, c2, c3;
+  asm("v_sub_co_u32_e64 %0, %12, %16, %24\n\t"
+      "v_sub_co_u32_e64 %1, %13, %17, %25\n\t"
+      "v_sub_co_u32_e64 %2, %14, %18, %26\n\t"
+      "v_sub_co_u32_e64 %3, %15, %19, %27\n\t"
+      "v_subb_co_u32_e64 %4, %12, %20, %28, %12\n\t"
+      "v_subb_co_u32_e64 %5, %13, %21, %29, %13\n\t"
+      "v_subb_co_u32_e64 %6, %14, %22, %30, %14\n\t"
+      "v_subb_co_u32_e64 %7, %15, %23, %31, %15\n\t"
+      "v_cndmask_b32_e64 %8, 0, -1, %12\n\t"
+      "v_cndmask_b32_e64 %9, 0, -1, %13\n\t"
+      "v_cndmask_b32_e64 %10, 0, -1, %14\n\t"
+      "v_cndmask_b32_e64 %11, 0, -1, %15\n\t"
+      "v_sub_co_u32_e64 %0, %12, %0, %8\n\t"
+      "v_sub_co_u32_e64 %1, %13, %1, %9\n\t"
+      "v_sub_co_u32_e64 %2, %14, %2, %10\n\t"
+      "v_sub_co_u32_e64 %3, %15, %3, %11\n\t"
+      "v_subb_co_u32_e64 %4, %12, %4, 0, %12\n\t"
+      "v_subb_co_u32_e64 %5, %13, %5, 0, %13\n\t"
+      "v_subb_co_u32_e64 %6, %14, %6, 0, %14\n\t"
+      "v_subb_co_u32_e64 %7, %15, %7, 0, %15\n\t"
+      "v_cndmask_b32_e64 %8, 0, -1, %12\n\t"
+      "v_cndmask_b32_e64 %9, 0, -1, %13\n\t"
+      "v_cndmask_b32_e64 %10, 0, -1, %14\n\t"
+      "v_cndmask_b32_e64 %11, 0, -1, %15\n\t"
+      "v_sub_co_u32_e64 %0, %12, %0, %8\n\t"
+      "v_sub_co_u32_e64 %1, %13, %1, %9\n\t"
+      "v_sub_co_u32_e64 %2, %14, %2, %10\n\t"
+      "v_sub_co_u32_e64 %3, %15, %3, %11\n\t"
+      "v_subb_co_u32_e64 %4, %12, %4, 0, %12\n\t"
+      "v_subb_co_u32_e64 %5, %13, %5, 0, %13\n\t"
+      "v_subb_co_u32_e64 %6, %14, %6, 0, %14\n\t"
+      "v_subb_co_u32_e64 %7, %15, %7, 0, %15"
+      : "=&v"(l0), "=&v"(l1), "=&v"(l2), "=&v"(l3), "=&v"(h0), "=&v"(h1), "=&v"(h2), "=&v"(h3), "=&v"(e0),
+        "=&v"(e1), "=&v"(e2), "=&v"(e3), "=&s"(c0), "=&s"(c1), "=&s"(c2), "=&s"(c3)
+      : "v"((uint32_t)a[0]), "v"((uint32_t)a[1]), "v"((uint32_t)a[2]), "v"((uint32_t)a[3]),
+        "v"((uint32_t)(a[0] >> 32)), "v"((uint32_t)(a[1] >> 32)), "v"((uint32_t)(a[2] >> 32)),
+        "v"((uint32_t)(a[3] >> 32)), "v"((uint32_t)b[0]), "v"((uint32_t)b[1]), "v"((uint32_t)b[2]),
+        "v"((uint32_t)b[3]), "v"((uint32_t)(b[0] >> 32)), "v"((uint32_t)(b[1] >> 32)), "v"((uint32_t)(b[2] >> 32)),
+        "v"((uint32_t)(b[3] >> 32)));
+  d[0] = ((uint64_t)h0 << 32) | l0;
+  d[1] = ((uint64_t)h1 << 32) | l1;
+  d[2] = ((uint64_t)h2 << 32) | l2;
+  d[3] = ((uint64_t)h3 << 32) | l3;
+}
+
 // radix-2 DIF stage of half-width H on a register array of size 16
 template <bool INV, int H>
 __device__ __forceinline__ void stage16(uint64_t a[16]) {
+  if constexpr (QP_NTT_ILV) {
+#pragma unroll
+    for (int g = 0; g < 8; g += 4) {
+      // butterflies g..g+3: index pairs (lo_i, lo_i + H)
+      int lo[4];
+#pragma unroll
+      for (int i = 0; i < 4; i++) lo[i] = ((g + i) / H) * 2 * H + (g + i) % H;
+      uint64_t u[4], v[4], s[4], d[4];
+#pragma unroll
+      for (int i = 0; i < 4; i++) {
+        u[i] = a[lo[i]];
+        v[i] = a[lo[i] + H];
+      }
+      add4(u, v, s);
+      sub4(u, v, d);
+#pragma unroll
+      for (int i = 0; i < 4; i++) {
+        a[lo[i]] = s[i];
+        switch ((lo[i] % H) * (8 / H)) {
+          case 0: a[lo[i] + H] = d[i]; break;
+          case 1: a[lo[i] + H] = mul_w16<INV, 1>(d[i]); break;
+          case 2: a[lo[i] + H] = mul_w16<INV, 2>(d[i]); break;
+          case 3: a[lo[i] + H] = mul_w16<INV, 3>(d[i]); break;
+          case 4: a[lo[i] + H] = mul_w16<INV, 4>(d[i]); break;
+          case 5: a[lo[i] + H] = mul_w16<INV, 5>(d[i]); break;
+          case 6: a[lo[i] + H] = mul_w16<INV, 6>(d[i]); break;
+          default: a[lo[i] + H] = mul_w16<INV, 7>(d[i]); break;
+        }
+      }
+    }
+    return;
+  }
 #pragma unroll
   for (int k = 0; k < 16; k += 2 * H) {
 #pragma unroll

@@ -78,6 +78,9 @@ __global__ void k_quotient_1r(QuotientArgs a);
 __global__ void k_quotient_fused(QuotientArgs a);
 template <int PART>
 __global__ void k_quotient_part(QuotientArgs a, uint32_t gi, uint32_t last);
+// the permutation terms + the gates of gmask that read routed wires only, one pass
+template <int QDF>
+__global__ void k_quotient_prefix(QuotientArgs a, uint32_t gmask, uint32_t last);
 __global__ void k_qintt_gather_big(const uint64_t *vals, uint64_t *out, uint32_t log_n, uint32_t rate_bits,
                                    uint64_t v_bstride, uint64_t o_bstride);
 __global__ void k_qintt_blocks(const uint64_t *vals, uint64_t *out, uint32_t log_n, uint32_t rate_bits,

@@ -16,6 +16,7 @@
 #include "poseidon.h"
 #include "poseidon_dev.h"
 #include "prover_kernels.h"
+#include <stdlib.h>
 #include "ntt16.h"
 
 namespace qpk {
@@ -1353,6 +1354,193 @@ __global__ void __launch_bounds__(256) k_quotient_part(QuotientArgs a, uint32_t 
     q[N + t] = acc1;
   }
 }
+// ---- k_quotient_prefix: the permutation terms and every gate of gmask that
+// reads routed wires only (Constant, PublicInput, BaseSum, Arithmetic,
+// ArithmeticExtension, MulExtension) in ONE pass over windows of QP_WIN routed
+// wires held in registers, where k_quotient_part<0> and one launch per gate read
+// the routed wires up to seven times and round-trip both accumulators through
+// HBM per gate.  Each term keeps its own alpha index and each gate's sum is
+// multiplied by its filter, so the result is the same field element (the sums
+// do not depend on evaluation order): bit-identical.  The other gates follow
+// as k_quotient_part launches.  QDF: the permutation chunk (quotient degree
+// factor), a divisor of QP_WIN, so windows hold whole chunks and whole ops.
+constexpr uint32_t QP_WIN = 24;  // multiple of 4 (Arithmetic), 6 (MulExtension), 8 (ArithmeticExtension, chunks)
+template <int QDF>
+#ifndef QP_QPREFIX_WAVES
+#define QP_QPREFIX_WAVES 4
+#endif
+__global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(QP_QPREFIX_WAVES)))
+k_quotient_prefix(QuotientArgs a, uint32_t gmask, uint32_t last) {
+  static_assert(QP_WIN % QDF == 0, "windows hold whole permutation chunks");
+  const uint32_t logN = a.log_n + a.rate_bits;
+  const uint64_t N = 1ull << logN;
+  const uint32_t t = blockIdx.x * blockDim.x + threadIdx.x;
+  if (t >= N) return;
+  const uint32_t b = blockIdx.y;
+  const uint64_t *ch = a.chal + b * CHAL_STRIDE;
+  const uint64_t *cs = a.cs_lde + t;
+  const uint64_t *wl = a.w_lde + b * a.w_bstride + t;
+  const uint64_t *zl = a.z_lde + b * a.z_bstride;
+  uint64_t *q = a.q_out + b * a.q_bstride;
+  const uint64_t *__restrict__ p0 = a.apow + (uint64_t)b * 2 * APOW_STRIDE;
+  const uint64_t *__restrict__ p1 = p0 + APOW_STRIDE;
+  const uint32_t R = a.R, nchunks = (R + QDF - 1) / QDF, npp = nchunks - 1;
+  const uint32_t gb = 2 * (1 + nchunks);  // alpha index of every gate's constraint 0
+  int gi_c = -1, gi_pi = -1, gi_bs = -1, gi_ar = -1, gi_ae = -1, gi_me = -1;
+  for (uint32_t gi = 0; gi < a.g.ngates; gi++)
+    if ((gmask >> gi) & 1) switch (a.g.kind[gi]) {
+        case GK_CONSTANT: gi_c = (int)gi; break;
+        case GK_PUBLIC_INPUT: gi_pi = (int)gi; break;
+        case GK_BASE_SUM: gi_bs = (int)gi; break;
+        case GK_ARITHMETIC: gi_ar = (int)gi; break;
+        case GK_ARITH_EXT: gi_ae = (int)gi; break;
+        case GK_MUL_EXT: gi_me = (int)gi; break;
+        default: break;
+      }
+  const uint32_t n_c = gi_c >= 0 ? a.g.param[gi_c] : 0, n_bs = gi_bs >= 0 ? a.g.param[gi_bs] : 0;
+  const uint32_t n_ar = gi_ar >= 0 ? a.g.param[gi_ar] : 0, n_ae = gi_ae >= 0 ? a.g.param[gi_ae] : 0;
+  const uint32_t n_me = gi_me >= 0 ? a.g.param[gi_me] : 0;
+  // one accumulator pair: a gate's terms enter multiplied by its selector
+  // filter, prod over the gate's group of (j - s), j != gate, times (UNUSED -
+  // s) with several groups (per-gate sums would hold 12 more registers)
+  uint64_t acc0 = 0, acc1 = 0;
+  auto emit = [&](uint32_t i, uint64_t term) {
+    uint64_t m0, m1;
+    mul2(term, p0[i], term, p1[i], m0, m1);
+    acc0 = gfn::add(acc0, m0);
+    acc1 = gfn::add(acc1, m1);
+  };
+  auto filter = [&](int gi) -> uint64_t {
+    if (gi < 0) return 0;
+    const uint32_t si = a.g.sel_index[gi];
+    const uint64_t sv = cs[(uint64_t)si * N];
+    uint64_t f = 1;
+    for (uint32_t jj = a.g.grp_lo[si]; jj < a.g.grp_hi[si]; jj++)
+      if (jj != (uint32_t)gi) f = gfn::mul(f, gfn::sub(jj, sv));
+    if (a.g.nsel > 1) f = gfn::mul(f, gfn::sub(0xFFFFFFFFull, sv));
+    return f;
+  };
+  const uint64_t f_c = filter(gi_c), f_pi = filter(gi_pi), f_bs = filter(gi_bs), f_ar = filter(gi_ar),
+                 f_ae = filter(gi_ae), f_me = filter(gi_me);
+  const uint32_t jn = gl::rev_bits(t, logN);
+  const uint32_t tn = gl::rev_bits((jn + (1u << a.rate_bits)) & (uint32_t)(N - 1), logN);
+  const uint64_t x = a.xtab[t], l0 = a.l0tab[t];
+  emit(0, gfn::mul(l0, gfn::sub(zl[t], 1)));
+  emit(1, gfn::mul(l0, gfn::sub(zl[N + t], 1)));
+  const uint64_t *gc = cs + (uint64_t)a.g.nsel * N;
+  const bool need_k0 = gi_c >= 0 || gi_ar >= 0 || gi_ae >= 0 || gi_me >= 0;
+  const bool need_k1 = (gi_c >= 0 && n_c > 1) || gi_ar >= 0 || gi_ae >= 0;
+  const uint64_t k0 = need_k0 ? gc[0] : 0, k1 = need_k1 ? gc[N] : 0;
+  const uint64_t beta0 = ch[CH_BETA], beta1 = ch[CH_BETA + 1], gam0 = ch[CH_GAMMA], gam1 = ch[CH_GAMMA + 1];
+  uint64_t bkx0 = gfn::mul(beta0, x), bkx1 = gfn::mul(beta1, x);
+  uint64_t bs_acc = 0, bs_pw = 1, wire0 = 0, bss0 = 0, bss1 = 0;
+  for (uint32_t base = 0; base < R; base += QP_WIN) {
+    const uint32_t nw = R - base < QP_WIN ? R - base : QP_WIN;
+    uint64_t w[QP_WIN];
+#pragma unroll
+    for (uint32_t k = 0; k < QP_WIN; k++) w[k] = k < nw ? WV(base + k) : 0;
+    if (base == 0) {
+      wire0 = w[0];
+      if (gi_c >= 0 && n_c > 0) emit(gb, gfn::mul(f_c, gfn::sub(k0, w[0])));
+      if (gi_c >= 0 && n_c > 1) emit(gb + 1, gfn::mul(f_c, gfn::sub(k1, w[1])));
+      if (gi_pi >= 0) {
+#pragma unroll
+        for (uint32_t i = 0; i < 4; i++) emit(gb + i, gfn::mul(f_pi, gfn::sub(w[i], ch[CH_PIH + i])));
+      }
+    }
+    // permutation: the window's chunks of QDF wires
+#pragma unroll
+    for (uint32_t c = 0; c < QP_WIN; c += QDF) {
+      if (c >= nw) break;
+      const uint32_t k = (base + c) / QDF;
+      uint64_t num0 = 1, den0 = 1, num1 = 1, den1 = 1;
+#pragma unroll
+      for (uint32_t i = 0; i < QDF; i++) {
+        if (c + i >= nw) break;
+        const uint64_t s = cs[(uint64_t)(a.num_constants + base + c + i) * N];
+        const uint64_t wg0 = gfn::add_c(w[c + i], gam0), wg1 = gfn::add_c(w[c + i], gam1);
+        num0 = gfn::mul(num0, gfn::add(wg0, bkx0));
+        num1 = gfn::mul(num1, gfn::add(wg1, bkx1));
+        den0 = gfn::mul(den0, gfn::add(wg0, gfn::mul(beta0, s)));
+        den1 = gfn::mul(den1, gfn::add(wg1, gfn::mul(beta1, s)));
+        bkx0 = gfn::mul(bkx0, gl::GEN);
+        bkx1 = gfn::mul(bkx1, gl::GEN);
+      }
+#pragma unroll
+      for (uint32_t cc = 0; cc < 2; cc++) {
+        const uint64_t prev = k == 0 ? zl[(uint64_t)cc * N + t] : zl[((uint64_t)2 + cc * npp + k - 1) * N + t];
+        const uint64_t next = k == nchunks - 1 ? zl[(uint64_t)cc * N + tn] : zl[((uint64_t)2 + cc * npp + k) * N + t];
+        emit(2 + cc * nchunks + k,
+             gfn::sub(gfn::mul(prev, cc ? num1 : num0), gfn::mul(next, cc ? den1 : den0)));
+      }
+    }
+    // Arithmetic ops (4 wires), ArithmeticExtension ops (8), MulExtension ops (6)
+#pragma unroll
+    for (uint32_t o = 0; o < QP_WIN; o += 4) {
+      const uint32_t op = (base + o) / 4;
+      if (o < nw && op < n_ar)
+        emit(gb + op, gfn::mul(f_ar, gfn::sub(w[o + 3], gfn::add(gfn::mul(gfn::mul(w[o], w[o + 1]), k0),
+                                                                  gfn::mul(w[o + 2], k1)))));
+    }
+#pragma unroll
+    for (uint32_t o = 0; o < QP_WIN; o += 8) {
+      const uint32_t op = (base + o) / 8;
+      if (o < nw && op < n_ae) {
+        uint64_t m0, m1;
+        alg_mul(w[o], w[o + 1], w[o + 2], w[o + 3], m0, m1);
+        emit(gb + 2 * op, gfn::mul(f_ae, gfn::sub(w[o + 6], gfn::add(gfn::mul(m0, k0), gfn::mul(w[o + 4], k1)))));
+        emit(gb + 2 * op + 1,
+             gfn::mul(f_ae, gfn::sub(w[o + 7], gfn::add(gfn::mul(m1, k0), gfn::mul(w[o + 5], k1)))));
+      }
+    }
+#pragma unroll
+    for (uint32_t o = 0; o < QP_WIN; o += 6) {
+      const uint32_t op = (base + o) / 6;
+      if (o < nw && op < n_me) {
+        uint64_t m0, m1;
+        alg_mul(w[o], w[o + 1], w[o + 2], w[o + 3], m0, m1);
+        emit(gb + 2 * op, gfn::mul(f_me, gfn::sub(w[o + 4], gfn::mul(m0, k0))));
+        emit(gb + 2 * op + 1, gfn::mul(f_me, gfn::sub(w[o + 5], gfn::mul(m1, k0))));
+      }
+    }
+    // BaseSum limbs (wires 1..n_bs): range checks at 1 + limb into their own
+    // sum (one filter product at the end), the limb sum by Horner over the
+    // window's limbs from the top, then scaled by 2^(the window's lowest limb)
+    if (gi_bs >= 0 && base < n_bs + 1) {
+      uint64_t h = 0;
+#pragma unroll
+      for (int k = QP_WIN - 1; k >= 0; k--) {
+        const uint32_t wi = base + k;
+        if ((uint32_t)k < nw && wi >= 1 && wi <= n_bs) {
+          uint64_t m0, m1;
+          const uint64_t tm = gfn::mul(w[k], gfn::sub(w[k], 1));
+          mul2(tm, p0[gb + wi], tm, p1[gb + wi], m0, m1);
+          bss0 = gfn::add(bss0, m0);
+          bss1 = gfn::add(bss1, m1);
+          h = gfn::add(gfn::add(h, h), w[k]);
+        }
+      }
+      bs_acc = gfn::add(bs_acc, gfn::mul(h, bs_pw));
+      bs_pw = gfn::mul(bs_pw, 1ull << (base == 0 ? QP_WIN - 1 : QP_WIN));  // 2^(first limb of the next window)
+    }
+  }
+  if (gi_bs >= 0) {
+    uint64_t m0, m1, d = gfn::sub(bs_acc, wire0);
+    mul2(d, p0[gb], d, p1[gb], m0, m1);
+    acc0 = gfn::add(acc0, gfn::mul(f_bs, gfn::add(bss0, m0)));
+    acc1 = gfn::add(acc1, gfn::mul(f_bs, gfn::add(bss1, m1)));
+  }
+  if (last) {
+    const uint64_t zh_inv = a.zh_inv[jn & ((1u << a.rate_bits) - 1)];
+    q[t] = gfn::canon(gfn::mul(acc0, zh_inv));
+    q[N + t] = gfn::canon(gfn::mul(acc1, zh_inv));
+  } else {
+    q[t] = acc0;
+    q[N + t] = acc1;
+  }
+}
+template __global__ void k_quotient_prefix<8>(QuotientArgs, uint32_t, uint32_t);
+
 template __global__ void k_quotient_part<0>(QuotientArgs, uint32_t, uint32_t);
 template __global__ void k_quotient_part<1>(QuotientArgs, uint32_t, uint32_t);
 template __global__ void k_quotient_part<2>(QuotientArgs, uint32_t, uint32_t);
@@ -1441,14 +1629,34 @@ void quotient_values(const QuotientArgs &a, QuotientKernel k, uint32_t nb, hipSt
   const dim3 qg((unsigned)((N + 255) / 256), nb);
   switch (k) {
     case QK_PARTS: {
-      // the permutation terms, then one launch per gate (each streams only its
-      // gate's columns), the last multiplying by 1/Z_H
+      // the permutation terms with the gates that read only routed wires
+      // (k_quotient_prefix: one pass, QPGPU_QPREFIX=0 turns it off), then one
+      // launch per other gate (each streams only its gate's columns), the
+      // last multiplying by 1/Z_H
+      uint32_t gmask = 0;
+      const char *pv = getenv("QPGPU_QPREFIX");
+      if (a.qdf == 8 && !(pv && pv[0] == '0'))
+        for (uint32_t gi = 0; gi < a.g.ngates; gi++) {
+          const uint32_t p = a.g.param[gi];
+          uint64_t wires = ~0ull;
+          switch (a.g.kind[gi]) {
+            case GK_CONSTANT: wires = p <= 2 ? p : ~0ull; break;
+            case GK_PUBLIC_INPUT: wires = 4; break;
+            case GK_BASE_SUM: wires = 1ull + p; break;
+            case GK_ARITHMETIC: wires = 4ull * p; break;
+            case GK_ARITH_EXT: wires = 8ull * p; break;
+            case GK_MUL_EXT: wires = 6ull * p; break;
+            default: break;
+          }
+          if (wires <= a.R) gmask |= 1u << gi;
+        }
       int lastg = -1;
       for (uint32_t gi = 0; gi < a.g.ngates; gi++)
-        if (a.g.kind[gi] != GK_NOOP) lastg = (int)gi;
-      k_quotient_part<0><<<qg, 256, 0, s>>>(a, 0, lastg < 0);
+        if (a.g.kind[gi] != GK_NOOP && !((gmask >> gi) & 1)) lastg = (int)gi;
+      if (gmask) k_quotient_prefix<8><<<qg, 256, 0, s>>>(a, gmask, lastg < 0);
+      else k_quotient_part<0><<<qg, 256, 0, s>>>(a, 0, lastg < 0);
       for (uint32_t gi = 0; gi < a.g.ngates; gi++) {
-        if (a.g.kind[gi] == GK_NOOP) continue;
+        if (a.g.kind[gi] == GK_NOOP || ((gmask >> gi) & 1)) continue;
         if (a.g.kind[gi] == GK_POSEIDON) k_quotient_part<2><<<qg, 256, 0, s>>>(a, gi, (int)gi == lastg);
         else k_quotient_part<1><<<qg, 256, 0, s>>>(a, gi, (int)gi == lastg);
       }

@@ -127,6 +127,21 @@ for s in "$@"; do
     c3prio) step c3_prio0 300 python -u bench.py --steps 2 --warmup 1 --cpu-sample 0 --agg-leaves 0 &&
             step c3_prio1 300 env QP_AGG_PRIORITY=1 python -u bench.py --steps 2 --warmup 1 --cpu-sample 0 --agg-leaves 0 ;;
     aggtrace) step prof_aggsub 300 rocprofv3 --kernel-trace --output-format csv -d gpurun_out/prof_aggsub -o run -- python3 tools/agg_subtree.py 256 2 ;;
+    qprefix) step pytest_qprefix 600 python -u -m pytest tests/test_gpu_aggregation.py tests/test_gpu_seams.py tests/test_gpu_seam_prove.py -x -q --timeout 400 --timeout-method thread &&
+             for r in 1 2; do
+               step qp_new_$r 300 python -u tools/agg_subtree.py 256 2 &&
+               step qp_off_$r 300 env QPGPU_QPREFIX=0 python -u tools/agg_subtree.py 256 2 &&
+               step qp_w3_$r 300 env QPGPU_LIB=gpurun_ab/libqpgpu_qpw3.so python -u tools/agg_subtree.py 256 2 || exit 1
+             done &&
+             step prof_qprefix 300 env QP_AGG_PROVERS=1 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/prof_qprefix -o run -- python3 tools/agg_subtree.py 256 1 &&
+             step prof_qoff 300 env QP_AGG_PROVERS=1 QPGPU_QPREFIX=0 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/prof_qoff -o run -- python3 tools/agg_subtree.py 256 1 ;;
+    ilv) step pytest_ilv 900 python -u -m pytest tests/test_gpu_commit.py tests/test_gpu_reference_proof.py tests/test_gpu_prover.py tests/test_gpu_aggregation.py tests/test_gpu_seams.py -x -q --timeout 400 --timeout-method thread &&
+         for r in 1 2; do
+           step prof_ilv1_$r 300 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/prof_ilv1_$r -o run -- python3 tools/kbench.py 86 2 &&
+           step prof_ilv0_$r 300 env QPGPU_LIB=gpurun_ab/libqpgpu_ilv0.so rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/prof_ilv0_$r -o run -- python3 tools/kbench.py 86 2 || exit 1
+         done &&
+         step bench_ilv1 300 python -u bench.py --steps 10 --warmup 2 --cpu-sample 0 --configs3 0 --agg-leaves 0 &&
+         step bench_ilv0 300 env QPGPU_LIB=gpurun_ab/libqpgpu_ilv0.so python -u bench.py --steps 10 --warmup 2 --cpu-sample 0 --configs3 0 --agg-leaves 0 ;;
     *) echo "unknown step $s" ;;
   esac
 done
