@@ -26,6 +26,8 @@ INSTRS = [
     ("v_mul_hi_u32", 32, "v_mul_hi_u32 %0, %0, %1"),
     ("v_mul_u32_u24", 32, "v_mul_u32_u24_e32 %0, 13, %0"),
     ("v_mad_u32_u24", 32, "v_mad_u32_u24 %0, %0, 13, %1"),
+    ("v_mul_hi_u32_u24", 32, "v_mul_hi_u32_u24_e32 %0, 13, %0"),
+    ("v_mul_u32_u24_vv", 32, "v_mul_u32_u24_e32 %0, %1, %0"),
     ("v_alignbit_b32", 32, "v_alignbit_b32 %0, %0, %1, 7"),
     ("v_lshlrev_b32", 32, "v_lshlrev_b32_e32 %0, 3, %0"),
     ("v_mad_u64_u32", 64, "v_mad_u64_u32 %0, s[40:41], %1, 13, %0"),
@@ -76,6 +78,9 @@ BLOCKS = [
     ("mov_b32 blk", 32, "v_mov_b32_e32 %0, %1", 1, -1),
     ("cndmask blk", 32, "v_cndmask_b32_e64 %0, %0, %1, s[40:41]", 1, -1),
     ("sub_co blk", 32, "v_sub_co_u32_e64 %0, s[42:43], %0, %1", 1, -1),
+    ("mul_u24 blk", 32, "v_mul_u32_u24_e32 %0, %1, %0", 1, -1),
+    ("mul_hi_u24 blk", 32, "v_mul_hi_u32_u24_e32 %0, %1, %0", 1, -1),
+    ("mad_u32_u24 blk", 32, "v_mad_u32_u24 %0, %0, %1, %0", 1, -1),
 ]
 ITERS = 65536
 
