@@ -7,6 +7,8 @@
 #include "field.h"
 #include "poseidon.h"
 #include "poseidon_dev.h"
+#include "poseidon_coop.h"
+#include <stdlib.h>
 #include "kernels.h"
 
 // trees narrower than 2^QP_MERKLE_FUSE_LOG nodes per level finish in one
@@ -175,9 +177,49 @@ __global__ void __launch_bounds__(256) QP_HASH_OCC k_merkle_level(uint64_t *__re
   for (int j = 0; j < 4; j++) o[j] = psd::canon(s[j]);
 }
 
+// one tree level of a small batch: one wave per node (pc::permute, the
+// cooperative permutation).  A level whose nodes x proofs fill a few waves per
+// SIMD at most costs the one-lane form the latency of one permutation
+// (≈70 us: a wave issues its ~15k instructions one per ≈8.5 cycles) whatever
+// its width; this form's chain is ≈125 instructions per round.  Exits are
+// wave-uniform (no barriers).
+__global__ void __launch_bounds__(256) k_merkle_level_coop(uint64_t *__restrict__ digests, uint32_t log_N, uint32_t k,
+                                                           uint64_t d_bstride) {
+  const uint32_t node = blockIdx.x * 4 + (threadIdx.x >> 6), lane = threadIdx.x & 63;
+  if (node >= (1u << (log_N - k))) return;
+  digests += blockIdx.y * d_bstride;
+  const uint64_t top = (uint64_t)1 << (log_N + 1);
+  const uint64_t *c = digests + (top - ((uint64_t)1 << (log_N - k + 2))) * 4 + (uint64_t)node * 8;
+  uint64_t x = lane < 8 ? c[lane] : 0;
+  x = pc::permute(x);
+  uint64_t *o = digests + (top - ((uint64_t)1 << (log_N - k + 1))) * 4 + (uint64_t)node * 4;
+  if (lane < 4) o[lane] = psd::canon(x);
+}
+
 #ifndef QP_MERKLE_SINGLE
 #define QP_MERKLE_SINGLE 1
 #endif
+// levels of at most this many nodes (over all proofs of the launch) run one
+// wave per node (k_merkle_level_coop) in launches of at most
+// QP_MERKLE_COOP_NBAT proofs: the latency-bound small batches of the
+// aggregation tree's upper levels (one aggregation proof 12.5 -> 10.8 ms,
+// 256-leaf subtree 0.42 -> 0.405 s); the leaf bench's 86-proof launches, which
+// share a saturated GPU, keep the one-lane and fused forms (1184 vs 1200
+// proofs/s with coop there; profiles/r05_ab_merkle_coop.log).
+// QPGPU_MERKLE_COOP overrides the node bound, 0 = never
+#ifndef QP_MERKLE_COOP_MAX
+#define QP_MERKLE_COOP_MAX 8192
+#endif
+#ifndef QP_MERKLE_COOP_NBAT
+#define QP_MERKLE_COOP_NBAT 32
+#endif
+static uint32_t merkle_coop_max() {
+  static const uint32_t v = [] {
+    const char *e = getenv("QPGPU_MERKLE_COOP");
+    return e && *e ? (uint32_t)strtoul(e, nullptr, 10) : (uint32_t)QP_MERKLE_COOP_MAX;
+  }();
+  return v;
+}
 
 void leaf_hash(const uint64_t *cols, uint64_t stride, uint32_t ncols, const uint64_t *salt, uint32_t nsalt,
                uint64_t *digests, uint32_t N, uint32_t nbat, uint64_t c_bstride, uint64_t s_bstride,
@@ -189,8 +231,14 @@ void leaf_hash(const uint64_t *cols, uint64_t stride, uint32_t ncols, const uint
 void merkle_tree_from(uint64_t *digests, uint32_t log_N, uint32_t cap_h, uint32_t nbat, uint64_t d_bstride,
                       uint32_t first_level, hipStream_t s) {
   const uint32_t K = log_N - cap_h;  // levels above the leaves
+  const uint64_t coop_max = merkle_coop_max();
   for (uint32_t k0 = first_level; k0 <= K;) {
     const uint32_t lc = log_N - k0;  // log2(nodes at level k0)
+    if (nbat <= QP_MERKLE_COOP_NBAT && ((uint64_t)nbat << lc) <= coop_max) {
+      k_merkle_level_coop<<<dim3(((1u << lc) + 3) / 4, nbat), 256, 0, s>>>(digests, log_N, k0, d_bstride);
+      k0++;
+      continue;
+    }
     const uint32_t lb = lc < 8 ? lc : 8;
     // wide levels one launch each (a fused block would idle all but one
     // wave through its lower levels: measured 165 -> 222 ms per bench run);

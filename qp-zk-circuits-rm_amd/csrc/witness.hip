@@ -18,6 +18,7 @@
 #include "field.h"
 #include "poseidon.h"
 #include "poseidon_dev.h"
+#include "poseidon_coop.h"
 #include "witness_kernels.h"
 
 namespace qpk {
@@ -249,17 +250,7 @@ __device__ __noinline__ bool poseidon_witness(uint64_t *v, const uint32_t *__res
 // The dependent chain of a round is one S-box plus six products (the
 // one-lane form runs all 12 S-boxes and 12 MDS rows in sequence).  All 64
 // lanes must be active; lanes >= 12 compute and never write.
-__device__ __forceinline__ uint64_t wave_mds_row(uint64_t y, const uint32_t (&coef)[12]) {
-  const uint32_t lo = (uint32_t)y, hi = (uint32_t)(y >> 32);
-  uint64_t al[2] = {0, 0}, ah[2] = {0, 0};
-#pragma unroll
-  for (int j = 0; j < 12; j++) {
-    const uint32_t xl = __builtin_amdgcn_readlane(lo, j), xh = __builtin_amdgcn_readlane(hi, j);
-    al[j & 1] += (uint64_t)xl * coef[j];
-    ah[j & 1] += (uint64_t)xh * coef[j];
-  }
-  return pf::reduce_row(al[0] + al[1], ah[0] + ah[1]);
-}
+using pc::wave_mds_row;
 __device__ __noinline__ bool poseidon_coop(uint64_t *v, const uint32_t *__restrict__ ws) {
   const uint32_t lane = threadIdx.x & 63;
   const bool act = lane < 12;

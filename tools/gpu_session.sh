@@ -142,6 +142,16 @@ for s in "$@"; do
          done &&
          step bench_ilv1 300 python -u bench.py --steps 10 --warmup 2 --cpu-sample 0 --configs3 0 --agg-leaves 0 &&
          step bench_ilv0 300 env QPGPU_LIB=gpurun_ab/libqpgpu_ilv0.so python -u bench.py --steps 10 --warmup 2 --cpu-sample 0 --configs3 0 --agg-leaves 0 ;;
+    mcoop) step pytest_mcoop 900 python -u -m pytest tests/test_gpu_commit.py tests/test_gpu_reference_proof.py tests/test_gpu_prover.py tests/test_gpu_aggregation.py tests/test_gpu_seams.py tests/test_gpu_witness.py -x -q --timeout 400 --timeout-method thread &&
+           step agglat_coop 300 python -u tools/agg_latency.py 1,2,4,8,16 5 &&
+           step agglat_nocoop 300 env QPGPU_MERKLE_COOP=0 python -u tools/agg_latency.py 1,2,4,8,16 5 &&
+           for r in 1 2; do
+             step sub_coop_$r 300 python -u tools/agg_subtree.py 256 2 &&
+             step sub_nocoop_$r 300 env QPGPU_MERKLE_COOP=0 python -u tools/agg_subtree.py 256 2 || exit 1
+           done &&
+           step bench_coop 300 python -u bench.py --steps 10 --warmup 2 --cpu-sample 0 --configs3 0 --agg-leaves 0 &&
+           step bench_nocoop 300 env QPGPU_MERKLE_COOP=0 python -u bench.py --steps 10 --warmup 2 --cpu-sample 0 --configs3 0 --agg-leaves 0 ;;
+    leafub) step leaf_ubench 300 tools/leaf_ubench 86 5 ;;
     *) echo "unknown step $s" ;;
   esac
 done
