@@ -152,6 +152,15 @@ for s in "$@"; do
            step bench_coop 300 python -u bench.py --steps 10 --warmup 2 --cpu-sample 0 --configs3 0 --agg-leaves 0 &&
            step bench_nocoop 300 env QPGPU_MERKLE_COOP=0 python -u bench.py --steps 10 --warmup 2 --cpu-sample 0 --configs3 0 --agg-leaves 0 ;;
     leafub) step leaf_ubench 300 tools/leaf_ubench 86 5 ;;
+    leaft) step pytest_leaft 600 python -u -m pytest tests/test_gpu_commit.py tests/test_gpu_reference_proof.py tests/test_gpu_prover.py tests/test_gpu_voting.py -x -q --timeout 400 --timeout-method thread &&
+           for r in 1 2; do
+             step prof_leaft1_$r 300 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/prof_leaft1_$r -o run -- python3 tools/kbench.py 86 2 &&
+             step prof_leaft0_$r 300 env QPGPU_LEAF_T=0 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/prof_leaft0_$r -o run -- python3 tools/kbench.py 86 2 || exit 1
+           done &&
+           for r in 1 2; do
+             step bench_leaft1_$r 300 python -u bench.py --steps 10 --warmup 2 --cpu-sample 0 --configs3 0 --agg-leaves 0 &&
+             step bench_leaft0_$r 300 env QPGPU_LEAF_T=0 python -u bench.py --steps 10 --warmup 2 --cpu-sample 0 --configs3 0 --agg-leaves 0 || exit 1
+           done ;;
     *) echo "unknown step $s" ;;
   esac
 done
