@@ -551,6 +551,33 @@ __global__ void __launch_bounds__(512) k_witness_gen(const WitnessGenArgs a) {
   if (!ok) atomicCAS(a.err + b, 0u, bad);
 }
 
+// one dependency level over the whole batch (the level-launch mode for small
+// batches: a launch per level instead of one workgroup per proof walking every
+// level): blocks [0, na) run the level's non-Poseidon generators one per lane,
+// blocks [na, ..) its Poseidon generators one per wave (poseidon_coop), so a
+// level costs one cooperative permutation's latency (≈25 us) rather than a
+// one-lane permutation's (≈65 us) or several cooperative ones in sequence.
+// Stream order separates the levels; the first failure per proof wins the CAS.
+__global__ void __launch_bounds__(256) k_witness_level(const WitnessGenArgs a, uint32_t l, uint32_t na) {
+  const uint32_t b = blockIdx.y;
+  uint64_t *v = a.vals + (uint64_t)b * a.v_bstride;
+  const DevGenD *gens = (const DevGenD *)a.gens;
+  const uint32_t lo = a.level_off[l], hi = a.level_off[l + 1];
+  const uint32_t plo = a.level_pos[2 * l], pcnt = a.level_pos[2 * l + 1];
+  uint32_t bad = 0;
+  if (blockIdx.x < na) {
+    const uint32_t k = blockIdx.x * blockDim.x + threadIdx.x;
+    if (k < hi - lo - pcnt) {
+      const uint32_t i = k < plo - lo ? lo + k : lo + k + pcnt;  // skip the Poseidon run [plo, plo + pcnt)
+      if (!run_gen(gens[i], v, a.wslot, a.W, a.limbs, a.zero_slot, a.num_consts)) bad = i + 1;
+    }
+  } else {
+    const uint32_t p = (blockIdx.x - na) * (blockDim.x >> 6) + (threadIdx.x >> 6);  // wave-uniform
+    if (p < pcnt && !poseidon_coop(v, a.wslot + (uint64_t)gens[plo + p].row * a.W)) bad = plo + p + 1;
+  }
+  if (bad) atomicCAS(a.err + b, 0u, bad);
+}
+
 // wires [b][col][row] = slot values through the column-major slot map;
 // public inputs gathered alongside
 __global__ void k_witness_expand(const uint64_t *vals, uint64_t v_bstride, const uint32_t *wslot_cm, uint64_t nwires,

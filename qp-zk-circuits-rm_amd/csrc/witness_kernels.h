@@ -23,6 +23,8 @@ __global__ void k_witness_init(uint64_t *vals, uint64_t v_bstride, uint32_t nslo
 __global__ void k_witness_inputs(uint64_t *vals, uint64_t v_bstride, const uint32_t *in_slots,
                                  const uint64_t *in_vals, uint32_t nin);
 __global__ void k_witness_gen(const WitnessGenArgs a);
+// one dependency level of nb proofs (grid (na + Poseidon blocks, nb), 256 threads)
+__global__ void k_witness_level(const WitnessGenArgs a, uint32_t l, uint32_t na);
 __global__ void k_witness_expand(const uint64_t *vals, uint64_t v_bstride, const uint32_t *wslot_cm, uint64_t nwires,
                                  uint64_t *wires, uint64_t w_bstride, const uint32_t *pi_slots, uint32_t npis,
                                  uint64_t *pis);

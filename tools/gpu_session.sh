@@ -161,6 +161,13 @@ for s in "$@"; do
              step bench_leaft1_$r 300 python -u bench.py --steps 10 --warmup 2 --cpu-sample 0 --configs3 0 --agg-leaves 0 &&
              step bench_leaft0_$r 300 env QPGPU_LEAF_T=0 python -u bench.py --steps 10 --warmup 2 --cpu-sample 0 --configs3 0 --agg-leaves 0 || exit 1
            done ;;
+    witlev) step pytest_witlev 900 python -u -m pytest tests/test_gpu_aggregation.py tests/test_gpu_witness.py tests/test_gpu_seam_prove.py -x -q --timeout 400 --timeout-method thread &&
+            step agglat_lev 300 python -u tools/agg_latency.py 1,2,4,8,16,32 5 &&
+            step agglat_wg 300 env QPGPU_WIT_MODE=wg python -u tools/agg_latency.py 1,2,4,8,16,32 5 &&
+            for r in 1 2; do
+              step sub_lev_$r 300 python -u tools/agg_subtree.py 256 2 &&
+              step sub_wg_$r 300 env QPGPU_WIT_MODE=wg python -u tools/agg_subtree.py 256 2 || exit 1
+            done ;;
     *) echo "unknown step $s" ;;
   esac
 done
