@@ -239,22 +239,17 @@ __global__ void __launch_bounds__(256) k_merkle_level_coop(uint64_t *__restrict_
 #ifndef QP_MERKLE_COOP_NBAT
 #define QP_MERKLE_COOP_NBAT 32
 #endif
-static uint32_t merkle_coop_max() {
-  static const uint32_t v = [] {
-    const char *e = getenv("QPGPU_MERKLE_COOP");
-    return e && *e ? (uint32_t)strtoul(e, nullptr, 10) : (uint32_t)QP_MERKLE_COOP_MAX;
-  }();
-  return v;
+static uint32_t merkle_coop_max() {  // read per tree: tests switch it in one process
+  const char *e = getenv("QPGPU_MERKLE_COOP");
+  return e && *e ? (uint32_t)strtoul(e, nullptr, 10) : (uint32_t)QP_MERKLE_COOP_MAX;
 }
 
 void leaf_hash(const uint64_t *cols, uint64_t stride, uint32_t ncols, const uint64_t *salt, uint32_t nsalt,
                uint64_t *digests, uint32_t N, uint32_t nbat, uint64_t c_bstride, uint64_t s_bstride,
                uint64_t d_bstride, hipStream_t s) {
   dim3 grid((N + 255) / 256, nbat);
-  static const bool generic = [] {
-    const char *e = getenv("QPGPU_LEAF_T");
-    return e && e[0] == '0';
-  }();
+  const char *lt = getenv("QPGPU_LEAF_T");
+  const bool generic = lt && lt[0] == '0';
   if (!nsalt && !generic) {
     switch (ncols) {
       case 135: k_leaf_hash_t<135><<<grid, 256, 0, s>>>(cols, stride, digests, N, c_bstride, d_bstride); return;

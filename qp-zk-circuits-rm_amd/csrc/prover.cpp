@@ -1039,7 +1039,7 @@ int gen_witness_batch(qp_prover *P, uint32_t nb) {
   // one permutation deep, and one workgroup per proof leaves each level at a
   // one-lane permutation's latency) or one workgroup per proof (the leaf
   // circuits' default)
-  static const int wmode = [] {
+  const int wmode = [] {  // read per call: tests switch modes in one process
     const char *e = getenv("QPGPU_WIT_MODE");
     return e && !strcmp(e, "levels") ? 1 : e && !strcmp(e, "wg") ? 0 : -1;
   }();

@@ -255,3 +255,42 @@ def test_device_witness_zk_aggregation(reference_leaves):
     b, = p.prove_aggregation(vo, [leaves])
     assert a != b and verify(vd, a) == 0 and verify(vd, b) == 0
     p.free()
+
+
+@pytest.mark.parametrize("env", [{"QPGPU_WIT_MODE": "wg"}, {"QPGPU_WIT_MODE": "levels"}, {"QPGPU_MERKLE_COOP": "0"},
+                                 {"QPGPU_QPREFIX": "0"}, {"QPGPU_LEAF_T": "0"}])
+def test_latency_paths_prove_the_same_bytes(reference_leaves, monkeypatch, env):
+    """The small-batch paths (device witness one launch per dependency level or
+    one workgroup per proof, cooperative Merkle levels, the prefix quotient
+    kernel, the compile-time leaf hash) against their alternatives: the same
+    proof bytes, at batch 1 and 3."""
+    import qp_wormhole
+    cb, vo, leaves = reference_leaves
+    circ = qp_wormhole.Circuit.aggregation(cb, 2)
+    chunks = [leaves, leaves[::-1], [leaves[1], leaves[1]]]
+    out = []
+    for e in ({}, env):
+        for k, v in e.items():
+            monkeypatch.setenv(k, v)
+        p = qp_wormhole.Prover(qp_wormhole.Context(0), circ, max_batch=3)
+        out.append((p.prove_aggregation(vo, chunks[:1]), p.prove_aggregation(vo, chunks)))
+        p.free()
+        for k in e:
+            monkeypatch.delenv(k)
+    assert out[0] == out[1]
+
+
+def test_high_priority_context_proves_the_same_bytes(reference_leaves):
+    """qp_ctx_set_priority: the level provers' optional high-priority stream."""
+    import qp_wormhole
+    cb, vo, leaves = reference_leaves
+    circ = qp_wormhole.Circuit.aggregation(cb, 2)
+    res = []
+    for high in (False, True):
+        ctx = qp_wormhole.Context(0)
+        if high:
+            ctx.set_priority(True)
+        p = qp_wormhole.Prover(ctx, circ, max_batch=1)
+        res.append(p.prove_aggregation(vo, [leaves])[0])
+        p.free()
+    assert res[0] == res[1]
