@@ -48,6 +48,24 @@ KSUM1_FILE = os.path.join(ROOT, "profiles", f"{PROFILE_TAG}_kernel_summary_1prov
 # per-class wall-time costs from a counter pass over saturated single-instruction
 # kernels, weighted by the kernel's static mix)
 CEIL_FILE = os.path.join(ROOT, "profiles", f"{PROFILE_TAG}_issue_ceiling.json")
+UBENCH_FILE = os.path.join(ROOT, "profiles", f"{PROFILE_TAG}_leaf_ubench.log")
+
+
+def register_replay():
+    """tools/leaf_ubench: the leaf-hash loop as built (L0) against the same loop
+    with the absorbed chunk derived from the lane index instead of loaded (L3),
+    back to back in one run: the kernel's instruction stream without memory is
+    its own issue ceiling, free of the per-class pricing of mix_ceiling."""
+    import re
+    try:
+        txt = open(UBENCH_FILE).read()
+    except OSError:
+        return None
+    g = {m.group(1): float(m.group(2)) for m in re.finditer(r"^(L\d)\b.*?([\d.]+) Gperm/s", txt, re.M)}
+    if "L0" not in g or "L3" not in g:
+        return None
+    return {"production_gperm_s": g["L0"], "no_load_gperm_s": g["L3"], "frac": g["L0"] / g["L3"],
+            "source": os.path.relpath(UBENCH_FILE, ROOT)}
 
 
 def load_json(path):
@@ -62,7 +80,7 @@ def perm_valu_instr():
     wires leaf-hash dispatch (17 permutations per leaf) in this build's PMC pass."""
     recs = load_json(PMC_SQ_FILE) or []
     for r in recs:
-        if r.get("kernel") == "qpk::k_leaf_hash" and r.get("valu_per_lane_max"):
+        if (r.get("kernel") or "").startswith("qpk::k_leaf_hash") and r.get("valu_per_lane_max"):
             return r["valu_per_lane_max"] / 17.0
     return None
 
@@ -663,6 +681,7 @@ def main():
         ksum, ksum1, ceil = load_json(KSUM_FILE), load_json(KSUM1_FILE), load_json(CEIL_FILE)
         if vk.get("leaf_hash_wires_perms_per_s") and ipp:
             ach = vk["leaf_hash_wires_perms_per_s"] / 64 * ipp
+            rr = register_replay()
             rec["dominant_kernel"] = {
                 "kernel": "k_leaf_hash (Poseidon Merkle leaves)", "bound": "valu",
                 # one prover: kernels do not overlap, so shares are shares of GPU time
@@ -676,6 +695,10 @@ def main():
                 # at its own clock, both from the same counter-pass dispatches
                 "frac_of_mix_ceiling_at_own_clock": ceil.get("frac_of_ceiling_in_counter_pass") if ceil else None,
                 "own_clock_ghz_in_counter_pass": ceil.get("leaf_hash_clock_ghz") if ceil else None,
+                # the additive class model underprices this mix (frac > 1 above):
+                # the loop replayed from registers is the ceiling that holds
+                "frac_of_register_replay": rr["frac"] if rr else None,
+                "register_replay": rr,
                 "sources": {"instr_per_perm": os.path.relpath(PMC_SQ_FILE, ROOT),
                             "mix_ceiling": os.path.relpath(CEIL_FILE, ROOT) if ceil else None,
                             "share": os.path.relpath(KSUM1_FILE, ROOT) if ksum1 else None,

@@ -73,7 +73,10 @@ def class_costs(d):
 
 
 def leaf_dispatches(d):
-    xs = [x for x in dispatches(d).values() if x["k"].endswith("k_leaf_hash")]
+    # the wires leaf hash: k_leaf_hash_t<135u> (compile-time column count), or
+    # the run-time form k_leaf_hash of earlier builds
+    ds = list(dispatches(d).values())
+    xs = [x for x in ds if x["k"].endswith("k_leaf_hash_t<135u>")] or [x for x in ds if x["k"].endswith("k_leaf_hash")]
     if not xs:
         return []
     g = max(x["grid"] for x in xs)
@@ -101,7 +104,9 @@ def static_mix():
         subprocess.run(["hipcc", "--offload-arch=gfx950", "-O3", "-std=c++17", "--cuda-device-only", "-S",
                         os.path.join(CSRC, "merkle.hip"), "-o", s], check=True, capture_output=True)
         text = open(s).read()
-    m = re.search(r"^(_ZN3qpk11k_leaf_hashE\w*):[^\n]*\n(.*?)\n\s*s_endpgm", text, re.S | re.M)
+    # the wires form k_leaf_hash_t<135> (compile-time column count), else k_leaf_hash
+    m = re.search(r"^(_ZN3qpk13k_leaf_hash_tILj135EE\w*):[^\n]*\n(.*?)\n\s*s_endpgm", text, re.S | re.M) or \
+        re.search(r"^(_ZN3qpk11k_leaf_hashE\w*):[^\n]*\n(.*?)\n\s*s_endpgm", text, re.S | re.M)
     ops = collections.Counter()
     for line in m.group(2).split("\n"):
         line = line.strip()

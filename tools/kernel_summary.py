@@ -4,7 +4,7 @@ bench JSON's measured fields (bench.py reads the JSON this writes):
   gpu_busy_frac:    |union of kernel intervals| / window: the fraction of the
                     window in which some kernel ran (with concurrent provers,
                     kernels of different streams overlap)
-  leaf_hash_share:  k_leaf_hash's share of all kernel time
+  leaf_hash_share:  the leaf-hash kernels' share of all kernel time (k_leaf_hash, k_leaf_hash_t<NC>)
 The window is the bench's timed region when the trace holds bench.py's two
 trace markers (at::cuda spin kernels launched just outside each end of the
 timed steps): kernels that start after the first marker ends and end before the
@@ -62,7 +62,8 @@ def main():
     rec = {"source": path, "label": sys.argv[3] if len(sys.argv) > 3 else "", "scope": scope, "lib_sha16": lib_sha16(),
            "window_ms": window / 1e6, "kernel_ms": total,
            "gpu_busy_frac": union_ms([(a, b) for a, b, _ in sel]) / window,
-           "leaf_hash_share": per.get("qpk::k_leaf_hash", [0])[0] / total,
+           # k_leaf_hash and its compile-time column-count forms k_leaf_hash_t<NC>
+           "leaf_hash_share": sum(v[0] for k, v in per.items() if k.startswith("qpk::k_leaf_hash")) / total,
            "kernels": {k: {"ms": v[0], "launches": v[1], "share": v[0] / total}
                        for k, v in sorted(per.items(), key=lambda kv: -kv[1][0])}}
     json.dump(rec, open(out, "w"), indent=1)
