@@ -222,6 +222,21 @@ __global__ void __launch_bounds__(256) k_merkle_level_coop(uint64_t *__restrict_
   if (lane < 4) o[lane] = psd::canon(x);
 }
 
+// the row form: one 16-lane row per node (pc::permute_row), 16 nodes per
+// block; rows past the level's end exit together
+__global__ void __launch_bounds__(256) k_merkle_level_row(uint64_t *__restrict__ digests, uint32_t log_N, uint32_t k,
+                                                          uint64_t d_bstride) {
+  const uint32_t node = blockIdx.x * 16 + (threadIdx.x >> 4), l16 = threadIdx.x & 15;
+  if (node >= (1u << (log_N - k))) return;
+  digests += blockIdx.y * d_bstride;
+  const uint64_t top = (uint64_t)1 << (log_N + 1);
+  const uint64_t *c = digests + (top - ((uint64_t)1 << (log_N - k + 2))) * 4 + (uint64_t)node * 8;
+  uint64_t x = l16 < 8 ? c[l16] : 0;
+  x = pc::permute_row(x);
+  uint64_t *o = digests + (top - ((uint64_t)1 << (log_N - k + 1))) * 4 + (uint64_t)node * 4;
+  if (l16 < 4) o[l16] = psd::canon(x);
+}
+
 #ifndef QP_MERKLE_SINGLE
 #define QP_MERKLE_SINGLE 1
 #endif
@@ -232,6 +247,10 @@ __global__ void __launch_bounds__(256) k_merkle_level_coop(uint64_t *__restrict_
 // 256-leaf subtree 0.42 -> 0.405 s); the leaf bench's 86-proof launches, which
 // share a saturated GPU, keep the one-lane and fused forms (1184 vs 1200
 // proofs/s with coop there; profiles/r05_ab_merkle_coop.log).
+// The row form (k_merkle_level_row: four nodes per wave, DPP broadcasts) takes
+// levels up to QP_MERKLE_ROW_MAX nodes: 256-leaf subtree 0.387 -> 0.361-0.365 s
+// with the row forms of the FRI leaves, the sliced openings and the per-coset
+// LDE of few columns (profiles/r05_ab_small_batch.log).
 // QPGPU_MERKLE_COOP overrides the node bound, 0 = never
 #ifndef QP_MERKLE_COOP_MAX
 #define QP_MERKLE_COOP_MAX 8192
@@ -239,9 +258,17 @@ __global__ void __launch_bounds__(256) k_merkle_level_coop(uint64_t *__restrict_
 #ifndef QP_MERKLE_COOP_NBAT
 #define QP_MERKLE_COOP_NBAT 32
 #endif
-static uint32_t merkle_coop_max() {  // read per tree: tests switch it in one process
+#ifndef QP_MERKLE_ROW_MAX
+#define QP_MERKLE_ROW_MAX 32768
+#endif
+// QPGPU_MERKLE_ROW=0: the one-wave-per-node form instead of the row form
+static bool merkle_row() {  // read per tree: tests switch it in one process
+  const char *e = getenv("QPGPU_MERKLE_ROW");
+  return !(e && e[0] == '0');
+}
+static uint32_t merkle_coop_max(bool row) {
   const char *e = getenv("QPGPU_MERKLE_COOP");
-  return e && *e ? (uint32_t)strtoul(e, nullptr, 10) : (uint32_t)QP_MERKLE_COOP_MAX;
+  return e && *e ? (uint32_t)strtoul(e, nullptr, 10) : row ? (uint32_t)QP_MERKLE_ROW_MAX : (uint32_t)QP_MERKLE_COOP_MAX;
 }
 
 void leaf_hash(const uint64_t *cols, uint64_t stride, uint32_t ncols, const uint64_t *salt, uint32_t nsalt,
@@ -264,11 +291,15 @@ void leaf_hash(const uint64_t *cols, uint64_t stride, uint32_t ncols, const uint
 void merkle_tree_from(uint64_t *digests, uint32_t log_N, uint32_t cap_h, uint32_t nbat, uint64_t d_bstride,
                       uint32_t first_level, hipStream_t s) {
   const uint32_t K = log_N - cap_h;  // levels above the leaves
-  const uint64_t coop_max = merkle_coop_max();
+  const bool row = merkle_row();
+  const uint64_t coop_max = merkle_coop_max(row);
   for (uint32_t k0 = first_level; k0 <= K;) {
     const uint32_t lc = log_N - k0;  // log2(nodes at level k0)
     if (nbat <= QP_MERKLE_COOP_NBAT && ((uint64_t)nbat << lc) <= coop_max) {
-      k_merkle_level_coop<<<dim3(((1u << lc) + 3) / 4, nbat), 256, 0, s>>>(digests, log_N, k0, d_bstride);
+      if (row)
+        k_merkle_level_row<<<dim3(((1u << lc) + 15) / 16, nbat), 256, 0, s>>>(digests, log_N, k0, d_bstride);
+      else
+        k_merkle_level_coop<<<dim3(((1u << lc) + 3) / 4, nbat), 256, 0, s>>>(digests, log_N, k0, d_bstride);
       k0++;
       continue;
     }

@@ -507,6 +507,9 @@ void intt(const Twiddles &t, const uint64_t *in, uint64_t in_stride, uint64_t *o
                                                          in_bstride, out_bstride);
 }
 
+#ifndef QP_LDE_FEW
+#define QP_LDE_FEW 256
+#endif
 void lde(const Twiddles &t, const uint64_t *coeffs, uint64_t c_stride, uint64_t *out, uint64_t o_stride,
          uint32_t ncols, uint32_t log_n, uint32_t rate_bits, uint64_t shift, uint32_t nbat, uint64_t c_bstride,
          uint64_t o_bstride, hipStream_t s) {
@@ -523,8 +526,14 @@ void lde(const Twiddles &t, const uint64_t *coeffs, uint64_t c_stride, uint64_t 
   }
   // n = 2^14 (the aggregation circuits): 1024 threads x 16 and 135 KB of LDS,
   // one workgroup per CU
+  // fewer columns x proofs than QP_LDE_FEW (QPGPU_LDE_FEW overrides, 0 =
+  // never): one workgroup per coset (k_lde), since one per column would leave
+  // most CUs idle while each walks its 2^rate cosets in turn (small
+  // aggregation batches, FRI layers)
+  const char *fe = getenv("QPGPU_LDE_FEW");
+  const uint64_t few = fe && *fe ? strtoull(fe, nullptr, 10) : QP_LDE_FEW;
   if (rate_bits >= 1 && rate_bits <= LDE_MAX_RATE && log_n >= LDE_COSETS_MIN_LOG && log_n <= LDE_COSETS_MAX_LOG &&
-      log_n + rate_bits <= TW_LOG &&
+      log_n + rate_bits <= TW_LOG && (uint64_t)ncols * nbat >= few &&
       !getenv_flag("QPGPU_LDE_PERCOSET")) {
     dim3 g(ncols, nbat);
     const size_t lds_bytes = (size_t)8 * (qpk::ntt_lds_words(1u << log_n) + QP_LDE_ALDS * (1u << (log_n - 4)));

@@ -104,7 +104,7 @@ struct qp_prover {
   Tree cs;
   DevBuf sigmas, kis;
   Tree wires, zs, quot;
-  DevBuf chal, apow, prods, qvals, cbuf, openings, comp, fin, pow_state, pow_found, pow_pos, pow_active, pow_next, qidx,
+  DevBuf chal, apow, prods, qvals, cbuf, openings, open_part, comp, fin, pow_state, pow_found, pow_pos, pow_active, pow_next, qidx,
       qout, qtab;
   std::vector<DevBuf> fvals, fdig, fcoef;
   size_t qout_words = 0;
@@ -341,6 +341,7 @@ int setup(qp_prover *P) {
   TRY(P->qvals.alloc((size_t)B * P->nc * N));
   TRY(P->cbuf.alloc((size_t)B * P->nc * N));
   TRY(P->openings.alloc((size_t)B * qpk::OPEN_STRIDE));
+  TRY(P->open_part.alloc((size_t)B * qpk::OPEN_MAX_SLICES * qpk::OPEN_STRIDE));
   TRY(P->comp.alloc((size_t)B * 4 * n));
   TRY(P->fin.alloc((size_t)B * 2 * N));
   TRY(hipMemsetAsync(P->fin.p, 0, (size_t)B * 2 * N * 8, c->stream));
@@ -705,17 +706,26 @@ int prove_batch(qp_prover *P, const uint64_t *d_wires, const uint64_t *const *wi
   // ---- 4. openings (a10)
   {
     const uint32_t ncs = P->NC + P->R, nzs = nc * P->nchunks, nq = nc * P->qdf;
-    const unsigned ot = (unsigned)std::min<uint64_t>(256, std::max<uint64_t>(64, n / 4));
-    auto og = [&](uint32_t np) { return dim3((np + qpk::OPEN_PB - 1) / qpk::OPEN_PB, nb); };
-    qpk::k_openings<<<og(ncs), ot, 0, s>>>(P->cs.coeffs.p, 0, ncs, P->log_n, P->chal.p, qpk::CH_ZETA, P->openings.p, 0);
-    qpk::k_openings<<<og(P->W), ot, 0, s>>>(P->wires.coeffs.p, P->wires.cbs(), P->W, P->log_n, P->chal.p,
-                                            qpk::CH_ZETA, P->openings.p, ncs);
-    qpk::k_openings<<<og(nzs), ot, 0, s>>>(P->zs.coeffs.p, P->zs.cbs(), nzs, P->log_n, P->chal.p, qpk::CH_ZETA,
-                                           P->openings.p, ncs + P->W);
-    qpk::k_openings<<<og(nq), ot, 0, s>>>(P->quot.coeffs.p, P->quot.cbs(), nq, P->log_n, P->chal.p, qpk::CH_ZETA,
-                                          P->openings.p, ncs + P->W + nzs);
-    qpk::k_openings<<<og(nc), ot, 0, s>>>(P->zs.coeffs.p, P->zs.cbs(), nc, P->log_n, P->chal.p, qpk::CH_ZETA_NEXT,
-                                          P->openings.p, ncs + P->W + nzs + nq);
+    // the zeta batch in oracle order (constants+sigmas, wires, Z+partial
+    // products, quotient chunks), then the g*zeta batch (the Zs)
+    qpk::OpeningsArgs oa;
+    const struct { const uint64_t *c; uint64_t bs; uint32_t np, pt; } segs[5] = {
+        {P->cs.coeffs.p, 0, ncs, qpk::CH_ZETA},
+        {P->wires.coeffs.p, P->wires.cbs(), P->W, qpk::CH_ZETA},
+        {P->zs.coeffs.p, P->zs.cbs(), nzs, qpk::CH_ZETA},
+        {P->quot.coeffs.p, P->quot.cbs(), nq, qpk::CH_ZETA},
+        {P->zs.coeffs.p, P->zs.cbs(), nc, qpk::CH_ZETA_NEXT}};
+    uint32_t off = 0;
+    for (const auto &g : segs) {
+      if (!g.np) continue;
+      oa.seg[oa.nseg++] = qpk::OpenSeg{g.c, g.bs, g.np, g.pt, off, 0};
+      off += g.np;
+    }
+    oa.log_n = P->log_n;
+    oa.pts = P->chal.p;
+    oa.out = P->openings.p;
+    oa.part = P->open_part.p;
+    qpk::openings(oa, nb, s);
     TRY(hipGetLastError());
     TRY(hipMemcpyAsync(P->h_open.data(), P->openings.p, (size_t)nb * qpk::OPEN_STRIDE * 8, hipMemcpyDeviceToHost, s));
     TRY(hipStreamSynchronize(s));
@@ -765,8 +775,7 @@ int prove_batch(qp_prover *P, const uint64_t *d_wires, const uint64_t *const *wi
       qpk::lde(c->tw, coef, coef_cs, P->fvals[l].p, 1ull << lg, 2, coef_log, lg - coef_log, shift, nb, coef_bs,
                2ull << lg, s);
       const uint64_t dbs = qpk::tree_digest_count(lg - ab, P->cap_h) * 4;
-      qpk::k_fri_leaf<<<dim3(cdiv(1ull << (lg - ab), 256), nb), 256, 0, s>>>(P->fvals[l].p, P->fdig[l].p, lg, ab,
-                                                                            2ull << lg, dbs);
+      qpk::fri_leaf(P->fvals[l].p, P->fdig[l].p, lg, ab, 2ull << lg, dbs, nb, s);
       qpk::merkle_tree(P->fdig[l].p, lg - ab, P->cap_h, nb, dbs, s);
       TRY(hipGetLastError());
       if ((rc = fetch_caps(P, P->fdig[l].p, dbs, lg - ab, nb))) return rc;

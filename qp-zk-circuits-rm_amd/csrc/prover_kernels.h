@@ -107,12 +107,35 @@ void quotient_coeffs(const Twiddles &tw, const uint64_t *qvals, uint64_t *cbuf, 
 constexpr int OPEN_PB = 8;  // polys per k_openings block
 __global__ void k_openings(const uint64_t *coeffs, uint64_t c_bstride, uint32_t npolys, uint32_t log_n,
                            const uint64_t *pts, uint32_t pt_off, uint64_t *out, uint32_t out_off);
+// every opening batch of a proof (OpeningSet::new's zeta and g*zeta
+// evaluations) in one launch (+ a reduction when the coefficient range is
+// split over S slices); out[b][OPEN_STRIDE] as k_openings writes it
+constexpr int OPEN_MAX_SEG = 6, OPEN_MAX_SLICES = 16;
+struct OpenSeg {
+  const uint64_t *coeffs;
+  uint64_t c_bstride;
+  uint32_t npolys, pt_off, out_off, g0;
+};
+struct OpeningsArgs {
+  OpenSeg seg[OPEN_MAX_SEG];
+  uint32_t nseg = 0, ngroups = 0, log_n = 0, S = 1, ntot = 0;
+  const uint64_t *pts = nullptr;
+  uint64_t *out = nullptr, *part = nullptr;  // part: nb * OPEN_MAX_SLICES * OPEN_STRIDE words
+};
+__global__ void k_openings_seg(OpeningsArgs a);
+__global__ void k_openings_reduce(const uint64_t *part, uint64_t *out, uint32_t ntot, uint32_t S);
+void openings(OpeningsArgs a, uint32_t nb, hipStream_t s);
 __global__ void k_fri_compose(FriComposeArgs a);
 template <int MAXPER>
 __global__ void k_fri_divide(const uint64_t *comp, uint64_t *fin, uint32_t log_n, const uint64_t *chal,
                              uint64_t f_bstride, uint64_t f_cstride);
 __global__ void k_fri_leaf(const uint64_t *vals, uint64_t *dig, uint32_t log_len, uint32_t ab, uint64_t v_bstride,
                            uint64_t d_bstride);
+__global__ void k_fri_leaf_row(const uint64_t *vals, uint64_t *dig, uint32_t log_len, uint32_t ab, uint64_t v_bstride,
+                               uint64_t d_bstride);
+// the leaf digests of a FRI layer for nb proofs (row or one-lane form by size)
+void fri_leaf(const uint64_t *vals, uint64_t *dig, uint32_t log_len, uint32_t ab, uint64_t v_bstride,
+              uint64_t d_bstride, uint32_t nb, hipStream_t s);
 __global__ void k_fold(const uint64_t *cin, uint64_t *cout, uint32_t log_len, uint32_t ab, uint32_t layer,
                        const uint64_t *chal, uint64_t i_bstride, uint64_t o_bstride, uint32_t log_nz);
 __global__ void k_pow_scan(const uint64_t *states, const uint32_t *pos, uint64_t *found, uint64_t *next, uint32_t nb,

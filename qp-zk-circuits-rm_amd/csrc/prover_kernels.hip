@@ -15,8 +15,10 @@
 #include "field.h"
 #include "poseidon.h"
 #include "poseidon_dev.h"
+#include "poseidon_coop.h"
 #include "prover_kernels.h"
 #include <stdlib.h>
+#include <algorithm>
 #include "ntt16.h"
 
 namespace qpk {
@@ -1735,6 +1737,82 @@ __global__ void __launch_bounds__(256) k_openings(const uint64_t *__restrict__ c
   }
 }
 
+// all of a proof's opening batches in one launch: segment j's polys form
+// groups of OPEN_PB from group g0; each group's coefficient range splits into
+// S slices of n / S (a small batch otherwise leaves most CUs idle: one proof
+// has ~33 groups), whose partial sums k_openings_reduce adds (S > 1)
+__global__ void __launch_bounds__(256) k_openings_seg(OpeningsArgs a) {
+  __shared__ ext red[OPEN_PB][256];
+  const uint32_t n = 1u << a.log_n, T = blockDim.x, t = threadIdx.x;
+  const uint32_t g = blockIdx.x / a.S, slice = blockIdx.x % a.S, b = blockIdx.y;
+  uint32_t j = 0;
+  while (j + 1 < a.nseg && g >= a.seg[j + 1].g0) j++;
+  const OpenSeg sg = a.seg[j];
+  const uint32_t p0 = (g - sg.g0) * OPEN_PB;
+  const uint32_t np = min((uint32_t)OPEN_PB, sg.npolys - p0);
+  const uint32_t len = n / a.S, lo = slice * len;
+  const uint64_t *cf = sg.coeffs + b * sg.c_bstride + (uint64_t)p0 * n;
+  const ext z = ext{a.pts[b * CHAL_STRIDE + sg.pt_off], a.pts[b * CHAL_STRIDE + sg.pt_off + 1]};
+  ext zp = gl::ext_pow(z, lo + t);
+  const ext zs = gl::ext_pow(z, T);
+  ext acc[OPEN_PB];
+#pragma unroll
+  for (int q = 0; q < OPEN_PB; q++) acc[q] = ext{0, 0};
+  for (uint32_t k = lo + t; k < lo + len; k += T) {
+#pragma unroll
+    for (int q = 0; q < OPEN_PB; q++)
+      if ((uint32_t)q < np) acc[q] = gl::ext_add(acc[q], gl::ext_scale(zp, cf[(uint64_t)q * n + k]));
+    zp = gl::ext_mul(zp, zs);
+  }
+#pragma unroll
+  for (int q = 0; q < OPEN_PB; q++) red[q][t] = acc[q];
+  __syncthreads();
+  for (uint32_t o = T / 2; o; o >>= 1) {
+    if (t < o)
+      for (uint32_t q = 0; q < np; q++) red[q][t] = gl::ext_add(red[q][t], red[q][t + o]);
+    __syncthreads();
+  }
+  if (t < np) {
+    const uint32_t idx = sg.out_off + p0 + t;
+    uint64_t *dst = a.S == 1 ? a.out + b * OPEN_STRIDE + 2 * idx
+                             : a.part + ((uint64_t)(b * a.S + slice) * OPEN_STRIDE + 2 * idx);
+    dst[0] = red[t][0].c0;
+    dst[1] = red[t][0].c1;
+  }
+}
+
+__global__ void __launch_bounds__(256) k_openings_reduce(const uint64_t *__restrict__ part, uint64_t *__restrict__ out,
+                                                         uint32_t ntot, uint32_t S) {
+  const uint32_t idx = blockIdx.x * blockDim.x + threadIdx.x, b = blockIdx.y;
+  if (idx >= ntot) return;
+  ext acc{0, 0};
+  for (uint32_t sl = 0; sl < S; sl++) {
+    const uint64_t *p = part + (uint64_t)(b * S + sl) * OPEN_STRIDE + 2 * idx;
+    acc = gl::ext_add(acc, ext{p[0], p[1]});
+  }
+  out[b * OPEN_STRIDE + 2 * idx] = acc.c0;
+  out[b * OPEN_STRIDE + 2 * idx + 1] = acc.c1;
+}
+
+void openings(OpeningsArgs a, uint32_t nb, hipStream_t s) {
+  const uint32_t n = 1u << a.log_n;
+  const unsigned T = (unsigned)std::min<uint32_t>(256, std::max<uint32_t>(64, n / 4));
+  a.ngroups = 0;
+  a.ntot = 0;
+  for (uint32_t j = 0; j < a.nseg; j++) {
+    a.seg[j].g0 = a.ngroups;
+    a.ngroups += (a.seg[j].npolys + OPEN_PB - 1) / OPEN_PB;
+    a.ntot = std::max(a.ntot, a.seg[j].out_off + a.seg[j].npolys);
+  }
+  // QPGPU_OPEN_SLICES=1: one block per group (the former launches' shape)
+  const char *e = getenv("QPGPU_OPEN_SLICES");
+  const uint32_t smax = e && *e ? (uint32_t)atoi(e) : OPEN_MAX_SLICES;
+  a.S = 1;
+  while (a.S * 2 <= smax && a.S * 2 * T * 8 <= n && (uint64_t)a.ngroups * nb * a.S < 1024) a.S *= 2;
+  k_openings_seg<<<dim3(a.ngroups * a.S, nb), T, 0, s>>>(a);
+  if (a.S > 1) k_openings_reduce<<<dim3((a.ntot + 255) / 256, nb), 256, 0, s>>>(a.part, a.out, a.ntot, a.S);
+}
+
 // ---------------------------------------------------------------- a11
 
 // comp[k] = sum_j alpha^j c_j[k] over the listed oracles (Horner, reverse order)
@@ -1864,6 +1942,43 @@ __global__ void __launch_bounds__(256) k_fri_leaf(const uint64_t *__restrict__ v
     psd::permute_nc(s);
   }
   o[0] = psd::canon(s[0]); o[1] = psd::canon(s[1]); o[2] = psd::canon(s[2]); o[3] = psd::canon(s[3]);
+}
+
+// k_fri_leaf with one 16-lane row per leaf (pc::permute_row): a layer of few
+// leaves (small batches, the upper FRI layers) otherwise costs a one-lane
+// permutation's latency per absorbed chunk whatever its width
+__global__ void __launch_bounds__(256) k_fri_leaf_row(const uint64_t *__restrict__ vals, uint64_t *__restrict__ dig,
+                                                      uint32_t log_len, uint32_t ab, uint64_t v_bstride,
+                                                      uint64_t d_bstride) {
+  const uint32_t i = blockIdx.x * 16 + (threadIdx.x >> 4), l16 = threadIdx.x & 15;
+  if (i >= (1u << (log_len - ab))) return;
+  const uint32_t b = blockIdx.y;
+  const uint64_t L = 1ull << log_len;
+  const uint64_t *c0 = vals + b * v_bstride + ((uint64_t)i << ab);
+  const uint32_t W = 2u << ab;  // > 4 (the launcher sends arity 2 to k_fri_leaf)
+  uint64_t x = 0;
+  for (uint32_t off = 0; off < W; off += 8) {
+    const uint32_t e = off + l16;  // element e: c0/c1 of value e >> 1
+    if (l16 < 8 && e < W) x = (e & 1 ? c0 + L : c0)[e >> 1];
+    x = pc::permute_row(x);
+  }
+  if (l16 < 4) dig[b * d_bstride + (uint64_t)i * 4 + l16] = psd::canon(x);
+}
+
+// leaves of a FRI layer: the row form up to QP_FRI_ROW_MAX leaves over the
+// batch (QPGPU_FRI_ROW overrides, 0 = never), the one-lane form above
+#ifndef QP_FRI_ROW_MAX
+#define QP_FRI_ROW_MAX 16384
+#endif
+void fri_leaf(const uint64_t *vals, uint64_t *dig, uint32_t log_len, uint32_t ab, uint64_t v_bstride,
+              uint64_t d_bstride, uint32_t nb, hipStream_t s) {
+  const char *e = getenv("QPGPU_FRI_ROW");
+  const uint64_t lim = e && *e ? strtoull(e, nullptr, 10) : QP_FRI_ROW_MAX;
+  const uint64_t nl = 1ull << (log_len - ab);
+  if ((2u << ab) > 4 && nl * nb <= lim)
+    k_fri_leaf_row<<<dim3((unsigned)((nl + 15) / 16), nb), 256, 0, s>>>(vals, dig, log_len, ab, v_bstride, d_bstride);
+  else
+    k_fri_leaf<<<dim3((unsigned)((nl + 255) / 256), nb), 256, 0, s>>>(vals, dig, log_len, ab, v_bstride, d_bstride);
 }
 
 // fold: out[k] = sum_{i<2^ab} beta^i c[2^ab k + i]  (coefficients, ext as 2 columns).

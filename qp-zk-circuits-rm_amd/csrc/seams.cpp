@@ -303,8 +303,7 @@ int qp_fri_layer_commit(qp_ctx *ctx, const uint64_t *coeffs, uint32_t log_coeffs
   if (!e) {
     // values = coset_fft(coeffs, shift), leaf (bit-reversed) order
     qpk::lde(ctx->tw, d_c.p, Lc, L->d_vals, Lv, 2, lc, log_values - lc, shift, 1, 2 * Lc, 2 * Lv, s);
-    qpk::k_fri_leaf<<<dim3(cdiv(1ull << log_leaves, 256), 1), 256, 0, s>>>(L->d_vals, L->d_dig, log_values, arity_bits,
-                                                                           2 * Lv, dbs);
+    qpk::fri_leaf(L->d_vals, L->d_dig, log_values, arity_bits, 2 * Lv, dbs, 1, s);
     qpk::merkle_tree(L->d_dig, log_leaves, cap_height, 1, dbs, s);
     e = hipGetLastError();
   }

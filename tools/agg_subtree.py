@@ -67,6 +67,16 @@ def main():
         # this job OMP_NUM_THREADS cores)
         res.append({"seconds": time.perf_counter() - t,
                     "levels": [(n, round(s * 1e3, 1), round(c * 1e3, 1)) for n, s, c in levels]})
+    # per level circuit (insertion order = level order): degree, proofs per
+    # level prover batch and its device stage times per run
+    per_level = []
+    for lp in A._levels.values():
+        st = {}
+        for p in lp.provers:
+            for k, v in p.stage_times().items():
+                st[k] = round(st.get(k, 0.0) + v / reps, 2)
+        per_level.append({"degree_bits": lp.circuit.degree_bits, "npis": lp.circuit.num_public_inputs,
+                          "max_batch": lp.max_batch, "provers": len(lp.provers), "stage_ms": st})
     stages = {}
     for lp in A._levels.values():
         for p in lp.provers:
@@ -81,6 +91,7 @@ def main():
         cg = {"nr_throttled": th1[0] - th0[0], "throttled_ms": (th1[1] - th0[1]) / 1e3}
     print(json.dumps({"leaves": nl, "env": env, "warm_s": round(warm, 2), "runs": res, "cgroup_throttling": cg,
                       "stage_ms_per_run_all_provers": {k: round(v, 1) for k, v in stages.items()},
+                      "per_level": per_level,
                       "root_verified": olib().ora_verify(rvd, len(rvd), rp, len(rp)) == 0}), flush=True)
 
 

@@ -152,6 +152,18 @@ for s in "$@"; do
            step bench_coop 300 python -u bench.py --steps 10 --warmup 2 --cpu-sample 0 --configs3 0 --agg-leaves 0 &&
            step bench_nocoop 300 env QPGPU_MERKLE_COOP=0 python -u bench.py --steps 10 --warmup 2 --cpu-sample 0 --configs3 0 --agg-leaves 0 ;;
     leafub) step leaf_ubench 300 tools/leaf_ubench 86 5 ;;
+    lat5) step pytest_lat5 900 python -u -m pytest tests/test_gpu_reference_proof.py tests/test_gpu_prover.py tests/test_gpu_aggregation.py tests/test_gpu_seams.py tests/test_gpu_seam_prove.py -x -q --timeout 400 --timeout-method thread &&
+          step lat_new 300 python -u tools/agg_latency.py 1,2,4,8,16,32 5 &&
+          step lat_off 300 env QPGPU_MERKLE_ROW=0 QPGPU_FRI_ROW=0 QPGPU_OPEN_SLICES=1 QPGPU_LDE_FEW=0 python -u tools/agg_latency.py 1,2,4,8,16,32 5 &&
+          step lat_nomrow 300 env QPGPU_MERKLE_ROW=0 python -u tools/agg_latency.py 1,8,32 5 &&
+          step lat_nofri 300 env QPGPU_FRI_ROW=0 python -u tools/agg_latency.py 1,8,32 5 &&
+          step lat_noopen 300 env QPGPU_OPEN_SLICES=1 python -u tools/agg_latency.py 1,8,32 5 &&
+          step lat_nolde 300 env QPGPU_LDE_FEW=0 python -u tools/agg_latency.py 1,8,32 5 &&
+          step sub_new 300 python -u tools/agg_subtree.py 256 2 &&
+          step sub_off 300 env QPGPU_MERKLE_ROW=0 QPGPU_FRI_ROW=0 QPGPU_OPEN_SLICES=1 QPGPU_LDE_FEW=0 python -u tools/agg_subtree.py 256 2 &&
+          step sub_m8k 300 env QPGPU_MERKLE_COOP=8192 python -u tools/agg_subtree.py 256 2 &&
+          step sub_m32k 300 env QPGPU_MERKLE_COOP=32768 python -u tools/agg_subtree.py 256 2 &&
+          step bench_lat5 600 python -u bench.py --steps 5 --warmup 1 --cpu-sample 0 ;;
     leaft) step pytest_leaft 600 python -u -m pytest tests/test_gpu_commit.py tests/test_gpu_reference_proof.py tests/test_gpu_prover.py tests/test_gpu_voting.py -x -q --timeout 400 --timeout-method thread &&
            for r in 1 2; do
              step prof_leaft1_$r 300 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/prof_leaft1_$r -o run -- python3 tools/kbench.py 86 2 &&
