@@ -1043,6 +1043,10 @@ int gen_witness_batch(qp_prover *P, uint32_t nb) {
     return e ? (uint32_t)atoi(e) : 4u;
   }();
   a.coop_max = coop_per_wave * (wthreads / 64);
+  // QPGPU_WIT_ROW=0: cooperative Poseidons one per wave instead of one per
+  // 16-lane row (read per call)
+  const char *wr = getenv("QPGPU_WIT_ROW");
+  a.row = !(wr && wr[0] == '0');
   // QPGPU_WIT_MODE=levels|wg: a launch per dependency level over the whole
   // batch (default for the aggregation circuits: their 55 levels are mostly
   // one permutation deep, and one workgroup per proof leaves each level at a
@@ -1061,7 +1065,7 @@ int gen_witness_batch(qp_prover *P, uint32_t nb) {
     const auto &lp = P->circuit->cd.level_pos;
     for (uint32_t l = 0; l < P->wg_nlev; l++) {
       const uint32_t pcnt = lp[2 * l + 1], nother = lo[l + 1] - lo[l] - pcnt;
-      const uint32_t na = cdiv(nother, 256), npb = cdiv(pcnt, 4);
+      const uint32_t na = cdiv(nother, 256), npb = cdiv(pcnt, a.row ? 16 : 4);
       if (na + npb) qpk::k_witness_level<<<dim3(na + npb, nb), 256, 0, s>>>(a, l, na);
     }
   } else {

@@ -250,9 +250,17 @@ __device__ __noinline__ bool poseidon_witness(uint64_t *v, const uint32_t *__res
 // The dependent chain of a round is one S-box plus six products (the
 // one-lane form runs all 12 S-boxes and 12 MDS rows in sequence).  All 64
 // lanes must be active; lanes >= 12 compute and never write.
-using pc::wave_mds_row;
+// ROW: one generator per 16-lane row (pc::row_mds, four per wave; a row is
+// wholly active or inactive); else one per wave (pc::wave_mds_row, all 64
+// lanes active)
+template <bool ROW>
+__device__ __forceinline__ uint64_t coop_mds(uint64_t y, const uint32_t (&coef)[12]) {
+  if constexpr (ROW) return pc::row_mds(y, coef);
+  else return pc::wave_mds_row(y, coef);
+}
+template <bool ROW>
 __device__ __noinline__ bool poseidon_coop(uint64_t *v, const uint32_t *__restrict__ ws) {
-  const uint32_t lane = threadIdx.x & 63;
+  const uint32_t lane = threadIdx.x & (ROW ? 15 : 63);
   const bool act = lane < 12;
   const uint32_t i = act ? lane : 0;
   // MDS row i: coefficient of element j = CIRC[(j - i) mod 12] (+ 8 on the diagonal of row 0)
@@ -264,7 +272,11 @@ __device__ __noinline__ bool poseidon_coop(uint64_t *v, const uint32_t *__restri
   const uint64_t a = rd(v, ws[i], in_ok), b = rd(v, ws[partner], in_ok);
   const uint64_t swap = rd(v, ws[24], in_ok);
   uint32_t sl = ws[act ? 29 + i : 29];
-  if (!__all(in_ok)) return false;
+  if constexpr (ROW) {
+    if ((__ballot(!in_ok) >> (threadIdx.x & 48)) & 0xffffull) return false;  // this row's lanes
+  } else {
+    if (!__all(in_ok)) return false;
+  }
   if (act && i < 4) wput(v, ws[25 + i], gl::mul(swap, gl::sub(b, a)), ok);
   uint64_t x = swap == 1 && i < 8 ? b : a;
   x = pf::add_c(x, ps::RC_DEV[i]);
@@ -274,7 +286,7 @@ __device__ __noinline__ bool poseidon_coop(uint64_t *v, const uint32_t *__restri
     if (r && act) wput(v, sl, x, ok);
     sl = ws[act ? (r < 3 ? 29 + 12 * r + i : 65) : 29];
     const uint64_t rc = ps::RC_DEV[(r + 1) * 12 + i];
-    x = pf::add_c(wave_mds_row(pf::sbox(x), coef), rc);
+    x = pf::add_c(coop_mds<ROW>(pf::sbox(x), coef), rc);
   }
   // partial rounds 4..25: lane 0's S-box input is the wire
 #pragma unroll 1
@@ -283,7 +295,7 @@ __device__ __noinline__ bool poseidon_coop(uint64_t *v, const uint32_t *__restri
     sl = ws[lane == 0 ? (r < 25 ? 66 + (r - 4) : 87) : (act ? 87 + i : 87)];
     const uint64_t rc = ps::RC_DEV[(r + 1) * 12 + i];
     const uint64_t y = pf::sbox(x);
-    x = pf::add_c(wave_mds_row(lane == 0 ? y : x, coef), rc);
+    x = pf::add_c(coop_mds<ROW>(lane == 0 ? y : x, coef), rc);
   }
   if (act) sl = ws[87 + i];
   // rounds 26..29: the state entering each is written, then the output
@@ -291,7 +303,7 @@ __device__ __noinline__ bool poseidon_coop(uint64_t *v, const uint32_t *__restri
   for (int r = 26; r < 30; r++) {
     if (act) wput(v, sl, x, ok);
     sl = ws[act ? (r < 29 ? 87 + 12 * (r - 25) + i : 12 + i) : 12];
-    x = wave_mds_row(pf::sbox(x), coef);
+    x = coop_mds<ROW>(pf::sbox(x), coef);
     if (r < 29) x = pf::add_c(x, ps::RC_DEV[(r + 1) * 12 + i]);
   }
   if (act) wput(v, sl, x, ok);
@@ -540,12 +552,19 @@ __global__ void __launch_bounds__(512) k_witness_gen(const WitnessGenArgs a) {
         bad = i + 1;
       }
     }
-    if (coop)
-      for (uint32_t p = plo + wave; p < plo + pcnt; p += nwaves)  // wave-uniform: every lane active
-        if (!poseidon_coop(v, a.wslot + (uint64_t)gens[p].row * a.W) && ok) {
+    if (coop && a.row) {
+      for (uint32_t p = plo + (threadIdx.x >> 4); p < plo + pcnt; p += blockDim.x >> 4)  // row-uniform
+        if (!poseidon_coop<true>(v, a.wslot + (uint64_t)gens[p].row * a.W) && ok) {
           ok = false;
           bad = p + 1;
         }
+    } else if (coop) {
+      for (uint32_t p = plo + wave; p < plo + pcnt; p += nwaves)  // wave-uniform: every lane active
+        if (!poseidon_coop<false>(v, a.wslot + (uint64_t)gens[p].row * a.W) && ok) {
+          ok = false;
+          bad = p + 1;
+        }
+    }
     __syncthreads();
   }
   if (!ok) atomicCAS(a.err + b, 0u, bad);
@@ -554,7 +573,8 @@ __global__ void __launch_bounds__(512) k_witness_gen(const WitnessGenArgs a) {
 // one dependency level over the whole batch (the level-launch mode for small
 // batches: a launch per level instead of one workgroup per proof walking every
 // level): blocks [0, na) run the level's non-Poseidon generators one per lane,
-// blocks [na, ..) its Poseidon generators one per wave (poseidon_coop), so a
+// blocks [na, ..) its Poseidon generators one per row (poseidon_coop; one
+// per wave under QPGPU_WIT_ROW=0), so a
 // level costs one cooperative permutation's latency (≈25 us) rather than a
 // one-lane permutation's (≈65 us) or several cooperative ones in sequence.
 // Stream order separates the levels; the first failure per proof wins the CAS.
@@ -572,8 +592,13 @@ __global__ void __launch_bounds__(256) k_witness_level(const WitnessGenArgs a, u
       if (!run_gen(gens[i], v, a.wslot, a.W, a.limbs, a.zero_slot, a.num_consts)) bad = i + 1;
     }
   } else {
-    const uint32_t p = (blockIdx.x - na) * (blockDim.x >> 6) + (threadIdx.x >> 6);  // wave-uniform
-    if (p < pcnt && !poseidon_coop(v, a.wslot + (uint64_t)gens[plo + p].row * a.W)) bad = plo + p + 1;
+    if (a.row) {
+      const uint32_t p = (blockIdx.x - na) * (blockDim.x >> 4) + (threadIdx.x >> 4);  // row-uniform
+      if (p < pcnt && !poseidon_coop<true>(v, a.wslot + (uint64_t)gens[plo + p].row * a.W)) bad = plo + p + 1;
+    } else {
+      const uint32_t p = (blockIdx.x - na) * (blockDim.x >> 6) + (threadIdx.x >> 6);  // wave-uniform
+      if (p < pcnt && !poseidon_coop<false>(v, a.wslot + (uint64_t)gens[plo + p].row * a.W)) bad = plo + p + 1;
+    }
   }
   if (bad) atomicCAS(a.err + b, 0u, bad);
 }

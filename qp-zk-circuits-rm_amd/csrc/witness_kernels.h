@@ -12,7 +12,8 @@ struct WitnessGenArgs {
   const uint32_t *level_off;  // [nlevels + 1]
   const uint32_t *level_pos;  // [nlevels][2]: first Poseidon generator, count
   uint32_t nlevels;
-  uint32_t coop_max;          // levels with at most this many Poseidons run them one per wave
+  uint32_t coop_max;          // levels with at most this many Poseidons run them cooperatively
+  uint32_t row;               // cooperative Poseidons one per 16-lane row (else one per wave)
   const uint32_t *wslot;      // row-major wire -> slot map [n][W]
   uint32_t W, limbs, zero_slot, num_consts;
   uint32_t *err;              // [B]: 0 = ok, else 1 + index of the first failing generator

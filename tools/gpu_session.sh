@@ -152,6 +152,14 @@ for s in "$@"; do
            step bench_coop 300 python -u bench.py --steps 10 --warmup 2 --cpu-sample 0 --configs3 0 --agg-leaves 0 &&
            step bench_nocoop 300 env QPGPU_MERKLE_COOP=0 python -u bench.py --steps 10 --warmup 2 --cpu-sample 0 --configs3 0 --agg-leaves 0 ;;
     leafub) step leaf_ubench 300 tools/leaf_ubench 86 5 ;;
+    witrow) step pytest_witrow 900 python -u -m pytest tests/test_gpu_aggregation.py tests/test_gpu_witness.py tests/test_gpu_reference_proof.py -x -q --timeout 400 --timeout-method thread &&
+            step wr_lat_new 300 python -u tools/agg_latency.py 1,8,32 5 &&
+            step wr_lat_off 300 env QPGPU_WIT_ROW=0 python -u tools/agg_latency.py 1,8,32 5 &&
+            step wr_sub_new 300 python -u tools/agg_subtree.py 256 2 &&
+            step wr_sub_off 300 env QPGPU_WIT_ROW=0 python -u tools/agg_subtree.py 256 2 &&
+            step wr_sub_new2 300 python -u tools/agg_subtree.py 256 2 &&
+            step wr_bench 600 python -u bench.py --steps 5 --warmup 1 --cpu-sample 0 &&
+            step wr_bench_off 600 env QPGPU_WIT_ROW=0 python -u bench.py --steps 5 --warmup 1 --cpu-sample 0 --agg-leaves 0 --configs3 0 ;;
     lat5) step pytest_lat5 900 python -u -m pytest tests/test_gpu_reference_proof.py tests/test_gpu_prover.py tests/test_gpu_aggregation.py tests/test_gpu_seams.py tests/test_gpu_seam_prove.py -x -q --timeout 400 --timeout-method thread &&
           step lat_new 300 python -u tools/agg_latency.py 1,2,4,8,16,32 5 &&
           step lat_off 300 env QPGPU_MERKLE_ROW=0 QPGPU_FRI_ROW=0 QPGPU_OPEN_SLICES=1 QPGPU_LDE_FEW=0 python -u tools/agg_latency.py 1,2,4,8,16,32 5 &&
