@@ -77,12 +77,11 @@ class _LevelProver:
     and workspace, so one prover's host phases (transcript, query assembly)
     overlap the other's kernels, as the leaf bench's provers do."""
 
-    def __init__(self, inner_common: bytes, branching: int, device: int, max_batch: int):
+    def __init__(self, inner_common: bytes, branching: int, device: int, max_batch: int, nprov: int = 0):
         self.circuit = aggregation_circuit(inner_common, branching)
         self.max_batch = max_batch
-        nprov = max(1, int(os.environ.get("QP_AGG_PROVERS", "2")))
-        if max_batch == 1:
-            nprov = 1
+        if not nprov:
+            nprov = _agg_provers() if max_batch > 1 else 1
         # QP_AGG_PRIORITY=1: the level provers' streams at the greatest priority,
         # so their latency-bound launches dispatch ahead of concurrent leaf kernels
         high = os.environ.get("QP_AGG_PRIORITY", "0") not in ("", "0")
@@ -100,9 +99,12 @@ class _LevelProver:
         common = self.circuit.common_data()
         assert vd.endswith(common)
         self.data = CircuitData(common, vd[:len(vd) - len(common)])
-        self.lock = threading.Lock()
+        self.lock = threading.Lock()  # the host-witness path's
+        self.locks = [threading.Lock() for _ in self.provers]
 
-    def prove_chunks(self, chunks, inner_vo: bytes) -> List[AggregatedProof]:
+    def prove_chunks(self, chunks, inner_vo: bytes, prover: Optional[int] = None) -> List[AggregatedProof]:
+        """Every chunk aggregated: split evenly over the provers, or all on
+        provers[prover] (a sub-tree's thread, see aggregate_to_tree)."""
         if os.environ.get("QP_AGG_WITNESS", "device") == "host":
             return self._prove_chunks_host(chunks, inner_vo)
         # device witness generation (qp_prover_prove_aggregation): the host only
@@ -110,32 +112,37 @@ class _LevelProver:
         # chunks are split evenly over the provers, each proving its share in
         # batches of max_batch on its own stream
         npis = self.circuit.num_public_inputs
-        np_ = min(len(self.provers), len(chunks))
-        per = [len(chunks) // np_ + (1 if i < len(chunks) % np_ else 0) for i in range(np_)]
-        first = [sum(per[:i]) for i in range(np_)]
-        outs = [None] * np_
+        if prover is not None:
+            sel = [prover % len(self.provers)]
+            per, first = [len(chunks)], [0]
+        else:
+            sel = list(range(min(len(self.provers), len(chunks))))
+            per = [len(chunks) // len(sel) + (1 if i < len(chunks) % len(sel) else 0) for i in range(len(sel))]
+            first = [sum(per[:i]) for i in range(len(sel))]
+        outs = [None] * len(sel)
         errors = []
 
-        def run(i):
+        def run(j):
+            i = sel[j]
             try:
                 res = []
-                mine = chunks[first[i]:first[i] + per[i]]
-                for k in range(0, len(mine), self.max_batch):
-                    grp = mine[k:k + self.max_batch]
-                    res += self.provers[i].prove_aggregation(inner_vo, [[p.to_bytes() for p in ch] for ch in grp])
-                outs[i] = res
+                mine = chunks[first[j]:first[j] + per[j]]
+                with self.locks[i]:
+                    for k in range(0, len(mine), self.max_batch):
+                        grp = mine[k:k + self.max_batch]
+                        res += self.provers[i].prove_aggregation(inner_vo, [[p.to_bytes() for p in ch] for ch in grp])
+                outs[j] = res
             except BaseException as e:  # re-raised on the calling thread
                 errors.append(e)
 
-        with self.lock:
-            if np_ == 1:
-                run(0)
-            else:
-                th = [threading.Thread(target=run, args=(i,)) for i in range(np_)]
-                for t in th:
-                    t.start()
-                for t in th:
-                    t.join()
+        if len(sel) == 1:
+            run(0)
+        else:
+            th = [threading.Thread(target=run, args=(j,)) for j in range(len(sel))]
+            for t in th:
+                t.start()
+            for t in th:
+                t.join()
         if errors:
             raise errors[0]
         out = []
@@ -207,12 +214,22 @@ _levels = {}
 _levels_lock = threading.Lock()
 
 
-def _level_prover(inner_common: bytes, branching: int, device: int, max_batch: int) -> _LevelProver:
+def _agg_provers() -> int:
+    """Device provers per aggregation level (QP_AGG_PROVERS, default 2)."""
+    return max(1, int(os.environ.get("QP_AGG_PROVERS", "2")))
+
+
+def _level_prover(inner_common: bytes, branching: int, device: int, max_batch: int,
+                  nprov: int = 0) -> _LevelProver:
+    """The cached level prover of (inner circuit, branching, device), rebuilt when
+    a call needs a larger batch or more provers than it has (nprov 0: the
+    default count)."""
     key = (bytes(inner_common), branching, device)
     with _levels_lock:
         lp = _levels.get(key)
-        if lp is None or lp.max_batch < max_batch:
-            lp = _LevelProver(inner_common, branching, device, max(max_batch, lp.max_batch if lp else 0))
+        if lp is None or lp.max_batch < max_batch or len(lp.provers) < nprov:
+            lp = _LevelProver(inner_common, branching, device, max(max_batch, lp.max_batch if lp else 0),
+                              max(nprov, len(lp.provers) if lp else 0))
             _levels[key] = lp
         return lp
 
@@ -229,11 +246,12 @@ def aggregate_chunk(chunk, common_data: bytes, verifier_only: bytes, device: int
 
 
 def aggregate_level(proofs, common_data: bytes, verifier_only: bytes, config: TreeAggregationConfig,
-                    device: int = 0, backend=None) -> List[AggregatedProof]:
+                    device: int = 0, backend=None, prover: Optional[int] = None) -> List[AggregatedProof]:
     """tree.rs:80-103: chunks of `tree_branching_factor` proofs, each aggregated
     (all chunks of the level proven as one GPU batch).  backend(inner_common,
     branching, device, max_batch) -> an object with .data and .prove_chunks()
-    (default: the GPU level prover; tests inject a CPU one)."""
+    (default: the GPU level prover; tests inject a CPU one).  prover: the level
+    prover's device prover that takes every chunk (a sub-tree's thread)."""
     k = config.tree_branching_factor
     proofs = [_as_proof(p) for p in proofs]
     if not proofs or k < 1:
@@ -244,14 +262,21 @@ def aggregate_level(proofs, common_data: bytes, verifier_only: bytes, config: Tr
     # if it is alone, as in the reference, whose next level uses proofs[0]'s
     # circuit data for every proof)
     tail = chunks.pop() if len(chunks[-1]) != k else None
-    make = backend or _level_prover
     out = []
+    if backend is not None:
+        if chunks:
+            out = backend(common_data, k, device, max(1, min(len(chunks), 32))).prove_chunks(chunks, verifier_only)
+        if tail is not None:
+            out += backend(common_data, len(tail), device, 1).prove_chunks([tail], verifier_only)
+        return out
+    nprov = max(prover + 1, _agg_provers()) if prover is not None else 0
     if chunks:
         # up to 32 aggregation proofs per GPU batch (2.7 vs 3.2 ms per proof at 16;
         # tools/agg_bench.py, profiles/r03_agg_bench.log)
-        out = make(common_data, k, device, max(1, min(len(chunks), 32))).prove_chunks(chunks, verifier_only)
+        out = _level_prover(common_data, k, device, max(1, min(len(chunks), 32)), nprov).prove_chunks(
+            chunks, verifier_only, prover)
     if tail is not None:
-        out += make(common_data, len(tail), device, 1).prove_chunks([tail], verifier_only)
+        out += _level_prover(common_data, len(tail), device, 1, nprov).prove_chunks([tail], verifier_only, prover)
     return out
 
 
@@ -291,16 +316,75 @@ def aggregate_to_tree(leaf_proofs, common_data: bytes, verifier_only: bytes,
     db = check(common_data, leaf_proofs)
     if db is not None:
         raise CircuitTooLarge(f"level-1 aggregation circuit is 2^{db} rows", [])
-    proofs = aggregate_level(leaf_proofs, common_data, verifier_only, config, device, backend)
-    while len(proofs) > 1:
-        cd = proofs[0].circuit_data
-        db = check(cd.common, proofs)
-        if db is not None:
-            raise CircuitTooLarge(f"the next level's aggregation circuit is 2^{db} rows (its public inputs: every "
-                                  f"leaf's); the GPU prover proves up to 2^{GPU_MAX_DEGREE_BITS}", proofs)
-        proofs = aggregate_level([p.proof for p in proofs], cd.common, cd.verifier_only, config, device, backend)
+
+    def levels(proofs, prover=None):
+        """Levels down to one proof; returns (proofs, None) or (the last level
+        proven, the message of the circuit that was too large)."""
+        while len(proofs) > 1:
+            cd = proofs[0].circuit_data
+            db = check(cd.common, proofs)
+            if db is not None:
+                return proofs, (f"the next level's aggregation circuit is 2^{db} rows (its public inputs: every "
+                                f"leaf's); the GPU prover proves up to 2^{GPU_MAX_DEGREE_BITS}")
+            proofs = aggregate_level([p.proof for p in proofs], cd.common, cd.verifier_only, config, device,
+                                     backend, prover)
+        return proofs, None
+
+    parts = _subtree_parts(len(leaf_proofs), config.tree_branching_factor) if backend is None else 1
+    if parts > 1:
+        # independent sub-trees (consecutive leaf ranges of k^m leaves, the
+        # same chunks as the level-by-level order), one thread and one device
+        # prover each: no level barrier between them, so one sub-tree's host
+        # phases and latency-bound launches overlap the other's kernels
+        m = len(leaf_proofs) // parts
+        res = [None] * parts
+        errors = []
+
+        def run(i):
+            try:
+                lv = aggregate_level(leaf_proofs[i * m:(i + 1) * m], common_data, verifier_only, config, device,
+                                     backend, i)
+                res[i] = levels(lv, i)
+            except BaseException as e:  # re-raised on the calling thread
+                errors.append(e)
+
+        th = [threading.Thread(target=run, args=(i,)) for i in range(parts)]
+        for t in th:
+            t.start()
+        for t in th:
+            t.join()
+        if errors:
+            raise errors[0]
+        msg = next((r[1] for r in res if r[1]), None)
+        proofs = [p for r in res for p in r[0]]
+        if msg:
+            raise CircuitTooLarge(msg, proofs)
+    else:
+        proofs = aggregate_level(leaf_proofs, common_data, verifier_only, config, device, backend)
+    proofs, msg = levels(proofs)
+    if msg:
+        raise CircuitTooLarge(msg, proofs)
     assert len(proofs) == 1
     return proofs[0]
+
+
+SUBTREE_MIN_LEAVES = 32
+
+
+def _subtree_parts(n: int, k: int) -> int:
+    """Sub-trees aggregate_to_tree proves concurrently: QP_AGG_SPLIT (default
+    4) when n leaves split into that many complete k-ary sub-trees of at least
+    SUBTREE_MIN_LEAVES leaves each, else 1.  256-leaf subtree: 0.376 s level
+    by level, 0.378 s as 2 sub-trees, 0.343-0.359 s as 4, 0.37-0.38 s as 8; a
+    tree of 8 leaves as 4 sub-trees of 2: 35 ms against 28 level by level
+    (profiles/r05_ab_subtree_split.log)."""
+    s = int(os.environ.get("QP_AGG_SPLIT") or 4)
+    if s < 2 or k < 2 or n % s or n // s < max(k, SUBTREE_MIN_LEAVES):
+        return 1
+    m = n // s
+    while m % k == 0:
+        m //= k
+    return s if m == 1 else 1
 
 
 def pad_with_dummy_proofs(proofs, proof_len: int, dummy_proof) -> list:

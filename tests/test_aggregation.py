@@ -222,3 +222,18 @@ def test_too_large_level_is_refused_before_proving(ref):
     with pytest.raises(CircuitTooLarge, match="2\\^16") as e:
         qp_wormhole.aggregate_to_tree([leaves[0]] * 9, cb, vo, TreeAggregationConfig.new(10, 1))
     assert e.value.proofs == []
+
+
+def test_subtree_parts(monkeypatch):
+    """aggregate_to_tree proves QP_AGG_SPLIT (default 4) complete k-ary
+    sub-trees concurrently, only when the leaves split into that many of at
+    least SUBTREE_MIN_LEAVES (32) leaves each."""
+    from qp_wormhole.aggregator import _subtree_parts
+    monkeypatch.delenv("QP_AGG_SPLIT", raising=False)
+    monkeypatch.delenv("QP_AGG_PROVERS", raising=False)
+    assert _subtree_parts(256, 2) == 4 and _subtree_parts(128, 2) == 4 and _subtree_parts(8, 2) == 1
+    assert _subtree_parts(192, 2) == 1 and _subtree_parts(324, 3) == 4 and _subtree_parts(81, 3) == 1
+    monkeypatch.setenv("QP_AGG_SPLIT", "2")
+    assert _subtree_parts(256, 2) == 2 and _subtree_parts(32, 2) == 1 and _subtree_parts(162, 3) == 2
+    monkeypatch.setenv("QP_AGG_SPLIT", "1")
+    assert _subtree_parts(256, 2) == 1

@@ -160,6 +160,18 @@ for s in "$@"; do
             step wr_sub_new2 300 python -u tools/agg_subtree.py 256 2 &&
             step wr_bench 600 python -u bench.py --steps 5 --warmup 1 --cpu-sample 0 &&
             step wr_bench_off 600 env QPGPU_WIT_ROW=0 python -u bench.py --steps 5 --warmup 1 --cpu-sample 0 --agg-leaves 0 --configs3 0 ;;
+    agg32prof) step prof_agg32 300 rocprofv3 --kernel-trace --output-format csv -d gpurun_out/prof_agg32 -o run -- python3 tools/agg_latency.py 32 3 ;;
+    split) step pytest_split 900 python -u -m pytest tests/test_gpu_aggregation.py tests/test_distributed.py -x -q --timeout 400 --timeout-method thread &&
+           step sp_sub_2 300 python -u tools/agg_subtree.py 256 3 &&
+           step sp_sub_1 300 env QP_AGG_SPLIT=1 python -u tools/agg_subtree.py 256 3 &&
+           step sp_sub_4 300 env QP_AGG_SPLIT=4 QP_AGG_PROVERS=4 python -u tools/agg_subtree.py 256 3 &&
+           step sp_sub_4p2 300 env QP_AGG_SPLIT=4 python -u tools/agg_subtree.py 256 3 &&
+           step sp_bench 600 python -u bench.py --steps 5 --warmup 1 --cpu-sample 0 ;;
+    split4) step pytest_split4 900 python -u -m pytest tests/test_gpu_aggregation.py -x -q --timeout 400 --timeout-method thread &&
+           step sp4_sub 300 python -u tools/agg_subtree.py 256 3 &&
+           step sp4_sub_8 300 env QP_AGG_SPLIT=8 python -u tools/agg_subtree.py 256 3 &&
+           step sp4_sub_4p3 300 env QP_AGG_PROVERS=3 python -u tools/agg_subtree.py 256 3 &&
+           step sp4_bench 600 python -u bench.py --steps 5 --warmup 1 --cpu-sample 0 ;;
     lat5) step pytest_lat5 900 python -u -m pytest tests/test_gpu_reference_proof.py tests/test_gpu_prover.py tests/test_gpu_aggregation.py tests/test_gpu_seams.py tests/test_gpu_seam_prove.py -x -q --timeout 400 --timeout-method thread &&
           step lat_new 300 python -u tools/agg_latency.py 1,2,4,8,16,32 5 &&
           step lat_off 300 env QPGPU_MERKLE_ROW=0 QPGPU_FRI_ROW=0 QPGPU_OPEN_SLICES=1 QPGPU_LDE_FEW=0 python -u tools/agg_latency.py 1,2,4,8,16,32 5 &&
