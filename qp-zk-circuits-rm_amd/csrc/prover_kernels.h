@@ -78,6 +78,9 @@ __global__ void k_quotient_1r(QuotientArgs a);
 __global__ void k_quotient_fused(QuotientArgs a);
 template <int PART>
 __global__ void k_quotient_part(QuotientArgs a, uint32_t gi, uint32_t last);
+// the gates of gmask (Poseidon, recursion gates) one after another per point, one launch
+template <bool POS>
+__global__ void k_quotient_rest(QuotientArgs a, uint32_t gmask, uint32_t last);
 // the permutation terms + the gates of gmask that read routed wires only, one pass
 template <int QDF>
 __global__ void k_quotient_prefix(QuotientArgs a, uint32_t gmask, uint32_t last);

@@ -1356,6 +1356,72 @@ __global__ void __launch_bounds__(256) k_quotient_part(QuotientArgs a, uint32_t 
     q[N + t] = acc1;
   }
 }
+// ---- k_quotient_rest: every gate of gmask (the ones k_quotient_prefix does
+// not take: Poseidon, Reducing(Extension), RandomAccess, CosetInterpolation,
+// PoseidonMds) in one launch, gate after gate per point with both accumulators
+// in registers, instead of one k_quotient_part launch per gate streaming the
+// accumulators through HBM and each gate's columns from HBM again: a point's
+// columns are re-read within microseconds, while the points in flight (≈64k
+// x 1 KB) fit the 256 MB MALL.  Same alpha indices and filters as the part
+// launches: bit-identical.
+#ifndef QP_QREST_WAVES
+#define QP_QREST_WAVES 4
+#endif
+template <bool POS>
+__global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(QP_QREST_WAVES)))
+k_quotient_rest(QuotientArgs a, uint32_t gmask, uint32_t last) {
+  const uint32_t logN = a.log_n + a.rate_bits;
+  const uint64_t N = 1ull << logN;
+  const uint32_t t = blockIdx.x * blockDim.x + threadIdx.x;
+  if (t >= N) return;
+  const uint32_t b = blockIdx.y;
+  const uint64_t *cs = a.cs_lde + t;
+  const uint64_t *wl = a.w_lde + b * a.w_bstride + t;
+  uint64_t *q = a.q_out + b * a.q_bstride;
+  TermAcc A;
+  A.p0 = a.apow + (uint64_t)b * 2 * APOW_STRIDE;
+  A.p1 = A.p0 + APOW_STRIDE;
+  const uint32_t R = a.R, qdf = a.qdf, nchunks = (R + qdf - 1) / qdf;
+  const uint32_t nsel = a.g.nsel;
+  const uint64_t *gc = cs + (uint64_t)nsel * N;
+  uint64_t acc0 = q[t], acc1 = q[N + t];
+#pragma unroll 1
+  for (uint32_t gi = 0; gi < a.g.ngates; gi++) {
+    if (!((gmask >> gi) & 1)) continue;
+    const uint32_t kind = a.g.kind[gi];
+    const uint32_t si = a.g.sel_index[gi];
+    const uint64_t sv = cs[(uint64_t)si * N];
+    uint64_t f = 1;
+    for (uint32_t jj = a.g.grp_lo[si]; jj < a.g.grp_hi[si]; jj++)
+      if (jj != gi) f = gfn::mul(f, gfn::sub(jj, sv));
+    if (nsel > 1) f = gfn::mul(f, gfn::sub(0xFFFFFFFFull, sv));
+    A.s0 = A.s1 = 0;
+    A.i = 2 * (1 + nchunks);
+    // opaque per iteration: keeps the column addresses of every gate from
+    // being hoisted out of the loop into registers (324 B of spill otherwise)
+    const uint64_t *wli = wl, *gci = gc;
+    asm volatile("" : "+v"(wli), "+v"(gci));
+    if (POS && kind == GK_POSEIDON)
+      poseidon_gate(wli, N, A);
+    else
+      recursion_gate_body(kind, a.g.param[gi], a.g.param2[gi], a.g.param3[gi], wli, gci, N, A);
+    acc0 = gfn::add(acc0, gfn::mul(f, A.s0));
+    acc1 = gfn::add(acc1, gfn::mul(f, A.s1));
+  }
+  if (last) {
+    const uint32_t j = gl::rev_bits(t, logN);
+    const uint64_t zh_inv = a.zh_inv[j & ((1u << a.rate_bits) - 1)];
+    q[t] = gfn::canon(gfn::mul(acc0, zh_inv));
+    q[N + t] = gfn::canon(gfn::mul(acc1, zh_inv));
+  } else {
+    q[t] = acc0;
+    q[N + t] = acc1;
+  }
+}
+
+template __global__ void k_quotient_rest<false>(QuotientArgs, uint32_t, uint32_t);
+template __global__ void k_quotient_rest<true>(QuotientArgs, uint32_t, uint32_t);
+
 // ---- k_quotient_prefix: the permutation terms and every gate of gmask that
 // reads routed wires only (Constant, PublicInput, BaseSum, Arithmetic,
 // ArithmeticExtension, MulExtension) in ONE pass over windows of QP_WIN routed
@@ -1652,16 +1718,42 @@ void quotient_values(const QuotientArgs &a, QuotientKernel k, uint32_t nb, hipSt
           }
           if (wires <= a.R) gmask |= 1u << gi;
         }
+      // QPGPU_QREST=1: the recursion gates in one k_quotient_rest launch after
+      // the others (=2: the Poseidon gate too).  Off by default: per 32-proof
+      // level-1 batch 2.18 ms against 2.05 for their five part launches (2: 3.77
+      // against 1.34 + 2.05), subtree unchanged -- these launches are
+      // instruction-bound, not re-read-bound (profiles/r05_ab_quotient_rest.log)
+      uint32_t rmask = 0;
+      const char *rv = getenv("QPGPU_QREST");
+      const int rmode = rv && *rv ? rv[0] - '0' : 0;
+      if (rmode)
+        for (uint32_t gi = 0; gi < a.g.ngates; gi++) {
+          if ((gmask >> gi) & 1) continue;
+          switch (a.g.kind[gi]) {
+            case GK_POSEIDON:
+              if (rmode == 2) rmask |= 1u << gi;
+              break;
+            case GK_ARITH_EXT: case GK_MUL_EXT: case GK_REDUCING: case GK_REDUCING_EXT:
+            case GK_EXPONENTIATION: case GK_POSEIDON_MDS: case GK_RANDOM_ACCESS: case GK_COSET_INTERP:
+              rmask |= 1u << gi;
+              break;
+            default: break;
+          }
+        }
       int lastg = -1;
       for (uint32_t gi = 0; gi < a.g.ngates; gi++)
-        if (a.g.kind[gi] != GK_NOOP && !((gmask >> gi) & 1)) lastg = (int)gi;
-      if (gmask) k_quotient_prefix<8><<<qg, 256, 0, s>>>(a, gmask, lastg < 0);
-      else k_quotient_part<0><<<qg, 256, 0, s>>>(a, 0, lastg < 0);
+        if (a.g.kind[gi] != GK_NOOP && !(((gmask | rmask) >> gi) & 1)) lastg = (int)gi;
+      const bool rest_last = rmask != 0;
+      if (gmask) k_quotient_prefix<8><<<qg, 256, 0, s>>>(a, gmask, lastg < 0 && !rest_last);
+      else k_quotient_part<0><<<qg, 256, 0, s>>>(a, 0, lastg < 0 && !rest_last);
       for (uint32_t gi = 0; gi < a.g.ngates; gi++) {
-        if (a.g.kind[gi] == GK_NOOP || ((gmask >> gi) & 1)) continue;
-        if (a.g.kind[gi] == GK_POSEIDON) k_quotient_part<2><<<qg, 256, 0, s>>>(a, gi, (int)gi == lastg);
-        else k_quotient_part<1><<<qg, 256, 0, s>>>(a, gi, (int)gi == lastg);
+        if (a.g.kind[gi] == GK_NOOP || (((gmask | rmask) >> gi) & 1)) continue;
+        const uint32_t l = (int)gi == lastg && !rest_last;
+        if (a.g.kind[gi] == GK_POSEIDON) k_quotient_part<2><<<qg, 256, 0, s>>>(a, gi, l);
+        else k_quotient_part<1><<<qg, 256, 0, s>>>(a, gi, l);
       }
+      if (rmask && rmode == 2) k_quotient_rest<true><<<qg, 256, 0, s>>>(a, rmask, 1);
+      else if (rmask) k_quotient_rest<false><<<qg, 256, 0, s>>>(a, rmask, 1);
       break;
     }
     case QK_ONEPASS: k_quotient<2><<<qg, 256, 0, s>>>(a); break;

@@ -172,6 +172,16 @@ for s in "$@"; do
            step sp4_sub_8 300 env QP_AGG_SPLIT=8 python -u tools/agg_subtree.py 256 3 &&
            step sp4_sub_4p3 300 env QP_AGG_PROVERS=3 python -u tools/agg_subtree.py 256 3 &&
            step sp4_bench 600 python -u bench.py --steps 5 --warmup 1 --cpu-sample 0 ;;
+    qrest) step pytest_qrest 900 python -u -m pytest tests/test_gpu_aggregation.py tests/test_gpu_seams.py tests/test_gpu_seam_prove.py -x -q --timeout 400 --timeout-method thread &&
+           step qr_lat_1 300 python -u tools/agg_latency.py 1,8,32 5 &&
+           step qr_lat_0 300 env QPGPU_QREST=0 python -u tools/agg_latency.py 1,8,32 5 &&
+           step qr_lat_2 300 env QPGPU_QREST=2 python -u tools/agg_latency.py 1,8,32 5 &&
+           step qr_sub_1 300 python -u tools/agg_subtree.py 256 3 &&
+           step qr_sub_0 300 env QPGPU_QREST=0 python -u tools/agg_subtree.py 256 3 &&
+           step qr_sub_2 300 env QPGPU_QREST=2 python -u tools/agg_subtree.py 256 3 &&
+           step prof_qr1 300 rocprofv3 --kernel-trace --output-format csv -d gpurun_out/prof_qr1 -o run -- python3 tools/agg_latency.py 32 3 &&
+           step prof_qr2 300 env QPGPU_QREST=2 rocprofv3 --kernel-trace --output-format csv -d gpurun_out/prof_qr2 -o run -- python3 tools/agg_latency.py 32 3 &&
+           step prof_qr0 300 env QPGPU_QREST=0 rocprofv3 --kernel-trace --output-format csv -d gpurun_out/prof_qr0 -o run -- python3 tools/agg_latency.py 32 3 ;;
     lat5) step pytest_lat5 900 python -u -m pytest tests/test_gpu_reference_proof.py tests/test_gpu_prover.py tests/test_gpu_aggregation.py tests/test_gpu_seams.py tests/test_gpu_seam_prove.py -x -q --timeout 400 --timeout-method thread &&
           step lat_new 300 python -u tools/agg_latency.py 1,2,4,8,16,32 5 &&
           step lat_off 300 env QPGPU_MERKLE_ROW=0 QPGPU_FRI_ROW=0 QPGPU_OPEN_SLICES=1 QPGPU_LDE_FEW=0 python -u tools/agg_latency.py 1,2,4,8,16,32 5 &&
