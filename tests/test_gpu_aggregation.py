@@ -298,3 +298,23 @@ def test_high_priority_context_proves_the_same_bytes(reference_leaves):
         res.append(p.prove_aggregation(vo, [leaves])[0])
         p.free()
     assert res[0] == res[1]
+
+
+@pytest.mark.parametrize("split", ["2", "4"])
+def test_concurrent_subtrees_prove_the_same_root(reference_leaves, monkeypatch, split):
+    """aggregate_to_tree's concurrent sub-trees (QP_AGG_SPLIT) take the same
+    chunks as the level-by-level order: the same root bytes over 128 leaves,
+    and the root verifies."""
+    import qp_wormhole
+    from qp_wormhole.aggregator import TreeAggregationConfig
+    cb, vo, leaves = reference_leaves
+    ls = [leaves[(i * 7 + i // 5) % 2] for i in range(128)]
+    roots = []
+    for s in ("1", split):
+        monkeypatch.setenv("QP_AGG_SPLIT", s)
+        roots.append(qp_wormhole.aggregate_to_tree(ls, cb, vo, TreeAggregationConfig.new(2, 7)))
+    assert roots[0].proof.to_bytes() == roots[1].proof.to_bytes()
+    assert roots[0].circuit_data.verifier_only == roots[1].circuit_data.verifier_only
+    vd = roots[1].circuit_data.verifier_data()
+    pb = roots[1].proof.to_bytes()
+    assert olib().ora_verify(vd, len(vd), pb, len(pb)) == 0

@@ -182,6 +182,19 @@ for s in "$@"; do
            step prof_qr1 300 rocprofv3 --kernel-trace --output-format csv -d gpurun_out/prof_qr1 -o run -- python3 tools/agg_latency.py 32 3 &&
            step prof_qr2 300 env QPGPU_QREST=2 rocprofv3 --kernel-trace --output-format csv -d gpurun_out/prof_qr2 -o run -- python3 tools/agg_latency.py 32 3 &&
            step prof_qr0 300 env QPGPU_QREST=0 rocprofv3 --kernel-trace --output-format csv -d gpurun_out/prof_qr0 -o run -- python3 tools/agg_latency.py 32 3 ;;
+    splitab) for r in 1 2; do
+             step sab_def_$r 300 python -u tools/agg_subtree.py 256 2 &&
+             step sab_m8k_$r 300 env QPGPU_MERKLE_COOP=8192 python -u tools/agg_subtree.py 256 2 &&
+             step sab_m2k_$r 300 env QPGPU_MERKLE_COOP=2048 python -u tools/agg_subtree.py 256 2 &&
+             step sab_wg_$r 300 env QPGPU_WIT_MODE=wg python -u tools/agg_subtree.py 256 2 &&
+             step sab_fri2k_$r 300 env QPGPU_FRI_ROW=2048 python -u tools/agg_subtree.py 256 2 &&
+             step sab_lde0_$r 300 env QPGPU_LDE_FEW=0 python -u tools/agg_subtree.py 256 2 &&
+             step sab_open1_$r 300 env QPGPU_OPEN_SLICES=1 python -u tools/agg_subtree.py 256 2 || exit 1
+             done ;;
+    qrestpmc) for m in 0 1 2; do
+             step pmc_qr${m}_fetch 300 env QPGPU_QREST=$m rocprofv3 --pmc FETCH_SIZE --kernel-include-regex k_quotient --output-format csv -d gpurun_out/pmc_qr${m}_fetch -o run -- python3 tools/agg_latency.py 32 2 &&
+             step pmc_qr${m}_write 300 env QPGPU_QREST=$m rocprofv3 --pmc WRITE_SIZE --kernel-include-regex k_quotient --output-format csv -d gpurun_out/pmc_qr${m}_write -o run -- python3 tools/agg_latency.py 32 2 || exit 1
+             done ;;
     lat5) step pytest_lat5 900 python -u -m pytest tests/test_gpu_reference_proof.py tests/test_gpu_prover.py tests/test_gpu_aggregation.py tests/test_gpu_seams.py tests/test_gpu_seam_prove.py -x -q --timeout 400 --timeout-method thread &&
           step lat_new 300 python -u tools/agg_latency.py 1,2,4,8,16,32 5 &&
           step lat_off 300 env QPGPU_MERKLE_ROW=0 QPGPU_FRI_ROW=0 QPGPU_OPEN_SLICES=1 QPGPU_LDE_FEW=0 python -u tools/agg_latency.py 1,2,4,8,16,32 5 &&
