@@ -1898,7 +1898,7 @@ void openings(OpeningsArgs a, uint32_t nb, hipStream_t s) {
   }
   // QPGPU_OPEN_SLICES=1: one block per group (the former launches' shape)
   const char *e = getenv("QPGPU_OPEN_SLICES");
-  const uint32_t smax = e && *e ? (uint32_t)atoi(e) : OPEN_MAX_SLICES;
+  const uint32_t smax = e && *e ? std::min<uint32_t>((uint32_t)atoi(e), OPEN_MAX_SLICES) : OPEN_MAX_SLICES;
   a.S = 1;
   while (a.S * 2 <= smax && a.S * 2 * T * 8 <= n && (uint64_t)a.ngroups * nb * a.S < 1024) a.S *= 2;
   k_openings_seg<<<dim3(a.ngroups * a.S, nb), T, 0, s>>>(a);
