@@ -195,6 +195,24 @@ for s in "$@"; do
              step pmc_qr${m}_fetch 300 env QPGPU_QREST=$m rocprofv3 --pmc FETCH_SIZE --kernel-include-regex k_quotient --output-format csv -d gpurun_out/pmc_qr${m}_fetch -o run -- python3 tools/agg_latency.py 32 2 &&
              step pmc_qr${m}_write 300 env QPGPU_QREST=$m rocprofv3 --pmc WRITE_SIZE --kernel-include-regex k_quotient --output-format csv -d gpurun_out/pmc_qr${m}_write -o run -- python3 tools/agg_latency.py 32 2 || exit 1
              done ;;
+    provab) for r in 1 2; do
+             step pv3_$r 300 python -u bench.py --steps 10 --warmup 1 --cpu-sample 0 --agg-leaves 0 --configs3 0 &&
+             step pv4_$r 300 python -u bench.py --steps 10 --warmup 1 --cpu-sample 0 --agg-leaves 0 --configs3 0 --provers 4 &&
+             step pv2_$r 300 python -u bench.py --steps 10 --warmup 1 --cpu-sample 0 --agg-leaves 0 --configs3 0 --provers 2 || exit 1
+             done ;;
+    final5) step pytest_gpu 900 python -u -m pytest tests -m gpu -x -v --timeout 400 --timeout-method thread &&
+            step smoke 300 python -c "import __graft_entry__ as g; g.smoke()" &&
+            step bench 900 python -u bench.py &&
+            step rocprof_bench 900 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/prof_bench -o run -- python3 bench.py --steps 2 --warmup 1 --cpu-sample 0 &&
+            step rocprof_bench1 600 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/prof_bench1 -o run -- python3 bench.py --steps 2 --warmup 1 --cpu-sample 0 --provers 1 &&
+            pmc fetch FETCH_SIZE && pmc write WRITE_SIZE &&
+            pmc sq SQ_WAVES SQ_INSTS_VALU SQ_ACTIVE_INST_VALU SQ_WAVE_CYCLES SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_BUSY_CYCLES SQ_WAIT_ANY &&
+            step pmc_calib 600 bash tools/pmc_calib.sh &&
+            step prof_agg 300 env QP_AGG_PROVERS=1 QP_AGG_SPLIT=1 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/prof_agg -o run -- python3 tools/agg_subtree.py 256 1 &&
+            step leaf_ubench 300 tools/leaf_ubench 86 5 &&
+            step agg_subtree 300 python -u tools/agg_subtree.py 256 3 &&
+            step bench_voting 600 python -u bench.py --circuit voting &&
+            step final_summaries 300 bash tools/final_summaries.sh r05 ;;
     lat5) step pytest_lat5 900 python -u -m pytest tests/test_gpu_reference_proof.py tests/test_gpu_prover.py tests/test_gpu_aggregation.py tests/test_gpu_seams.py tests/test_gpu_seam_prove.py -x -q --timeout 400 --timeout-method thread &&
           step lat_new 300 python -u tools/agg_latency.py 1,2,4,8,16,32 5 &&
           step lat_off 300 env QPGPU_MERKLE_ROW=0 QPGPU_FRI_ROW=0 QPGPU_OPEN_SLICES=1 QPGPU_LDE_FEW=0 python -u tools/agg_latency.py 1,2,4,8,16,32 5 &&
