@@ -167,9 +167,11 @@ def parse():
     ap.add_argument("--warmup", type=int, default=1)
     ap.add_argument("--batch", type=int, default=0,
                     help="proofs per GPU per step (default: 256 Wormhole, 1024 voting)")
-    ap.add_argument("--provers", type=int, default=3,
+    ap.add_argument("--provers", type=int, default=0,
                     help="concurrent provers per GPU (own HIP stream + host thread each, B/provers proofs each): "
-                         "one prover's host transcript phases overlap the other's kernels")
+                         "one prover's host transcript phases overlap the other's kernels; 0 = the measured best "
+                         "per circuit: 3 for Wormhole (2: same, 4: -3 %%), 6 for voting (3: 9.4-10.8 k, 4: "
+                         "11.9-12.1 k, 6: 12.4-13.0 k, 8: 12.0-12.5 k proofs/s; profiles/r05_ab_provers.log)")
     ap.add_argument("--circuit", choices=["wormhole", "voting"], default="wormhole",
                     help="wormhole = BASELINE configs[2] (the headline); voting = configs[4]")
     ap.add_argument("--mode", choices=["e2e", "wires-dev"], default="e2e",
@@ -444,7 +446,7 @@ def main():
     circuit = qp_wormhole.Circuit.voting() if voting else qp_wormhole.Circuit.wormhole(zero_knowledge=False)
     B = args.batch or (1024 if voting else 256)
     inputs = make_inputs(circuit, rank * B, B)
-    NP = max(1, min(args.provers, B))
+    NP = max(1, min(args.provers or (6 if args.circuit == "voting" else 3), B))
     per = [B // NP + (1 if i < B % NP else 0) for i in range(NP)]
     first = [sum(per[:i]) for i in range(NP)]
     provers = [qp_wormhole.Prover(qp_wormhole.Context(local), circuit, max_batch=per[i]) for i in range(NP)]

@@ -842,8 +842,17 @@ int prove_batch(qp_prover *P, const uint64_t *d_wires, const uint64_t *const *wi
     // next proof once theirs has a hit below the claimed block
     const uint64_t limit = 1ull << std::min<uint32_t>(P->pow_bits + 20, 62);
     TRY(hipMemsetAsync(P->pow_next.p, 0, (size_t)nb * 8, s));
-    qpk::k_pow_scan<<<2048, 256, 0, s>>>(P->pow_state.p, (const uint32_t *)P->pow_pos.p, P->pow_found.p,
-                                         P->pow_next.p, nb, P->pow_bits, limit);
+    // QPGPU_POW_WAVE=1: per-wave claims of 64 candidates (k_pow_scan_w; A/B:
+    // voting 10.8-11.1 k vs 12.9-13.4 k proofs/s with workgroup claims, the
+    // leaf bench unchanged -- four times the atomics on each proof's counter;
+    // profiles/r05_ab_pow_wave.log)
+    const char *pw = getenv("QPGPU_POW_WAVE");
+    if (!(pw && pw[0] == '1'))
+      qpk::k_pow_scan<<<2048, 256, 0, s>>>(P->pow_state.p, (const uint32_t *)P->pow_pos.p, P->pow_found.p,
+                                           P->pow_next.p, nb, P->pow_bits, limit);
+    else
+      qpk::k_pow_scan_w<<<2048, 256, 0, s>>>(P->pow_state.p, (const uint32_t *)P->pow_pos.p, P->pow_found.p,
+                                             P->pow_next.p, nb, P->pow_bits, limit);
     TRY(hipGetLastError());
     TRY(hipMemcpyAsync(P->h_found.data(), P->pow_found.p, (size_t)nb * 8, hipMemcpyDeviceToHost, s));
     TRY(hipStreamSynchronize(s));

@@ -2152,6 +2152,37 @@ __global__ void __launch_bounds__(256) k_pow_scan(const uint64_t *__restrict__ s
   }
 }
 
+// k_pow_scan with per-wave claims: lane 0 of each wave takes the next 64-candidate
+// chunk of its proof (a vector atomic, broadcast with readfirstlane), so no
+// workgroup barrier stands between a claim and the permutations; waves start
+// spread over the proofs and move on as k_pow_scan's workgroups do.  Same
+// minimal witness (every candidate below the first hit is tested).
+__global__ void __launch_bounds__(256) k_pow_scan_w(const uint64_t *__restrict__ states,
+                                                    const uint32_t *__restrict__ pos, uint64_t *__restrict__ found,
+                                                    uint64_t *__restrict__ next, uint32_t nb, uint32_t bits,
+                                                    uint64_t limit) {
+  const uint32_t lane = threadIdx.x & 63;
+  const uint32_t wave = blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6);
+  for (uint32_t i = 0; i < nb; i++) {
+    const uint32_t b = (wave + i) % nb;
+    const uint64_t *pre = states + b * 24;
+    for (;;) {
+      uint64_t k = 0, f = 0;
+      if (lane == 0) {
+        k = atomicAdd((unsigned long long *)(next + b), 1ull);
+        f = *(const volatile uint64_t *)(found + b);
+      }
+      k = ((uint64_t)__builtin_amdgcn_readfirstlane((uint32_t)(k >> 32)) << 32) |
+          __builtin_amdgcn_readfirstlane((uint32_t)k);
+      f = ((uint64_t)__builtin_amdgcn_readfirstlane((uint32_t)(f >> 32)) << 32) |
+          __builtin_amdgcn_readfirstlane((uint32_t)f);
+      if (k * 64 >= limit || k * 64 >= f) break;  // wave-uniform
+      const uint64_t cand = k * 64 + lane;
+      if (pow_hit(pre, pos[b], cand, bits)) atomicMin((unsigned long long *)(found + b), (unsigned long long)cand);
+    }
+  }
+}
+
 __global__ void __launch_bounds__(256) k_pow(const uint64_t *__restrict__ states, const uint32_t *__restrict__ pos,
                                              const uint32_t *__restrict__ active, uint64_t *__restrict__ found,
                                              uint64_t base, uint32_t bits) {

@@ -213,6 +213,26 @@ for s in "$@"; do
             step agg_subtree 300 python -u tools/agg_subtree.py 256 3 &&
             step bench_voting 600 python -u bench.py --circuit voting &&
             step final_summaries 300 bash tools/final_summaries.sh r05 ;;
+    votab) step vot_def 600 python -u bench.py --circuit voting --agg-leaves 0 --configs3 0 &&
+           step vot_split 600 python -u bench.py --circuit voting --agg-leaves 0 --configs3 0 --host-threads -1 &&
+           step vot_p2 600 python -u bench.py --circuit voting --agg-leaves 0 --configs3 0 --provers 2 &&
+           step vot_p4 600 python -u bench.py --circuit voting --agg-leaves 0 --configs3 0 --provers 4 &&
+           step vot_prof 600 rocprofv3 --kernel-trace --output-format csv -d gpurun_out/prof_vot -o run -- python3 bench.py --circuit voting --steps 3 --warmup 1 --cpu-sample 0 --agg-leaves 0 --configs3 0 &&
+           step vot_sum 120 python3 tools/kernel_summary.py gpurun_out/prof_vot/run_kernel_trace.csv gpurun_out/vot_ksum.json "voting bench, 3 provers" &&
+           rm -rf gpurun_out/prof_vot ;;
+    votab2) for r in 1 2; do
+           step vot3_$r 600 python -u bench.py --circuit voting --agg-leaves 0 --configs3 0 &&
+           step vot4_$r 600 python -u bench.py --circuit voting --agg-leaves 0 --configs3 0 --provers 4 &&
+           step vot6_$r 600 python -u bench.py --circuit voting --agg-leaves 0 --configs3 0 --provers 6 &&
+           step vot8_$r 600 python -u bench.py --circuit voting --agg-leaves 0 --configs3 0 --provers 8 || exit 1
+           done ;;
+    powab) step pytest_pow 600 python -u -m pytest tests/test_gpu_reference_proof.py tests/test_gpu_prover.py tests/test_gpu_voting.py -x -q --timeout 300 --timeout-method thread &&
+           for r in 1 2; do
+           step pw1_$r 300 python -u bench.py --steps 10 --warmup 1 --cpu-sample 0 --agg-leaves 0 --configs3 0 &&
+           step pw0_$r 300 env QPGPU_POW_WAVE=0 python -u bench.py --steps 10 --warmup 1 --cpu-sample 0 --agg-leaves 0 --configs3 0 &&
+           step vw1_$r 300 python -u bench.py --circuit voting --agg-leaves 0 --configs3 0 &&
+           step vw0_$r 300 env QPGPU_POW_WAVE=0 python -u bench.py --circuit voting --agg-leaves 0 --configs3 0 || exit 1
+           done ;;
     lat5) step pytest_lat5 900 python -u -m pytest tests/test_gpu_reference_proof.py tests/test_gpu_prover.py tests/test_gpu_aggregation.py tests/test_gpu_seams.py tests/test_gpu_seam_prove.py -x -q --timeout 400 --timeout-method thread &&
           step lat_new 300 python -u tools/agg_latency.py 1,2,4,8,16,32 5 &&
           step lat_off 300 env QPGPU_MERKLE_ROW=0 QPGPU_FRI_ROW=0 QPGPU_OPEN_SLICES=1 QPGPU_LDE_FEW=0 python -u tools/agg_latency.py 1,2,4,8,16,32 5 &&
