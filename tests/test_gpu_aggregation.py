@@ -261,7 +261,7 @@ def test_device_witness_zk_aggregation(reference_leaves):
                                  {"QPGPU_QPREFIX": "0"}, {"QPGPU_LEAF_T": "0"}, {"QPGPU_MERKLE_ROW": "0"},
                                  {"QPGPU_FRI_ROW": "0"}, {"QPGPU_OPEN_SLICES": "1"}, {"QPGPU_LDE_FEW": "0"},
                                  {"QPGPU_WIT_ROW": "0"}, {"QPGPU_WIT_ROW": "0", "QPGPU_WIT_MODE": "wg"},
-                                 {"QPGPU_QREST": "1"}, {"QPGPU_QREST": "2"}])
+                                 {"QPGPU_QREST": "1"}, {"QPGPU_QREST": "2"}, {"QPGPU_POW_WAVE": "1"}])
 def test_latency_paths_prove_the_same_bytes(reference_leaves, monkeypatch, env):
     """The small-batch paths (device witness one launch per dependency level or
     one workgroup per proof, cooperative Merkle levels in the row or wave form,
