@@ -847,10 +847,21 @@ int prove_batch(qp_prover *P, const uint64_t *d_wires, const uint64_t *const *wi
     // leaf bench unchanged -- four times the atomics on each proof's counter;
     // profiles/r05_ab_pow_wave.log)
     const char *pw = getenv("QPGPU_POW_WAVE");
-    if (!(pw && pw[0] == '1'))
-      qpk::k_pow_scan<<<2048, 256, 0, s>>>(P->pow_state.p, (const uint32_t *)P->pow_pos.p, P->pow_found.p,
-                                           P->pow_next.p, nb, P->pow_bits, limit);
-    else
+    // QPGPU_POW_CPT=1/2/4: candidates per thread per claimed block (A/B: no
+    // change, profiles/r05_ab_pow_cpt.log)
+    const char *pc = getenv("QPGPU_POW_CPT");
+    const int cpt = pc && *pc ? atoi(pc) : 1;
+    if (!(pw && pw[0] == '1')) {
+      if (cpt == 4)
+        qpk::k_pow_scan<4><<<2048, 256, 0, s>>>(P->pow_state.p, (const uint32_t *)P->pow_pos.p, P->pow_found.p,
+                                                P->pow_next.p, nb, P->pow_bits, limit);
+      else if (cpt == 2)
+        qpk::k_pow_scan<2><<<2048, 256, 0, s>>>(P->pow_state.p, (const uint32_t *)P->pow_pos.p, P->pow_found.p,
+                                                P->pow_next.p, nb, P->pow_bits, limit);
+      else
+        qpk::k_pow_scan<1><<<2048, 256, 0, s>>>(P->pow_state.p, (const uint32_t *)P->pow_pos.p, P->pow_found.p,
+                                                P->pow_next.p, nb, P->pow_bits, limit);
+    } else
       qpk::k_pow_scan_w<<<2048, 256, 0, s>>>(P->pow_state.p, (const uint32_t *)P->pow_pos.p, P->pow_found.p,
                                              P->pow_next.p, nb, P->pow_bits, limit);
     TRY(hipGetLastError());

@@ -143,6 +143,7 @@ __global__ void k_fold(const uint64_t *cin, uint64_t *cout, uint32_t log_len, ui
                        const uint64_t *chal, uint64_t i_bstride, uint64_t o_bstride, uint32_t log_nz);
 __global__ void k_pow_scan_w(const uint64_t *states, const uint32_t *pos, uint64_t *found, uint64_t *next, uint32_t nb,
                              uint32_t bits, uint64_t limit);
+template <int CPT>
 __global__ void k_pow_scan(const uint64_t *states, const uint32_t *pos, uint64_t *found, uint64_t *next, uint32_t nb,
                            uint32_t bits, uint64_t limit);
 __global__ void k_pow(const uint64_t *states, const uint32_t *pos, const uint32_t *active, uint64_t *found, uint64_t base,

@@ -2127,9 +2127,12 @@ __device__ __forceinline__ bool pow_hit(const uint64_t *__restrict__ pre, uint32
   return (psd::canon(s[7]) >> (64 - bits)) == 0;
 }
 
+// CPT candidates per thread per claimed block (blocks of 256 CPT candidates)
+template <int CPT>
 __global__ void __launch_bounds__(256) k_pow_scan(const uint64_t *__restrict__ states, const uint32_t *__restrict__ pos,
                                                   uint64_t *__restrict__ found, uint64_t *__restrict__ next, uint32_t nb,
                                                   uint32_t bits, uint64_t limit) {
+  constexpr uint64_t BLK = 256ull * CPT;
   __shared__ uint64_t blk;
   __shared__ uint32_t done;
   for (uint32_t i = 0; i < nb; i++) {
@@ -2139,18 +2142,27 @@ __global__ void __launch_bounds__(256) k_pow_scan(const uint64_t *__restrict__ s
       if (threadIdx.x == 0) {
         const uint64_t k = atomicAdd((unsigned long long *)(next + b), 1ull);
         blk = k;
-        done = k * 256 >= limit || k * 256 >= *(const volatile uint64_t *)(found + b);
+        done = k * BLK >= limit || k * BLK >= *(const volatile uint64_t *)(found + b);
       }
       __syncthreads();
       const uint64_t k = blk;
       const uint32_t d = done;
       __syncthreads();  // every lane has read blk / done before lane 0 rewrites them
       if (d) break;
-      const uint64_t cand = k * 256 + threadIdx.x;
-      if (pow_hit(pre, pos[b], cand, bits)) atomicMin((unsigned long long *)(found + b), (unsigned long long)cand);
+#pragma unroll 1
+      for (int j = 0; j < CPT; j++) {
+        const uint64_t cand = k * BLK + 256ull * j + threadIdx.x;
+        if (pow_hit(pre, pos[b], cand, bits)) atomicMin((unsigned long long *)(found + b), (unsigned long long)cand);
+      }
     }
   }
 }
+template __global__ void k_pow_scan<1>(const uint64_t *, const uint32_t *, uint64_t *, uint64_t *, uint32_t, uint32_t,
+                                       uint64_t);
+template __global__ void k_pow_scan<2>(const uint64_t *, const uint32_t *, uint64_t *, uint64_t *, uint32_t, uint32_t,
+                                       uint64_t);
+template __global__ void k_pow_scan<4>(const uint64_t *, const uint32_t *, uint64_t *, uint64_t *, uint32_t, uint32_t,
+                                       uint64_t);
 
 // k_pow_scan with per-wave claims: lane 0 of each wave takes the next 64-candidate
 // chunk of its proof (a vector atomic, broadcast with readfirstlane), so no

@@ -407,7 +407,7 @@ int qp_pow_grind(qp_ctx *ctx, const uint64_t *states, const uint32_t *pos, uint3
     QP_HIP_TRY(ctx, hipMemsetAsync(d_next.p, 0, n * 8ull, s));
     // the prover's single-launch minimal-witness search (prover.cpp stage 6)
     const uint64_t limit = 1ull << std::min<uint32_t>(pow_bits + 20, 62);
-    qpk::k_pow_scan<<<2048, 256, 0, s>>>(d_pre.p, (const uint32_t *)d_pos.p, d_found.p, d_next.p, n, pow_bits, limit);
+    qpk::k_pow_scan<1><<<2048, 256, 0, s>>>(d_pre.p, (const uint32_t *)d_pos.p, d_found.p, d_next.p, n, pow_bits, limit);
     QP_HIP_TRY(ctx, hipGetLastError());
     QP_HIP_TRY(ctx, hipMemcpyAsync(found.data(), d_found.p, n * 8ull, hipMemcpyDeviceToHost, s));
     QP_HIP_TRY(ctx, hipStreamSynchronize(s));
