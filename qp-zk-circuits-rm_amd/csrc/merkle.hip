@@ -293,9 +293,12 @@ void merkle_tree_from(uint64_t *digests, uint32_t log_N, uint32_t cap_h, uint32_
   const uint32_t K = log_N - cap_h;  // levels above the leaves
   const bool row = merkle_row();
   const uint64_t coop_max = merkle_coop_max(row);
+  // QPGPU_MERKLE_NBAT: the batch size up to which the cooperative forms apply
+  const char *nbe = getenv("QPGPU_MERKLE_NBAT");
+  const uint32_t coop_nbat = nbe && *nbe ? (uint32_t)strtoul(nbe, nullptr, 10) : (uint32_t)QP_MERKLE_COOP_NBAT;
   for (uint32_t k0 = first_level; k0 <= K;) {
     const uint32_t lc = log_N - k0;  // log2(nodes at level k0)
-    if (nbat <= QP_MERKLE_COOP_NBAT && ((uint64_t)nbat << lc) <= coop_max) {
+    if (nbat <= coop_nbat && ((uint64_t)nbat << lc) <= coop_max) {
       if (row)
         k_merkle_level_row<<<dim3(((1u << lc) + 15) / 16, nbat), 256, 0, s>>>(digests, log_N, k0, d_bstride);
       else
