@@ -243,6 +243,11 @@ for s in "$@"; do
            step nb128_$r 300 env QPGPU_MERKLE_NBAT=128 python -u bench.py --steps 10 --warmup 1 --cpu-sample 0 --agg-leaves 0 --configs3 0 &&
            step nb128c8_$r 300 env QPGPU_MERKLE_NBAT=128 QPGPU_MERKLE_COOP=12000 python -u bench.py --steps 10 --warmup 1 --cpu-sample 0 --agg-leaves 0 --configs3 0 || exit 1
            done ;;
+    witab3) for r in 1 2; do
+             step w3_def_$r 300 python -u tools/agg_subtree.py 256 2 &&
+             step w3_lev_$r 300 env QPGPU_WIT_MODE=levels python -u tools/agg_subtree.py 256 2 &&
+             step w3_t256_$r 300 env QPGPU_WIT_THREADS=256 python -u tools/agg_subtree.py 256 2 || exit 1
+             done ;;
     lat5) step pytest_lat5 900 python -u -m pytest tests/test_gpu_reference_proof.py tests/test_gpu_prover.py tests/test_gpu_aggregation.py tests/test_gpu_seams.py tests/test_gpu_seam_prove.py -x -q --timeout 400 --timeout-method thread &&
           step lat_new 300 python -u tools/agg_latency.py 1,2,4,8,16,32 5 &&
           step lat_off 300 env QPGPU_MERKLE_ROW=0 QPGPU_FRI_ROW=0 QPGPU_OPEN_SLICES=1 QPGPU_LDE_FEW=0 python -u tools/agg_latency.py 1,2,4,8,16,32 5 &&
