@@ -210,6 +210,11 @@ __global__ void __launch_bounds__(512) QP_NTT_OCC k_lde(const uint64_t *__restri
 #ifndef QP_LDE_ALDS
 #define QP_LDE_ALDS 3
 #endif
+// QP_LDE_WAVELOCAL=1: the n = 2^13 coset LDE's last two passes wave-local
+// (two workgroup barriers per coset instead of four)
+#ifndef QP_LDE_WAVELOCAL
+#define QP_LDE_WAVELOCAL 1
+#endif
 // MODE (QPGPU_LDE_MODE): 0 = MTW (default; measured 548 vs 701 us per
 // 64-column launch for mode 1 at n = 2^13, profiles/r04_lde_ab.log), 1 =
 // factored with both tables re-read per coset, 2 = factored with the coset
@@ -299,6 +304,60 @@ __global__ void __launch_bounds__(1 << LOG_T) QP_NTT_OCC k_lde_cosets(const uint
 #pragma unroll
     for (int m = 0; m < 16; m++) lds[nt::lp(t) + nt::lp(T * m)] = r[m];
     __syncthreads();
+    if constexpr (QP_LDE_WAVELOCAL && LOG_N == 13 && LOG_T == 9) {
+      // n = 2^13, T = 512: after the cross-wave pass (stride-32 groups of each
+      // 512-element block) wave w holds elements [1024 w, 1024 w + 1024), so the
+      // stride-2 pass and the last radix-2 level run on the wave's own LDS
+      // words: in-order LDS within a wave, no workgroup barrier between them
+      const uint32_t lane = t & 63, w = t >> 6;
+      {
+        const uint32_t sp = t >> 5, tt = t & 31;  // n / 16 == T groups: one per thread
+        uint64_t *base = lds + nt::lp((sp << 9) + tt);
+        uint64_t q[16];
+#pragma unroll
+        for (int m = 0; m < 16; m++) q[m] = base[nt::lp(m * 32)];
+        nt::dft16<false>(q);
+        if (tt) {
+          const uint64_t *ptS = pt + pt_offset(9) + tt;
+          nt::mul_rows<QP_LDE_MULK>(q, [&](int m) { return ptS[m * 32]; });
+        }
+#pragma unroll
+        for (int m = 0; m < 16; m++) base[nt::lp(m * 32)] = q[m];
+      }
+      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+      __builtin_amdgcn_wave_barrier();
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+      {
+        // the stride-2 pass (twiddles w_32^{tt brev4(m)}: shifts) on the wave's 32
+        // blocks of 32, lanes 0..31 the even halves, 32..63 the odd ones
+        const uint32_t b32 = 32 * w + (lane & 31), tt = lane >> 5;
+        uint64_t *base = lds + nt::lp((b32 << 5) + tt);
+        uint64_t q[16];
+#pragma unroll
+        for (int m = 0; m < 16; m++) q[m] = base[nt::lp(2 * m)];
+        nt::dft16<false>(q);
+        if (tt) {
+#pragma unroll
+          for (int m = 1; m < 16; m++) q[m] = nt::mul_w32<false>(q[m], (int)nt::brev4(m));
+        }
+#pragma unroll
+        for (int m = 0; m < 16; m++) base[nt::lp(2 * m)] = q[m];
+      }
+      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+      __builtin_amdgcn_wave_barrier();
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+      uint64_t *dst = dst0 + ((uint64_t)gl::rev_bits(s, rate_bits) << LOG_N);
+#pragma unroll
+      for (uint32_t k = 0; k < 8; k++) {
+        const uint32_t g0 = 1024 * w + 2 * (lane + 64 * k);
+        uint64_t q[2] = {lds[nt::lp(g0)], lds[nt::lp(g0 + 1)]};
+        nt::tail_group<false, 1>(q);
+        dst[g0] = nt::canon(q[0]);
+        dst[g0 + 1] = nt::canon(q[1]);
+      }
+      __syncthreads();
+      continue;
+    }
     // the last radix-2^g levels (g = LOG_N mod 4) run in the store loop: each
     // thread takes 16 / 2^g groups of 2^g contiguous values, transforms them in
     // registers and stores them contiguously (leaf order = DIF order)

@@ -248,6 +248,19 @@ for s in "$@"; do
              step w3_lev_$r 300 env QPGPU_WIT_MODE=levels python -u tools/agg_subtree.py 256 2 &&
              step w3_t256_$r 300 env QPGPU_WIT_THREADS=256 python -u tools/agg_subtree.py 256 2 || exit 1
              done ;;
+    wlab) step pytest_wl 900 python -u -m pytest tests/test_gpu_commit.py tests/test_gpu_reference_proof.py tests/test_gpu_prover.py tests/test_gpu_seams.py -x -q --timeout 400 --timeout-method thread &&
+          for r in 1 2; do
+          step wl_kb1_$r 300 python -u tools/kbench.py 16 5 &&
+          step wl_kb0_$r 300 env QPGPU_LIB=ab_libs/libqpgpu_wl0.so python -u tools/kbench.py 16 5 &&
+          step wl_b1_$r 300 python -u bench.py --steps 10 --warmup 1 --cpu-sample 0 --agg-leaves 0 --configs3 0 &&
+          step wl_b0_$r 300 env QPGPU_LIB=ab_libs/libqpgpu_wl0.so python -u bench.py --steps 10 --warmup 1 --cpu-sample 0 --agg-leaves 0 --configs3 0 || exit 1
+          done ;;
+    wlprof) for r in 1 2; do
+          step wlp1_$r 300 rocprofv3 --kernel-trace --output-format csv -d gpurun_out/wlp1_$r -o run -- python3 tools/kbench.py 32 5 &&
+          step wlp0_$r 300 env QPGPU_LIB=ab_libs/libqpgpu_wl0.so rocprofv3 --kernel-trace --output-format csv -d gpurun_out/wlp0_$r -o run -- python3 tools/kbench.py 32 5 || exit 1
+          done &&
+          step wlsq1 300 rocprofv3 --pmc SQ_WAVES SQ_INSTS_VALU SQ_ACTIVE_INST_VALU SQ_WAVE_CYCLES SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_BUSY_CYCLES SQ_WAIT_ANY --kernel-include-regex k_lde_cosets --output-format csv -d gpurun_out/wlsq1 -o run -- python3 tools/kbench.py 32 2 &&
+          step wlsq0 300 env QPGPU_LIB=ab_libs/libqpgpu_wl0.so rocprofv3 --pmc SQ_WAVES SQ_INSTS_VALU SQ_ACTIVE_INST_VALU SQ_WAVE_CYCLES SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_BUSY_CYCLES SQ_WAIT_ANY --kernel-include-regex k_lde_cosets --output-format csv -d gpurun_out/wlsq0 -o run -- python3 tools/kbench.py 32 2 ;;
     lat5) step pytest_lat5 900 python -u -m pytest tests/test_gpu_reference_proof.py tests/test_gpu_prover.py tests/test_gpu_aggregation.py tests/test_gpu_seams.py tests/test_gpu_seam_prove.py -x -q --timeout 400 --timeout-method thread &&
           step lat_new 300 python -u tools/agg_latency.py 1,2,4,8,16,32 5 &&
           step lat_off 300 env QPGPU_MERKLE_ROW=0 QPGPU_FRI_ROW=0 QPGPU_OPEN_SLICES=1 QPGPU_LDE_FEW=0 python -u tools/agg_latency.py 1,2,4,8,16,32 5 &&
