@@ -215,6 +215,11 @@ __global__ void __launch_bounds__(512) QP_NTT_OCC k_lde(const uint64_t *__restri
 #ifndef QP_LDE_WAVELOCAL
 #define QP_LDE_WAVELOCAL 1
 #endif
+// QP_LDE_EARLY_SYNC=1 (wave-local form): the coset's closing barrier moved
+// after the next coset's register work
+#ifndef QP_LDE_EARLY_SYNC
+#define QP_LDE_EARLY_SYNC 1
+#endif
 // MODE (QPGPU_LDE_MODE): 0 = MTW (default; measured 548 vs 701 us per
 // 64-column launch for mode 1 at n = 2^13, profiles/r04_lde_ab.log), 1 =
 // factored with both tables re-read per coset, 2 = factored with the coset
@@ -301,6 +306,12 @@ __global__ void __launch_bounds__(1 << LOG_T) QP_NTT_OCC k_lde_cosets(const uint
           nt::mul_rows<QP_LDE_MULK>(r, [&](int m) { return p1[T * m]; });
       }
     }
+    // wave-local tail: the barrier that keeps this coset's writes from
+    // overtaking other waves' reads of the previous coset's words sits here,
+    // after this wave's registers are ready, so a wave that finished its
+    // stores early transforms the next coset's 16 values instead of idling
+    if constexpr (QP_LDE_WAVELOCAL && QP_LDE_EARLY_SYNC && LOG_N == 13 && LOG_T == 9)
+      if (s) __syncthreads();
 #pragma unroll
     for (int m = 0; m < 16; m++) lds[nt::lp(t) + nt::lp(T * m)] = r[m];
     __syncthreads();
@@ -355,7 +366,7 @@ __global__ void __launch_bounds__(1 << LOG_T) QP_NTT_OCC k_lde_cosets(const uint
         dst[g0] = nt::canon(q[0]);
         dst[g0 + 1] = nt::canon(q[1]);
       }
-      __syncthreads();
+      if constexpr (!QP_LDE_EARLY_SYNC) __syncthreads();
       continue;
     }
     // the last radix-2^g levels (g = LOG_N mod 4) run in the store loop: each

@@ -261,6 +261,12 @@ for s in "$@"; do
           done &&
           step wlsq1 300 rocprofv3 --pmc SQ_WAVES SQ_INSTS_VALU SQ_ACTIVE_INST_VALU SQ_WAVE_CYCLES SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_BUSY_CYCLES SQ_WAIT_ANY --kernel-include-regex k_lde_cosets --output-format csv -d gpurun_out/wlsq1 -o run -- python3 tools/kbench.py 32 2 &&
           step wlsq0 300 env QPGPU_LIB=ab_libs/libqpgpu_wl0.so rocprofv3 --pmc SQ_WAVES SQ_INSTS_VALU SQ_ACTIVE_INST_VALU SQ_WAVE_CYCLES SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_BUSY_CYCLES SQ_WAIT_ANY --kernel-include-regex k_lde_cosets --output-format csv -d gpurun_out/wlsq0 -o run -- python3 tools/kbench.py 32 2 ;;
+    esprof) step pytest_es 900 python -u -m pytest tests/test_gpu_commit.py tests/test_gpu_reference_proof.py tests/test_gpu_prover.py tests/test_gpu_seams.py -x -q --timeout 400 --timeout-method thread &&
+          for r in 1 2; do
+          step esp1_$r 300 rocprofv3 --kernel-trace --output-format csv -d gpurun_out/esp1_$r -o run -- python3 tools/kbench.py 32 5 &&
+          step esp0_$r 300 env QPGPU_LIB=ab_libs/libqpgpu_es0.so rocprofv3 --kernel-trace --output-format csv -d gpurun_out/esp0_$r -o run -- python3 tools/kbench.py 32 5 &&
+          step espw_$r 300 env QPGPU_LIB=ab_libs/libqpgpu_wl0.so rocprofv3 --kernel-trace --output-format csv -d gpurun_out/espw_$r -o run -- python3 tools/kbench.py 32 5 || exit 1
+          done ;;
     lat5) step pytest_lat5 900 python -u -m pytest tests/test_gpu_reference_proof.py tests/test_gpu_prover.py tests/test_gpu_aggregation.py tests/test_gpu_seams.py tests/test_gpu_seam_prove.py -x -q --timeout 400 --timeout-method thread &&
           step lat_new 300 python -u tools/agg_latency.py 1,2,4,8,16,32 5 &&
           step lat_off 300 env QPGPU_MERKLE_ROW=0 QPGPU_FRI_ROW=0 QPGPU_OPEN_SLICES=1 QPGPU_LDE_FEW=0 python -u tools/agg_latency.py 1,2,4,8,16,32 5 &&
