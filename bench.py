@@ -701,6 +701,9 @@ def main():
                 # the loop replayed from registers is the ceiling that holds
                 "frac_of_register_replay": rr["frac"] if rr else None,
                 "register_replay": rr,
+                "frac_of_ceiling": rr["frac"] if rr else None,
+                "ceiling_kind": "the kernel's own instruction stream replayed from registers (tools/leaf_ubench L3 "
+                                "vs L0, same run); mix_ceiling* = an additive per-class estimate",
                 "sources": {"instr_per_perm": os.path.relpath(PMC_SQ_FILE, ROOT),
                             "mix_ceiling": os.path.relpath(CEIL_FILE, ROOT) if ceil else None,
                             "share": os.path.relpath(KSUM1_FILE, ROOT) if ksum1 else None,
