@@ -193,7 +193,99 @@ def parse():
                          "leaves -> its subtree root; roots gathered over RCCL; rank 0: the tree root); 0 = skip")
     ap.add_argument("--cpu-sample", type=int, default=2, help="min proofs in the CPU baseline sample (0 = skip)")
     ap.add_argument("--cpu-seconds", type=float, default=10.0, help="min seconds of CPU baseline proving")
+    ap.add_argument("--launch-selftest", choices=["ok", "fail-rank1"], default=None,
+                    help="test the --gpus N launcher without a GPU: every rank joins a gloo group and rank 0 prints "
+                         "the ranks it saw (fail-rank1: rank 1 exits non-zero first)")
     return ap.parse_args()
+
+
+def launch_ranks(n, argv):
+    """`bench.py --gpus N` (N > 1) with no WORLD_SIZE in the environment: start N
+    rank processes of this script, one per GPU (RANK = LOCAL_RANK = 0..N-1,
+    WORLD_SIZE = N, a free 127.0.0.1 port), before anything here imports torch or
+    the library -- child processes, never an exec.  Rank 0's stdout is this
+    process's (the one JSON line); the other ranks' stdout goes to stderr.  When a
+    rank fails the others are stopped (they would wait in a collective).
+    Returns the exit status: 0 when every rank succeeded, else the first
+    non-zero one."""
+    import signal
+    import socket
+    import subprocess
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        port = s.getsockname()[1]
+    procs = []
+    for r in range(n):
+        env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(n), LOCAL_WORLD_SIZE=str(n),
+                   GROUP_RANK="0", MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+        env.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
+        procs.append(subprocess.Popen([sys.executable, "-u", os.path.abspath(__file__)] + argv, env=env,
+                                      stdout=None if r == 0 else sys.stderr.fileno()))
+    rc = 0
+    try:
+        while [p.poll() for p in procs].count(None):
+            bad = [p.returncode for p in procs if p.returncode not in (None, 0)]
+            if bad and not rc:
+                rc = bad[0]
+                print(f"bench.py launcher: a rank exited with status {rc}; stopping the other ranks",
+                      file=sys.stderr, flush=True)
+                for p in procs:
+                    if p.poll() is None:
+                        p.send_signal(signal.SIGTERM)
+                deadline = time.time() + 30
+                while any(p.poll() is None for p in procs) and time.time() < deadline:
+                    time.sleep(0.2)
+                for p in procs:
+                    if p.poll() is None:
+                        p.kill()
+            time.sleep(0.2)
+    except KeyboardInterrupt:
+        for p in procs:
+            if p.poll() is None:
+                p.kill()
+        raise
+    for p in procs:
+        p.wait()
+    if not rc:
+        rc = next((p.returncode for p in procs if p.returncode), 0)
+    # a signal-killed rank reports a negative status: exit with 128 + signal
+    return rc if rc >= 0 else 128 - rc
+
+
+def launch_selftest(mode, gpus):
+    """One rank of the launcher self-test (no GPU): a gloo group of WORLD_SIZE
+    ranks; rank 0 prints one JSON line with every rank's (RANK, LOCAL_RANK,
+    WORLD_SIZE) as the group saw them."""
+    import torch.distributed as dist
+    rank = int(os.environ.get("RANK", "0"))
+    if mode == "fail-rank1" and rank == 1:
+        sys.exit(5)
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    if world != gpus:
+        print(f"bench.py: WORLD_SIZE {world} != --gpus {gpus}", file=sys.stderr)
+        sys.exit(3)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    me = {"rank": dist.get_rank(), "local_rank": int(os.environ.get("LOCAL_RANK", "0")),
+          "world": dist.get_world_size()}
+    seen = [None] * world
+    dist.all_gather_object(seen, me)
+    if rank == 0:
+        print(json.dumps({"launch_selftest": mode, "gpus": gpus, "world_size": dist.get_world_size(),
+                          "ranks": seen}), flush=True)
+    dist.destroy_process_group()
+
+
+def check_world(args, world, torch):
+    """Every rank: the process group is the --gpus N the line will report, and
+    this node has N devices (before any collective, so every rank fails alike
+    instead of one waiting on another)."""
+    if world != args.gpus:
+        print(f"bench.py: WORLD_SIZE {world} != --gpus {args.gpus}", file=sys.stderr, flush=True)
+        sys.exit(3)
+    ndev = torch.cuda.device_count()
+    if ndev < args.gpus:
+        print(f"bench.py: --gpus {args.gpus} but this node has {ndev} GPU(s)", file=sys.stderr, flush=True)
+        sys.exit(3)
 
 
 def trace_marker(torch):
@@ -431,15 +523,24 @@ def configs3(args, circuit, prover, provers, cin, per, NP, B, dist, world, rank,
 
 def main():
     args = parse()
+    if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
+        sys.exit(launch_ranks(args.gpus, sys.argv[1:]))
+    if args.launch_selftest:
+        return launch_selftest(args.launch_selftest, args.gpus)
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
     import torch
+    check_world(args, world, torch)
     dist = None
     if world > 1:
         import torch.distributed as dist
         torch.cuda.set_device(local)
         dist.init_process_group("nccl")
+        if dist.get_world_size() != args.gpus:
+            print(f"bench.py: process group of {dist.get_world_size()} ranks != --gpus {args.gpus}",
+                  file=sys.stderr, flush=True)
+            sys.exit(3)
     import qp_wormhole
 
     voting = args.circuit == "voting"
@@ -474,10 +575,15 @@ def main():
         return provers[i].prove_wires_dev(d_wires.data_ptr() + first[i] * wstride,
                                           pis[first[i]:first[i] + per[i]], per[i])
 
+    gathered = []  # rank 0: leaf proofs that reached it per timed step (world x B)
+
+    def on_leaves(s, res):
+        gathered.append(sum(res[1]) if dist is not None else len(res))
+
     def steps(k, pipelined):
         # leaf proofs -> aggregator rank over RCCL (raw gather) after every step
         return run_steps(prove_share, NP, k, dist=dist, slot=prover.proof_size, device=f"cuda:{local}",
-                         pipelined=pipelined)
+                         pipelined=pipelined, on_leaves=on_leaves)
 
     proofs = steps(args.warmup, False) if args.warmup else None
     # proofs of the warmup verify (rank 0 checks the first and last with the oracle verifier)
@@ -492,6 +598,7 @@ def main():
         p.stage_times(reset=True)
     if dist is not None:
         dist.barrier()
+    gathered.clear()
     trace_marker(torch)
     torch.cuda.synchronize()
     t0 = time.perf_counter()
@@ -612,6 +719,9 @@ def main():
             "value": total / dt,
             "unit": "proofs/s",
             "n_gpus": world,
+            "rccl_world_size": dist.get_world_size() if dist is not None else 1,
+            "process_group_backend": dist.get_backend() if dist is not None else None,
+            "leaf_proofs_gathered_per_step": gathered[-1] if gathered else None,
             "steps": args.steps,
             "warmup": args.warmup,
             "ms_per_step": dt / args.steps * 1e3,

@@ -353,7 +353,9 @@ CircuitData CircuitBuilder::build() {
   for (size_t i = 0; i < consts.size(); i += ncg) {
     F c0 = consts[i].first, c1 = i + 1 < consts.size() ? consts[i + 1].first : 0;
     uint32_t row = add_gate(G_CONSTANT, c0, c1);
-    for (uint32_t j = 0; j < ncg && i + j < consts.size(); j++) connect(consts[i + j].second, Target::wire(row, j));
+    // connect(wire, t) as upstream: the fresh gate wire's set absorbs t's, so the
+    // wire becomes the set's root (representative_map, prover.bin's watch keys)
+    for (uint32_t j = 0; j < ncg && i + j < consts.size(); j++) connect(Target::wire(row, j), consts[i + j].second);
   }
   // pad to a power of two with NoopGate
   size_t nrows = rows_.size();

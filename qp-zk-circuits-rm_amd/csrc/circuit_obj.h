@@ -1,6 +1,7 @@
 // circuit_obj.h — definitions behind qp_circuit / qp_witness handles.
 #pragma once
 #include <stdint.h>
+#include <mutex>
 #include <vector>
 #include "circuit.h"
 #include "recursion.h"
@@ -15,7 +16,8 @@ struct qp_circuit {
   qr::AggregationTargets aggregation;
   uint32_t gates_used = 0;
   // upstream-format prover.bin between qp_circuit_prover_only_bytes' size and copy calls
-  mutable std::vector<uint8_t> prover_bin;
+  mutable std::vector<uint8_t> prover_bin;  // guarded by prover_bin_mu
+  mutable std::mutex prover_bin_mu;
 };
 
 // commit(): the fragments' fill_targets into w (no generation); "" on success,

@@ -33,6 +33,7 @@
 #include <string.h>
 #include <algorithm>
 #include <map>
+#include <mutex>
 #include <new>
 #include <thread>
 #include <vector>
@@ -345,6 +346,9 @@ extern "C" int qp_circuit_prover_only_bytes(const qp_circuit *c, uint8_t *out, s
   if (!c || (!out && !len)) return QP_ERR_ARG;
   for (qc::GateKind k : c->cd.gate_kinds)
     if (k > qc::G_POSEIDON) return QP_ERR_ARG;  // the leaf circuits' gate set only
+  // the size query builds the file and keeps it for the copy call that follows;
+  // concurrent calls on one shared circuit handle serialise here
+  std::lock_guard<std::mutex> lk(c->prover_bin_mu);
   try {
     if (c->prover_bin.empty()) c->prover_bin = prover_only_bytes(c);
   } catch (const std::bad_alloc &) {

@@ -246,12 +246,15 @@ def aggregate_chunk(chunk, common_data: bytes, verifier_only: bytes, device: int
 
 
 def aggregate_level(proofs, common_data: bytes, verifier_only: bytes, config: TreeAggregationConfig,
-                    device: int = 0, backend=None, prover: Optional[int] = None) -> List[AggregatedProof]:
+                    device: int = 0, backend=None, prover: Optional[int] = None,
+                    nprov: int = 0) -> List[AggregatedProof]:
     """tree.rs:80-103: chunks of `tree_branching_factor` proofs, each aggregated
     (all chunks of the level proven as one GPU batch).  backend(inner_common,
     branching, device, max_batch) -> an object with .data and .prove_chunks()
     (default: the GPU level prover; tests inject a CPU one).  prover: the level
-    prover's device prover that takes every chunk (a sub-tree's thread)."""
+    prover's device prover that takes every chunk (a sub-tree's thread);
+    nprov: the device provers the cached level prover must have (the sub-tree
+    threads all pass the same count, so the first call builds it once)."""
     k = config.tree_branching_factor
     proofs = [_as_proof(p) for p in proofs]
     if not proofs or k < 1:
@@ -269,7 +272,8 @@ def aggregate_level(proofs, common_data: bytes, verifier_only: bytes, config: Tr
         if tail is not None:
             out += backend(common_data, len(tail), device, 1).prove_chunks([tail], verifier_only)
         return out
-    nprov = max(prover + 1, _agg_provers()) if prover is not None else 0
+    if prover is not None:
+        nprov = max(nprov, prover + 1, _agg_provers())
     if chunks:
         # up to 32 aggregation proofs per GPU batch (2.7 vs 3.2 ms per proof at 16;
         # tools/agg_bench.py, profiles/r03_agg_bench.log)
@@ -317,7 +321,7 @@ def aggregate_to_tree(leaf_proofs, common_data: bytes, verifier_only: bytes,
     if db is not None:
         raise CircuitTooLarge(f"level-1 aggregation circuit is 2^{db} rows", [])
 
-    def levels(proofs, prover=None):
+    def levels(proofs, prover=None, nprov=0):
         """Levels down to one proof; returns (proofs, None) or (the last level
         proven, the message of the circuit that was too large)."""
         while len(proofs) > 1:
@@ -327,7 +331,7 @@ def aggregate_to_tree(leaf_proofs, common_data: bytes, verifier_only: bytes,
                 return proofs, (f"the next level's aggregation circuit is 2^{db} rows (its public inputs: every "
                                 f"leaf's); the GPU prover proves up to 2^{GPU_MAX_DEGREE_BITS}")
             proofs = aggregate_level([p.proof for p in proofs], cd.common, cd.verifier_only, config, device,
-                                     backend, prover)
+                                     backend, prover, nprov)
         return proofs, None
 
     parts = _subtree_parts(len(leaf_proofs), config.tree_branching_factor) if backend is None else 1
@@ -337,14 +341,17 @@ def aggregate_to_tree(leaf_proofs, common_data: bytes, verifier_only: bytes,
         # prover each: no level barrier between them, so one sub-tree's host
         # phases and latency-bound launches overlap the other's kernels
         m = len(leaf_proofs) // parts
+        # one device prover per sub-tree, the same count for every thread (so
+        # no thread rebuilds a level prover another thread has just built)
+        nprov = max(parts, _agg_provers())
         res = [None] * parts
         errors = []
 
         def run(i):
             try:
                 lv = aggregate_level(leaf_proofs[i * m:(i + 1) * m], common_data, verifier_only, config, device,
-                                     backend, i)
-                res[i] = levels(lv, i)
+                                     backend, i, nprov)
+                res[i] = levels(lv, i, nprov)
             except BaseException as e:  # re-raised on the calling thread
                 errors.append(e)
 

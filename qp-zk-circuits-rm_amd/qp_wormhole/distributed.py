@@ -249,7 +249,9 @@ def pipeline_aggregate_steps(prove_leaves, steps: int, common: bytes, verifier_o
     levels).  The subtree's narrow top levels are latency-bound (one proof's
     sequential Poseidon chains), so the leaf proofs of the next batch fill the
     GPU they leave idle.  At most one finished batch waits in between.  Only
-    this thread issues collectives, in the same order on every rank.  Returns
+    this thread issues collectives, in the same order on every rank; each step
+    starts with an all-reduce of a per-rank ok flag, so a leaf failure on one
+    rank stops every rank at that step (each raises).  Returns
     ([root per step on dst / None], [stage seconds per step])."""
     import queue
     import threading
@@ -273,10 +275,22 @@ def pipeline_aggregate_steps(prove_leaves, steps: int, common: bytes, verifier_o
     th = threading.Thread(target=leaf_worker, daemon=True)
     th.start()
     roots, tms = [], []
+    def all_ok(ok):
+        # every rank stops at the same step when one rank's leaf step failed
+        # (its peers would otherwise wait in this step's collectives forever)
+        if dist is None:
+            return ok
+        import torch
+        t = torch.tensor([1 if ok else 0], dtype=torch.int64, device=device)
+        dist.all_reduce(t, op=dist.ReduceOp.MIN)
+        return bool(t.item())
+
     try:
         for _ in range(steps):
             item = q.get()
-            if item is None:
+            if not all_ok(item is not None):
+                if item is not None:
+                    errors.append(RuntimeError("another rank's leaf step failed"))
                 break
             leaves, lt = item
             tm = {"leaves_s": lt}

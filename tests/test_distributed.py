@@ -361,3 +361,52 @@ def test_configs3_pipelined_steps_world2_gloo():
     res, ncalls, stages = _run(_worker_pipeline_steps, 2)
     assert res == [True] * 3 and ncalls == 3
     assert stages == [["gather_s", "leaves_s", "subtree_s", "top_s"]] * 3
+
+
+def _worker_pipeline_steps_fail(rank, world, port, q):
+    """A leaf failure on rank 1 at batch 2 of 3: every rank stops at that
+    step's ok-flag all-reduce and raises (none waits in the roots gather)."""
+    import torch.distributed as dist
+
+    from agg_oracle_backend import oracle_backend
+    from qp_wormhole.distributed import pipeline_aggregate_steps
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    from current_circuit_vd import current_circuit_verifier_data
+    from oracle_lib import golden
+    from test_oracle_golden import current_common_bytes
+    cb = current_common_bytes()
+    vd = current_circuit_verifier_data(cb)[0]
+    fx = [golden("dummy_proof.bin"), golden("dummy_proof_zk.bin")]
+    calls = []
+
+    def prove_leaves():
+        calls.append(1)
+        if rank == 1 and len(calls) == 2:
+            raise ValueError("leaf failure on rank 1")
+        return fx
+    try:
+        pipeline_aggregate_steps(prove_leaves, 3, cb, vd[:len(vd) - len(cb)], 2, dist, backend=oracle_backend)
+        err = None
+    except Exception as e:  # noqa: BLE001
+        err = str(e)
+    q.put((rank, err))
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+def test_configs3_pipelined_leaf_failure_stops_every_rank():
+    import torch.multiprocessing as mp
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_worker_pipeline_steps_fail, args=(r, 2, port, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    got = dict(q.get(timeout=180) for _ in procs)
+    for p in procs:
+        p.join(timeout=180)
+        assert p.exitcode == 0
+    assert got[1] == "leaf failure on rank 1"
+    assert got[0] == "another rank's leaf step failed"

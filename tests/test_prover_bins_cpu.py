@@ -95,6 +95,13 @@ def test_upstream_prover_bin_round_trip(circ, upstream):
     # every generator's watched targets are indexed under their representatives
     rep = f["representative_map"]
     assert all(rep[key] == key for key in f["watches"])
+    # build() connects each ConstantGate's output wire to its constant's target as
+    # connect(Target::wire(row, wire), t): Forest::merge puts t's root under the
+    # fresh wire, which stays its set's representative
+    W = circ.num_wires
+    consts = [b for name, b in f["generators"] if name == "ConstantGenerator"]
+    assert consts
+    assert all(rep[int(b[0]) * W + int(b[2])] == int(b[0]) * W + int(b[2]) for b in consts)
     assert P.upstream_prover_layout(upstream, circ, cap, check_subtrees=2) == tuple(dig)
     nz = P._common_of("standard_recursion_config")
     parsed = P._parse_prover_only(upstream, nz, circ, vo)
