@@ -191,6 +191,9 @@ def parse():
     ap.add_argument("--configs3", type=int, default=1,
                     help="after the headline, time BASELINE configs[3] as one pipeline (every rank: its batch of "
                          "leaves -> its subtree root; roots gathered over RCCL; rank 0: the tree root); 0 = skip")
+    ap.add_argument("--ref-shapes", type=int, default=1,
+                    help="after the headline, time the reference's own bench shapes: prover_create_proof "
+                         "(new + commit + prove, zk config), the aggregator bench trees, one voting pass (0 = skip)")
     ap.add_argument("--cpu-sample", type=int, default=2, help="min proofs in the CPU baseline sample (0 = skip)")
     ap.add_argument("--cpu-seconds", type=float, default=10.0, help="min seconds of CPU baseline proving")
     ap.add_argument("--launch-selftest", choices=["ok", "fail-rank1"], default=None,
@@ -359,8 +362,33 @@ def cpu_baseline(circuit, inputs, sample, min_seconds):
     dt = time.perf_counter() - t
     nproc = os.cpu_count() or 1
     value = done / dt
+    # the reference's bench iteration (prover/benches/prover.rs:11-21) on the same
+    # cores: WormholeProver::new(standard_recursion_zk_config) = the circuit build
+    # (host C++) + the constants||sigmas commitment (oracle ora_commit_values, one
+    # thread), then commit(test_inputs()) + prove (oracle/prover.c, OpenMP)
+    import wormhole_inputs
+    L.ora_commit_values.argtypes = [U64P, ctypes.c_uint, ctypes.c_uint, ctypes.c_uint, ctypes.c_uint, ctypes.c_void_p,
+                                    ctypes.c_uint, ctypes.c_int, ctypes.c_void_p, ctypes.c_void_p, U64P]
+    t0 = time.perf_counter()
+    zc = type(circuit).wormhole(zero_knowledge=True)
+    zcs = np.ascontiguousarray(zc.constants_sigmas())
+    zcap = np.zeros(64, np.uint64)
+    rc = L.ora_commit_values(zcs, zcs.shape[0], zc.degree_bits, 3, 4, None, 0, 0, None, None, zcap)
+    assert rc == 0
+    t1 = time.perf_counter()
+    w = zc.commit(wormhole_inputs.test_inputs())
+    zw, zpis = w.wires(), w.public_inputs()
+    w.free()
+    t2 = time.perf_counter()
+    zcb = zc.common_data()
+    assert L.ora_prove(zcb, len(zcb), zcs, zw, zpis, len(zpis), out, 400000, ctypes.byref(ln), cap, dig) == 0
+    t3 = time.perf_counter()
+    create = {"new_ms": (t1 - t0) * 1e3, "commit_ms": (t2 - t1) * 1e3, "prove_ms": (t3 - t2) * 1e3,
+              "iteration_ms": (t3 - t0) * 1e3,
+              "note": "one iteration: circuit build (host C++) + constants||sigmas commit (oracle, 1 thread) + "
+                      "commit(test_inputs()) + prove (oracle/prover.c, OpenMP)"}
     return {"value": value, "unit": "proofs/s", "cores": cores, "kind": "port",
-            "per_core": value / cores,
+            "per_core": value / cores, "prover_create_proof": create,
             "sample": f"{done} {circuit.kind} proofs (deg {circuit.degree_bits}, standard_recursion_config) from the "
                       f"bench's CircuitInputs, {dt:.1f} s: commit + witness generation {t_wit:.2f} s (host C++, one "
                       f"thread), prove {dt - t_wit:.1f} s (oracle/prover.c, C + OpenMP, {cores} threads)",
@@ -413,6 +441,128 @@ def reference_parity(qp_wormhole, device):
     out["note"] = ("GPU proof bytes == the reference's own proof of test_inputs() given its PI-row random cells "
                    "and PoW witness (its find_any witness is nondeterministic); after the timed region")
     return out
+
+
+def cargo_bench_shape(qp_wormhole, local, iters=3):
+    """The reference's own benchmark iteration (wormhole/prover/benches/prover.rs:11-21,
+    "prover_create_proof"): WormholeProver::new(standard_recursion_zk_config) --
+    the circuit build plus the constants||sigmas commitment (prover/src/lib.rs:
+    190-202) -- then commit(test_inputs()) and prove(), every iteration from
+    scratch (a new device context and prover each time, nothing cached).  One
+    untimed iteration first (code objects, allocator); median of `iters`."""
+    import wormhole_inputs
+    from oracle_lib import lib as olib
+    rows = []
+    ok = None
+    for it in range(iters + 1):
+        t0 = time.perf_counter()
+        ctx = qp_wormhole.Context(local)
+        circ = qp_wormhole.Circuit.wormhole(zero_knowledge=True)
+        p = qp_wormhole.Prover(ctx, circ, max_batch=1)
+        ctx.synchronize()
+        t1 = time.perf_counter()
+        w = circ.commit(wormhole_inputs.test_inputs())
+        t2 = time.perf_counter()
+        proof = p.prove_witnesses([w])[0]
+        t3 = time.perf_counter()
+        if it:
+            rows.append((t1 - t0, t2 - t1, t3 - t2, t3 - t0))
+        if it == iters:
+            vd = p.verifier_data()
+            ok = olib().ora_verify(vd, len(vd), proof, len(proof)) == 0
+        w.free()
+        p.free()
+        ctx.close()
+    med = [sorted(c)[len(c) // 2] * 1e3 for c in zip(*rows)]
+    return {"new_ms": med[0], "commit_ms": med[1], "prove_ms": med[2], "iteration_ms": med[3],
+            "iterations": iters, "proof_verified": ok,
+            "note": "WormholeProver::new(standard_recursion_zk_config) (circuit build on the host + device "
+                    "preprocessing: constants||sigmas LDE and Merkle tree) + commit(test_inputs()) + prove(), from "
+                    "scratch each iteration; medians; after the timed region"}
+
+
+# the reference's aggregator benchmark shapes (wormhole/aggregator/benches/aggregator.rs:106-123)
+AGG_SHAPES = [(2, 1), (2, 2), (2, 3), (2, 4), (2, 5), (3, 2), (4, 2), (5, 2), (6, 2), (7, 2)]
+
+
+def aggregator_shapes(qp_wormhole, local):
+    """aggregate_proofs_{k}_{depth} of aggregator.rs:22-58: WormholeProofAggregator::default()
+    (standard_recursion_zk_config leaves) with TreeAggregationConfig::new(k, depth),
+    num_leaf_proofs copies of dummy_proof_zk.bin pushed, aggregate() timed.  The
+    reference builds every chunk's circuit inside aggregate() (tree.rs:106-125);
+    here level circuits are built once and cached, so each shape reports its
+    first call (circuits built + device preprocessing) and the best of two
+    cached calls.  Every root is verified by the oracle verifier afterwards."""
+    from oracle_lib import lib as olib
+    from qp_wormhole import aggregator as A
+    out = {}
+    base = A.WormholeProofAggregator.default(local)
+    dummy = base.dummy_proof()
+    for k, depth in AGG_SHAPES:
+        cfg = A.TreeAggregationConfig.new(k, depth)
+        times, root = [], None
+        for _ in range(3):
+            agg = A.WormholeProofAggregator(base.leaf_circuit_data, dummy, local).with_config(cfg)
+            for _ in range(cfg.num_leaf_proofs):
+                agg.push_proof(dummy)
+            t0 = time.perf_counter()
+            root = agg.aggregate()
+            times.append(time.perf_counter() - t0)
+        rvd, rp = root.circuit_data.verifier_data(), root.proof.to_bytes()
+        from qp_wormhole.prover import _common_degree_bits
+        out[f"aggregate_proofs_{k}_{depth}"] = {
+            "leaves": cfg.num_leaf_proofs, "first_call_ms": times[0] * 1e3,
+            "cached_ms": min(times[1:]) * 1e3,
+            "root_degree_bits": _common_degree_bits(root.circuit_data.common),
+            "root_verified": olib().ora_verify(rvd, len(rvd), rp, len(rp)) == 0}
+        # release this shape's level provers (device workspaces) before the next
+        with A._levels_lock:
+            A._levels.clear()
+    out["note"] = ("the reference's aggregator bench shapes (binary 2..32 leaves, (k,2) for k = 3..7) on the GPU: "
+                   "first_call_ms builds the level circuits and their device preprocessing (the reference builds "
+                   "them inside every aggregate()); cached_ms (best of two) reuses them; after the timed region")
+    return out
+
+
+def voting_pass(qp_wormhole, local, batch=1024, nprov=6):
+    """BASELINE configs[4]: one pass of `batch` voting proofs (voting/src/lib.rs:346-360
+    circuit), end to end from the synthetic vote inputs, `nprov` provers in
+    parallel on their own streams (the --circuit voting bench's shape), timed
+    after one untimed pass."""
+    import threading
+    from qp_wormhole.synthetic import synthetic_vote_inputs
+    circ = qp_wormhole.Circuit.voting()
+    per = [batch // nprov + (1 if i < batch % nprov else 0) for i in range(nprov)]
+    first = [sum(per[:i]) for i in range(nprov)]
+    inputs = [synthetic_vote_inputs(i) for i in range(batch)]
+    ps = [qp_wormhole.Prover(qp_wormhole.Context(local), circ, max_batch=per[i]) for i in range(nprov)]
+    cin = [ps[i].inputs_array(inputs[first[i]:first[i] + per[i]]) for i in range(nprov)]
+    outs = [None] * nprov
+
+    def run(i):
+        outs[i] = ps[i].prove_inputs_array(cin[i], per[i])
+
+    def once():
+        th = [threading.Thread(target=run, args=(i,)) for i in range(nprov)]
+        for t in th:
+            t.start()
+        for t in th:
+            t.join()
+        if any(o is None for o in outs):
+            raise RuntimeError("a voting prover thread failed")
+    once()
+    t0 = time.perf_counter()
+    once()
+    dt = time.perf_counter() - t0
+    from oracle_lib import lib as olib
+    vd = ps[0].verifier_data()
+    ok = all(olib().ora_verify(vd, len(vd), pf, len(pf)) == 0 for pf in (outs[0][0], outs[-1][-1]))
+    for p in ps:
+        p.free()
+    return {"proofs": batch, "provers": nprov, "seconds": dt, "proofs_per_s": batch / dt,
+            "degree_bits": circ.degree_bits, "proofs_verified": ok,
+            "note": "voting circuit, synthetic seeded vote inputs, one timed pass after an untimed one; after the "
+                    "timed region"}
 
 
 def configs3(args, circuit, prover, provers, cin, per, NP, B, dist, world, rank, local, torch):
@@ -709,6 +859,16 @@ def main():
     ref_parity = None
     if rank == 0 and not voting and args.mode == "e2e":
         ref_parity = reference_parity(qp_wormhole, local)
+    shapes = None
+    if rank == 0 and not voting and args.mode == "e2e" and args.ref_shapes:
+        tr = time.perf_counter()
+        shapes = {"prover_create_proof": cargo_bench_shape(qp_wormhole, local)}
+        tc = time.perf_counter()
+        shapes["aggregator"] = aggregator_shapes(qp_wormhole, local)
+        ta = time.perf_counter()
+        shapes["voting_configs4"] = voting_pass(qp_wormhole, local)
+        shapes["wall_s"] = {"prover_create_proof": tc - tr, "aggregator": ta - tc,
+                            "voting": time.perf_counter() - ta}
     if rank == 0:
         total = world * B * args.steps
         lde = ks["lde_wires"]
@@ -767,6 +927,7 @@ def main():
             "prove_only_1prover_proofs_per_s": prove_only,
             "warmup_proof_verified": verified,
             "reference_proof_bytes_equal": ref_parity,
+            "reference_bench_shapes": shapes,
         }
         if iso is not None and iso["lde_wires"]["ms"]:
             # with concurrent provers a launch's event-to-event time includes the

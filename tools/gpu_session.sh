@@ -57,6 +57,11 @@ for s in "$@"; do
     isa) step isa_rates 300 tools/isa_rates ;;
     test_agg) step pytest_agg 900 python -u -m pytest tests/test_gpu_aggregation.py tests/test_gpu_guards.py -x -v --timeout 400 --timeout-method thread ;;
     test_ref) step pytest_ref 600 python -u -m pytest tests/test_gpu_reference_proof.py tests/test_gpu_prover.py -x -v --timeout 300 --timeout-method thread ;;
+    gpus2) echo "=== gpus2 (expect a refusal: one GPU on this box)" | tee -a gpurun_out/session.log
+           timeout -k 10 300 python -u bench.py --gpus 2 --steps 1 --warmup 0 > gpurun_out/gpus2.log 2>&1
+           echo "=== gpus2 rc=$?" | tee -a gpurun_out/session.log; tail -5 gpurun_out/gpus2.log ;;
+    shapes) step shapes 900 python -u bench.py --steps 2 --warmup 1 --cpu-sample 0 --configs3 0 --agg-leaves 0 ;;
+    benchfull) step benchfull 900 python -u bench.py --steps 20 --warmup 5 ;;
     bench5) step bench5 600 python -u bench.py --steps 5 --warmup 1 --cpu-sample 0 ;;
     agg_ab) step agg_dev2 300 python -u tools/agg_subtree.py 256 2 &&
             step agg_dev1 300 env QP_AGG_PROVERS=1 python -u tools/agg_subtree.py 256 2 &&
