@@ -8,6 +8,7 @@
 //                           (greedy groups, max degree = qdf + 1), wire
 //                           partition -> sigma polys (k_i * w^row)
 //   gates/poseidon.rs       PoseidonGenerator wire layout
+#include "paths.h"
 #include "circuit.h"
 #include <algorithm>
 #include <numeric>
@@ -716,8 +717,7 @@ CircuitData CircuitBuilder::build() {
       // constant) generators computable from inputs alone with their chain
       // depth in permutations; backward, those at least tmin deep and every
       // such generator feeding one
-      uint32_t tmin = HOST_CHAIN_MIN;
-      if (const char *e = getenv("QPGPU_HOST_CHAIN")) tmin = (uint32_t)strtoul(e, nullptr, 10);
+      const uint32_t tmin = (uint32_t)qpk::path_opt("host_chain", HOST_CHAIN_MIN);  // path hook host_chain
       std::vector<uint8_t> on_host(ng, 0);
       if (tmin) {
         std::vector<uint8_t> hostable(ng, 0), hw(nslots, 0), need(nslots, 0);

@@ -44,29 +44,20 @@ struct Twiddles {
   // coset pre-twists of the fused LDE: for rate r (1..LDE_MAX_RATE), at
   // offset 16*(2^r - 2): ptw[16 s + m] = w_{16*2^r}^(s*m), s < 2^r, m < 16
   uint64_t *ptw = nullptr;
-  // the same for the radix-8 LDE: ptw8[8 (2^r - 2) + 8 s + m] = w_{8*2^r}^(s*m), m < 8
-  uint64_t *ptw8 = nullptr;
   // twiddles of the radix-16 LDS passes laid out per pass so a wave's lanes
   // (consecutive t) read consecutive words: for S = 2^L, 4 <= L <= TW_LOG, at
   // pt_offset(L): pt[m (S/16) + t] = w_S^(+-t brev4(m)), t < S/16, m < 16
   uint64_t *pt_fwd = nullptr, *pt_inv = nullptr;
   // merged first-pass twiddles of k_lde_cosets per (log_n, r), n = 16 T,
   // N = n 2^r: at mtw_off[log_n][r], mtw[(16 s + m) T + t] = w_N^(t (s + 2^r brev4(m)))
-  // (QPGPU_LDE_MODE=0, the default: N words per (log_n, r) re-read by every
-  // column's workgroup -- round-3 PMC: LDE reads 4.8x algorithmic -- yet the
-  // factored modes' extra vector loads cost more, profiles/r04_lde_ab.log)
+  // (N words per (log_n, r) re-read by every column's workgroup, from L2;
+  // factored tables' extra vector loads cost more, profiles/r04_lde_ab.log)
   uint64_t *mtw = nullptr;
   uint64_t mtw_off[TW_LOG + 1][LDE_MAX_RATE + 1] = {};
-  // coset steps of k_lde_cosets per (log_n, r): at utw_off[log_n][r],
-  // utw[k] = w_N^k, k < n (n words; with the pass table pt for S = n the
-  // first-pass twiddles factor into coset-independent tables that stay in L2)
-  uint64_t *utw = nullptr;
-  uint64_t utw_off[TW_LOG + 1][LDE_MAX_RATE + 1] = {};
 };
 __host__ __device__ constexpr uint32_t pt_offset(uint32_t log_S) { return (1u << log_S) - 16u; }
 constexpr uint32_t LDE_COSETS_MIN_LOG = 10, LDE_COSETS_MAX_LOG = 14;  // k_lde_cosets sizes
 __host__ __device__ inline uint32_t ptw_offset(uint32_t rate_bits) { return 16u * ((1u << rate_bits) - 2u); }
-__host__ __device__ inline uint32_t ptw8_offset(uint32_t rate_bits) { return 8u * ((1u << rate_bits) - 2u); }
 
 hipError_t twiddles_init(Twiddles &t, hipStream_t s);
 void twiddles_free(Twiddles &t);
@@ -99,14 +90,13 @@ void leaf_hash(const uint64_t *cols, uint64_t stride, uint32_t ncols, const uint
 // parent levels down to the cap (two_to_one), appended after the N leaf digests
 void merkle_tree(uint64_t *digests, uint32_t log_N, uint32_t cap_h, uint32_t nbat, uint64_t d_bstride,
                  hipStream_t s);
-// leaf digests and, when the tree has a level below the cap, its first level
-// in the same kernel; returns the first level merkle_tree_from still builds
+// leaf digests; returns the first level merkle_tree_from still builds (1)
 uint32_t leaf_hash_first(const uint64_t *cols, uint64_t stride, uint32_t ncols, const uint64_t *salt, uint32_t nsalt,
                          uint64_t *digests, uint32_t log_N, uint32_t cap_h, uint32_t nbat, uint64_t c_bstride,
                          uint64_t s_bstride, uint64_t d_bstride, hipStream_t s);
 void merkle_tree_from(uint64_t *digests, uint32_t log_N, uint32_t cap_h, uint32_t nbat, uint64_t d_bstride,
                       uint32_t first_level, hipStream_t s);
-// leaf digests + the whole tree (first level fused into the leaf kernel)
+// leaf digests + the whole tree
 void leaf_hash_tree(const uint64_t *cols, uint64_t stride, uint32_t ncols, const uint64_t *salt, uint32_t nsalt,
                     uint64_t *digests, uint32_t log_N, uint32_t cap_h, uint32_t nbat, uint64_t c_bstride,
                     uint64_t s_bstride, uint64_t d_bstride, hipStream_t s);

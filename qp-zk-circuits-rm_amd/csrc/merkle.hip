@@ -10,29 +10,12 @@
 #include "poseidon_coop.h"
 #include <stdlib.h>
 #include "kernels.h"
+#include "paths.h"
 
-// trees narrower than 2^QP_MERKLE_FUSE_LOG nodes per level finish in one
-// launch (one wave per block at 6, so no wave idles at the level barriers)
-// QP_LEAF_PAIRS 1: leaf digests and the first tree level in one kernel
-// (k_leaf_hash2); 0 (default): leaf kernel + a level launch.  Measured
-// (python bench.py --steps 10, two runs each, one box): fused 919.8 / 924.9 vs
-// 930.0 / 933.0 proofs/s — three inlined permutations in one kernel cost more
-// than the level launch they save (profiles/r02_ab_leaf_pairs.log)
-#ifndef QP_LEAF_PAIRS
-#define QP_LEAF_PAIRS 0
-#endif
-// occupancy cap of the hashing kernels (0: compiler's choice, 72 VGPRs = 7 waves/SIMD)
-#ifndef QP_HASH_WAVES
-#define QP_HASH_WAVES 0
-#endif
-#if QP_HASH_WAVES
-#define QP_HASH_OCC __attribute__((amdgpu_waves_per_eu(QP_HASH_WAVES)))
-#else
-#define QP_HASH_OCC
-#endif
-#ifndef QP_MERKLE_FUSE_LOG
-#define QP_MERKLE_FUSE_LOG 6
-#endif
+// Leaf digests and the first tree level are separate launches: one kernel
+// doing both (three inlined permutations per lane) measured slower, 919.8 /
+// 924.9 vs 930.0 / 933.0 proofs/s (profiles/r02_ab_leaf_pairs.log).  The
+// hashing kernels run at the compiler's occupancy (72 VGPRs = 7 waves/SIMD).
 
 namespace qpk {
 
@@ -60,7 +43,7 @@ __device__ __forceinline__ void leaf_digest(const uint64_t *__restrict__ cols, u
   for (int k = 0; k < 4; k++) s[k] = psd::canon(s[k]);
 }
 
-__global__ void __launch_bounds__(256) QP_HASH_OCC k_leaf_hash(const uint64_t *__restrict__ cols, uint64_t stride, uint32_t ncols,
+__global__ void __launch_bounds__(256) k_leaf_hash(const uint64_t *__restrict__ cols, uint64_t stride, uint32_t ncols,
                                                    const uint64_t *__restrict__ salt, uint32_t nsalt,
                                                    uint64_t *__restrict__ dig, uint32_t N, uint64_t c_bstride,
                                                    uint64_t s_bstride, uint64_t d_bstride) {
@@ -81,7 +64,7 @@ __global__ void __launch_bounds__(256) QP_HASH_OCC k_leaf_hash(const uint64_t *_
 // 7 % below the same loop with a constant count (tools/leaf_ubench L0: 2.87
 // vs 2.67 Gperm/s per 86-proof wires launch)
 template <uint32_t NC>
-__global__ void __launch_bounds__(256) QP_HASH_OCC k_leaf_hash_t(const uint64_t *__restrict__ cols, uint64_t stride,
+__global__ void __launch_bounds__(256) k_leaf_hash_t(const uint64_t *__restrict__ cols, uint64_t stride,
                                                                  uint64_t *__restrict__ dig, uint32_t N,
                                                                  uint64_t c_bstride, uint64_t d_bstride) {
   const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
@@ -101,42 +84,6 @@ __global__ void __launch_bounds__(256) QP_HASH_OCC k_leaf_hash_t(const uint64_t 
   for (int k = 0; k < 4; k++) o[k] = psd::canon(s[k]);
 }
 
-// leaves 2j and 2j+1 and their parent in one lane: the first tree level runs
-// at the leaf kernel's occupancy instead of as its own launch (level 1 of a
-// tree sits at node offset N)
-__global__ void __launch_bounds__(256) k_leaf_hash2(const uint64_t *__restrict__ cols, uint64_t stride, uint32_t ncols,
-                                                    const uint64_t *__restrict__ salt, uint32_t nsalt,
-                                                    uint64_t *__restrict__ dig, uint32_t N, uint64_t c_bstride,
-                                                    uint64_t s_bstride, uint64_t d_bstride) {
-  const uint32_t j = blockIdx.x * blockDim.x + threadIdx.x;
-  if (2 * j >= N) return;
-  cols += blockIdx.y * c_bstride;
-  if (salt) salt += blockIdx.y * s_bstride;
-  dig += blockIdx.y * d_bstride;
-  uint64_t s[12], d0[4];
-  leaf_digest(cols, stride, ncols, salt, nsalt, 2 * j, s);
-#pragma unroll
-  for (int k = 0; k < 4; k++) d0[k] = s[k];
-  leaf_digest(cols, stride, ncols, salt, nsalt, 2 * j + 1, s);
-  uint64_t *o = dig + (uint64_t)j * 8;
-#pragma unroll
-  for (int k = 0; k < 4; k++) {
-    o[k] = d0[k];
-    o[4 + k] = s[k];
-  }
-  // two_to_one(left, right) = permute([left, right, 0, 0, 0, 0])[0..4]
-#pragma unroll
-  for (int k = 3; k >= 0; k--) {
-    s[4 + k] = s[k];
-    s[k] = d0[k];
-  }
-#pragma unroll
-  for (int k = 8; k < 12; k++) s[k] = 0;
-  psd::permute_nc(s);
-  uint64_t *p = dig + ((uint64_t)N + j) * 4;
-#pragma unroll
-  for (int k = 0; k < 4; k++) p[k] = psd::canon(s[k]);
-}
 
 // 1..9 tree levels per launch: a block takes B = min(256, count) nodes of
 // level k0 (their 2B children read from HBM), then folds them level by level
@@ -186,7 +133,7 @@ __global__ void __launch_bounds__(256) k_merkle_levels(uint64_t *__restrict__ di
 // one wide tree level: lane t hashes children 2t, 2t+1 of level k-1 into node t
 // of level k (no LDS, no level loop: 69 VGPRs = 7 waves/SIMD against the
 // folding kernel's 103 = 4)
-__global__ void __launch_bounds__(256) QP_HASH_OCC k_merkle_level(uint64_t *__restrict__ digests, uint32_t log_N, uint32_t k,
+__global__ void __launch_bounds__(256) k_merkle_level(uint64_t *__restrict__ digests, uint32_t log_N, uint32_t k,
                                                       uint64_t d_bstride) {
   const uint32_t t = blockIdx.x * blockDim.x + threadIdx.x;
   if (t >= (1u << (log_N - k))) return;
@@ -237,46 +184,34 @@ __global__ void __launch_bounds__(256) k_merkle_level_row(uint64_t *__restrict__
   if (l16 < 4) o[l16] = psd::canon(x);
 }
 
-#ifndef QP_MERKLE_SINGLE
-#define QP_MERKLE_SINGLE 1
-#endif
 // levels of at most this many nodes (over all proofs of the launch) run one
 // wave per node (k_merkle_level_coop) in launches of at most
-// QP_MERKLE_COOP_NBAT proofs: the latency-bound small batches of the
+// MERKLE_COOP_NBAT proofs: the latency-bound small batches of the
 // aggregation tree's upper levels (one aggregation proof 12.5 -> 10.8 ms,
 // 256-leaf subtree 0.42 -> 0.405 s); the leaf bench's 86-proof launches, which
 // share a saturated GPU, keep the one-lane and fused forms (1184 vs 1200
 // proofs/s with coop there; profiles/r05_ab_merkle_coop.log).
 // The row form (k_merkle_level_row: four nodes per wave, DPP broadcasts) takes
-// levels up to QP_MERKLE_ROW_MAX nodes: 256-leaf subtree 0.387 -> 0.361-0.365 s
+// levels up to MERKLE_ROW_MAX nodes: 256-leaf subtree 0.387 -> 0.361-0.365 s
 // with the row forms of the FRI leaves, the sliced openings and the per-coset
 // LDE of few columns (profiles/r05_ab_small_batch.log).
-// QPGPU_MERKLE_COOP overrides the node bound, 0 = never
-#ifndef QP_MERKLE_COOP_MAX
-#define QP_MERKLE_COOP_MAX 8192
-#endif
-#ifndef QP_MERKLE_COOP_NBAT
-#define QP_MERKLE_COOP_NBAT 32
-#endif
-#ifndef QP_MERKLE_ROW_MAX
-#define QP_MERKLE_ROW_MAX 32768
-#endif
-// QPGPU_MERKLE_ROW=0: the one-wave-per-node form instead of the row form
-static bool merkle_row() {  // read per tree: tests switch it in one process
-  const char *e = getenv("QPGPU_MERKLE_ROW");
-  return !(e && e[0] == '0');
-}
-static uint32_t merkle_coop_max(bool row) {
-  const char *e = getenv("QPGPU_MERKLE_COOP");
-  return e && *e ? (uint32_t)strtoul(e, nullptr, 10) : row ? (uint32_t)QP_MERKLE_ROW_MAX : (uint32_t)QP_MERKLE_COOP_MAX;
+// (path hook merkle_coop overrides the node bound, 0 = never)
+constexpr long MERKLE_COOP_MAX = 8192, MERKLE_COOP_NBAT = 32, MERKLE_ROW_MAX = 32768;
+// trees narrower than 2^MERKLE_FUSE_LOG nodes per level finish in one launch
+// (one wave per block at 6, so no wave idles at the level barriers)
+constexpr uint32_t MERKLE_FUSE_LOG = 6;
+// path hook merkle_row=0: the one-wave-per-node form instead of the row form
+// (read per tree: tests switch it in one process)
+static bool merkle_row() { return path_opt("merkle_row", 1) != 0; }
+static uint64_t merkle_coop_max(bool row) {
+  return (uint64_t)path_opt("merkle_coop", row ? MERKLE_ROW_MAX : MERKLE_COOP_MAX);
 }
 
 void leaf_hash(const uint64_t *cols, uint64_t stride, uint32_t ncols, const uint64_t *salt, uint32_t nsalt,
                uint64_t *digests, uint32_t N, uint32_t nbat, uint64_t c_bstride, uint64_t s_bstride,
                uint64_t d_bstride, hipStream_t s) {
   dim3 grid((N + 255) / 256, nbat);
-  const char *lt = getenv("QPGPU_LEAF_T");
-  const bool generic = lt && lt[0] == '0';
+  const bool generic = path_opt("leaf_t", 1) == 0;  // path hook: the any-width form
   if (!nsalt && !generic) {
     switch (ncols) {
       case 135: k_leaf_hash_t<135><<<grid, 256, 0, s>>>(cols, stride, digests, N, c_bstride, d_bstride); return;
@@ -293,9 +228,8 @@ void merkle_tree_from(uint64_t *digests, uint32_t log_N, uint32_t cap_h, uint32_
   const uint32_t K = log_N - cap_h;  // levels above the leaves
   const bool row = merkle_row();
   const uint64_t coop_max = merkle_coop_max(row);
-  // QPGPU_MERKLE_NBAT: the batch size up to which the cooperative forms apply
-  const char *nbe = getenv("QPGPU_MERKLE_NBAT");
-  const uint32_t coop_nbat = nbe && *nbe ? (uint32_t)strtoul(nbe, nullptr, 10) : (uint32_t)QP_MERKLE_COOP_NBAT;
+  // the batch size up to which the cooperative forms apply (path hook merkle_nbat)
+  const uint64_t coop_nbat = (uint64_t)path_opt("merkle_nbat", MERKLE_COOP_NBAT);
   for (uint32_t k0 = first_level; k0 <= K;) {
     const uint32_t lc = log_N - k0;  // log2(nodes at level k0)
     if (nbat <= coop_nbat && ((uint64_t)nbat << lc) <= coop_max) {
@@ -309,10 +243,10 @@ void merkle_tree_from(uint64_t *digests, uint32_t log_N, uint32_t cap_h, uint32_
     const uint32_t lb = lc < 8 ? lc : 8;
     // wide levels one launch each (a fused block would idle all but one
     // wave through its lower levels: measured 165 -> 222 ms per bench run);
-    // from 2^QP_MERKLE_FUSE_LOG nodes per tree down, the rest of the tree in one launch
-    const uint32_t nl = lc > QP_MERKLE_FUSE_LOG ? 1 : ((lb + 1) < (K - k0 + 1) ? (lb + 1) : (K - k0 + 1));
+    // from 2^MERKLE_FUSE_LOG nodes per tree down, the rest of the tree in one launch
+    const uint32_t nl = lc > MERKLE_FUSE_LOG ? 1 : ((lb + 1) < (K - k0 + 1) ? (lb + 1) : (K - k0 + 1));
     dim3 grid(1u << (lc - lb), nbat);
-    if (QP_MERKLE_SINGLE && nl == 1)
+    if (nl == 1)  // one level: the single-level kernel
       k_merkle_level<<<grid, 1u << lb, 0, s>>>(digests, log_N, k0, d_bstride);
     else
       k_merkle_levels<<<grid, 1u << lb, 0, s>>>(digests, log_N, k0, nl, d_bstride);
@@ -328,14 +262,9 @@ void merkle_tree(uint64_t *digests, uint32_t log_N, uint32_t cap_h, uint32_t nba
 uint32_t leaf_hash_first(const uint64_t *cols, uint64_t stride, uint32_t ncols, const uint64_t *salt, uint32_t nsalt,
                          uint64_t *digests, uint32_t log_N, uint32_t cap_h, uint32_t nbat, uint64_t c_bstride,
                          uint64_t s_bstride, uint64_t d_bstride, hipStream_t s) {
-  const uint32_t N = 1u << log_N;
-  if (!QP_LEAF_PAIRS || log_N <= cap_h) {
-    leaf_hash(cols, stride, ncols, salt, nsalt, digests, N, nbat, c_bstride, s_bstride, d_bstride, s);
-    return 1;
-  }
-  dim3 grid((N / 2 + 255) / 256, nbat);
-  k_leaf_hash2<<<grid, 256, 0, s>>>(cols, stride, ncols, salt, nsalt, digests, N, c_bstride, s_bstride, d_bstride);
-  return 2;
+  (void)cap_h;
+  leaf_hash(cols, stride, ncols, salt, nsalt, digests, 1u << log_N, nbat, c_bstride, s_bstride, d_bstride, s);
+  return 1;
 }
 
 void leaf_hash_tree(const uint64_t *cols, uint64_t stride, uint32_t ncols, const uint64_t *salt, uint32_t nsalt,

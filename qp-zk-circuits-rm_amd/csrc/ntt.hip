@@ -15,26 +15,14 @@
 #include "kernels.h"
 #include "ntt_device.h"
 #include "ntt16.h"
+#include "paths.h"
 
 // occupancy target of the LDS NTT kernels (64 KiB LDS per size-2^13 workgroup
 // allows 2 workgroups = 4 waves per SIMD; uncapped, the compiler spends ~165
-// VGPRs and only one workgroup fits per CU).  QP_NTT_WAVES=0: no cap.
-#ifndef QP_NTT_WAVES
-#define QP_NTT_WAVES 4
-#endif
-#if QP_NTT_WAVES
-#define QP_NTT_OCC __attribute__((amdgpu_waves_per_eu(QP_NTT_WAVES)))
-#else
-#define QP_NTT_OCC
-#endif
+// VGPRs and only one workgroup fits per CU)
+#define QP_NTT_OCC __attribute__((amdgpu_waves_per_eu(4)))
 
 namespace qpk {
-
-// A/B switch for measurements: QPGPU_LDE_PERCOSET=1 selects the per-coset LDE
-static bool getenv_flag(const char *name) {
-  const char *v = getenv(name);
-  return v && v[0] && v[0] != '0';
-}
 
 __global__ void k_twiddles(uint64_t *fwd, uint64_t *inv, uint64_t w, uint64_t wi, uint32_t half) {
   uint32_t j = blockIdx.x * blockDim.x + threadIdx.x;
@@ -65,12 +53,6 @@ __global__ void k_merged_twiddles(uint64_t *mtw, const uint64_t *__restrict__ tw
   mtw[i] = nt::tw_pow(tw, t * (s + (nt::brev4(m) << rate_bits)), logN);
 }
 
-// coset steps of k_lde_cosets for one (log_n, rate): utw[k] = w_N^k, k < n
-__global__ void k_coset_steps(uint64_t *utw, const uint64_t *__restrict__ tw, uint32_t log_n, uint32_t rate_bits) {
-  const uint32_t k = blockIdx.x * blockDim.x + threadIdx.x;
-  if (k < (1u << log_n)) utw[k] = nt::tw_pow(tw, k, log_n + rate_bits);
-}
-
 hipError_t twiddles_init(Twiddles &t, hipStream_t s) {
   uint32_t half = 1u << (TW_LOG - 1);
   hipError_t e = hipMalloc(&t.fwd, half * 8ull);
@@ -92,16 +74,6 @@ hipError_t twiddles_init(Twiddles &t, hipStream_t s) {
   if (e) return e;
   e = hipMemcpyAsync(t.ptw, ptw.data(), ptw.size() * 8, hipMemcpyHostToDevice, s);
   if (e) return e;
-  std::vector<uint64_t> ptw8(ptw8_offset(LDE_MAX_RATE + 1));
-  for (uint32_t r = 1; r <= LDE_MAX_RATE; r++) {
-    const uint64_t wr = gl::root_of_unity(3 + r);
-    for (uint32_t sc = 0; sc < (1u << r); sc++)
-      for (uint32_t m = 0; m < 8; m++) ptw8[ptw8_offset(r) + 8 * sc + m] = gl::pow(wr, (uint64_t)sc * m);
-  }
-  e = hipMalloc(&t.ptw8, ptw8.size() * 8);
-  if (e) return e;
-  e = hipMemcpyAsync(t.ptw8, ptw8.data(), ptw8.size() * 8, hipMemcpyHostToDevice, s);
-  if (e) return e;
   const uint32_t npt = pt_offset(TW_LOG + 1);
   if ((e = hipMalloc(&t.pt_fwd, npt * 8ull)) || (e = hipMalloc(&t.pt_inv, npt * 8ull))) return e;
   k_pass_twiddles<<<(npt + 255) / 256, 256, 0, s>>>(t.pt_fwd, t.fwd, npt);
@@ -116,16 +88,6 @@ hipError_t twiddles_init(Twiddles &t, hipStream_t s) {
   for (uint32_t ln = LDE_COSETS_MIN_LOG; ln <= LDE_COSETS_MAX_LOG; ln++)
     for (uint32_t r = 1; r <= LDE_MAX_RATE && ln + r <= TW_LOG; r++)
       k_merged_twiddles<<<((1u << (ln + r)) + 255) / 256, 256, 0, s>>>(t.mtw + t.mtw_off[ln][r], t.fwd, ln, r);
-  uint64_t nu = 0;
-  for (uint32_t ln = LDE_COSETS_MIN_LOG; ln <= LDE_COSETS_MAX_LOG; ln++)
-    for (uint32_t r = 1; r <= LDE_MAX_RATE && ln + r <= TW_LOG; r++) {
-      t.utw_off[ln][r] = nu;
-      nu += 1ull << ln;
-    }
-  if ((e = hipMalloc(&t.utw, nu * 8))) return e;
-  for (uint32_t ln = LDE_COSETS_MIN_LOG; ln <= LDE_COSETS_MAX_LOG; ln++)
-    for (uint32_t r = 1; r <= LDE_MAX_RATE && ln + r <= TW_LOG; r++)
-      k_coset_steps<<<((1u << ln) + 255) / 256, 256, 0, s>>>(t.utw + t.utw_off[ln][r], t.fwd, ln, r);
   if ((e = hipGetLastError())) return e;
   return hipStreamSynchronize(s);
 }
@@ -134,12 +96,10 @@ void twiddles_free(Twiddles &t) {
   if (t.fwd) (void)hipFree(t.fwd);
   if (t.inv) (void)hipFree(t.inv);
   if (t.ptw) (void)hipFree(t.ptw);
-  if (t.ptw8) (void)hipFree(t.ptw8);
   if (t.pt_fwd) (void)hipFree(t.pt_fwd);
   if (t.pt_inv) (void)hipFree(t.pt_inv);
   if (t.mtw) (void)hipFree(t.mtw);
-  if (t.utw) (void)hipFree(t.utw);
-  t.fwd = t.inv = t.ptw = t.ptw8 = t.pt_fwd = t.pt_inv = t.mtw = t.utw = nullptr;
+  t.fwd = t.inv = t.ptw = t.pt_fwd = t.pt_inv = t.mtw = nullptr;
 }
 
 __global__ void __launch_bounds__(512) QP_NTT_OCC k_intt(const uint64_t *__restrict__ in, uint64_t in_stride,
@@ -184,47 +144,29 @@ __global__ void __launch_bounds__(512) QP_NTT_OCC k_lde(const uint64_t *__restri
 // Coset-fused LDE: one workgroup per column produces all B = 2^r cosets, so
 // the n coefficients are read from HBM once (the per-coset kernel above reads
 // them B times) and scaled by shift^k once.  n = 16 T (T = 2^LOG_T threads):
-// thread t holds a_m = c_{t+Tm} shift^{t+Tm}, m < 16, in registers — exactly
+// thread t holds a_m = c_{t+Tm} shift^{t+Tm}, m < 16, in registers -- exactly
 // the inputs of its first radix-16 DIF butterfly.  For coset s the inputs are
-// a_m w_N^{s(t+Tm)}: the registers step from coset s-1 to s by one product
-// with w_N^{t+Tm} (utw, n words per (log_n, r)), and after the 16-point DFT
-// the pass's own twiddle w_n^{t brev4(m)} (pt for S = n) applies unchanged to
-// every coset.  Both tables are coset-independent and together n + n words
-// (128 KiB at n = 2^13), so they stay in L2 across the columns; the same 31
-// products per 16 elements as the MTW form, which multiplies by w_{16B}^{sm}
-// before and by the merged w_N^{t(s + B brev4(m))} (N words, 512 KiB at
-// n = 2^13, evicted by the streaming output) after the DFT.
-// The remaining levels run in LDS (ntt_lds_from); output rows in leaf order.
-// QP_LDE_MULK=0 (default): the coset LDE's twiddle products one at a time
-// rather than as interleaved triples (nt::mul_rows): fewer live temporaries at
-// the 128-VGPR cap (72 -> 48 B of spill per lane); 4.33 -> 4.18 ms per
-// 86-proof launch, while the iNTT keeps the triples (0.86 vs 0.93 ms;
-// profiles/r04_lde_ab.log)
-#ifndef QP_LDE_MULK
-#define QP_LDE_MULK 0
-#endif
-// QP_LDE_ALDS=3 (default): the last 3 shifted coefficients in LDS past the
-// transform (12 KB per 8192-point workgroup: 2 still fit per CU); spill
-// 48 -> 12 B per lane, 4.11 -> 4.06 ms per 86-proof launch
-// (profiles/r04_lde_ab.log)
-#ifndef QP_LDE_ALDS
-#define QP_LDE_ALDS 3
-#endif
-// QP_LDE_WAVELOCAL=1: the n = 2^13 coset LDE's last two passes wave-local
-// (two workgroup barriers per coset instead of four)
-#ifndef QP_LDE_WAVELOCAL
-#define QP_LDE_WAVELOCAL 1
-#endif
-// QP_LDE_EARLY_SYNC=1 (wave-local form): the coset's closing barrier moved
-// after the next coset's register work
-#ifndef QP_LDE_EARLY_SYNC
-#define QP_LDE_EARLY_SYNC 1
-#endif
-// MODE (QPGPU_LDE_MODE): 0 = MTW (default; measured 548 vs 701 us per
-// 64-column launch for mode 1 at n = 2^13, profiles/r04_lde_ab.log), 1 =
-// factored with both tables re-read per coset, 2 = factored with the coset
-// steps held in registers, 3 = factored with both tables held in registers.
-template <int LOG_T, int MODE>
+// a_m w_N^{s(t+Tm)} = a_m w_N^{st} w_{16B}^{sm}: the registers are multiplied
+// by w_{16B}^{sm} (ptw) before the 16-point DFT and by the merged twiddle
+// w_N^{t(s + B brev4(m))} (mtw: N words per (log_n, r), read from L2 by every
+// column's workgroup) after it.  The remaining levels run in LDS; output rows
+// in leaf order.
+//   * twiddle products one at a time (nt::mul_rows<0>), not as interleaved
+//     triples: fewer live temporaries at the 128-VGPR cap (72 -> 48 B of spill
+//     per lane; 4.33 -> 4.18 ms per 86-proof launch, profiles/r04_lde_ab.log)
+//   * the last LDE_ALDS shifted coefficients in LDS past the transform
+//     (12 KB per 8192-point workgroup: 2 still fit per CU); spill 48 -> 12 B
+//     per lane, 4.11 -> 4.06 ms per 86-proof launch (profiles/r04_lde_ab.log)
+//   * n = 2^13: the last two passes wave-local (two workgroup barriers per
+//     coset instead of four), the closing barrier after the next coset's
+//     register work (profiles/r05_ab_lde_wavelocal.log)
+//   * factored first-pass tables (coset steps and pass twiddles, held in
+//     registers or re-read) measured slower: 701 vs 548 us per 64-column
+//     launch at n = 2^13 (profiles/r04_lde_ab.log); so did a radix-8 form at
+//     twice the threads (4.63 vs 4.48 ms per 64-proof launch: LDS stalls,
+//     profiles/r02_ab_lde_radix8.log)
+constexpr int LDE_ALDS = 3;
+template <int LOG_T>
 __global__ void __launch_bounds__(1 << LOG_T) QP_NTT_OCC k_lde_cosets(const uint64_t *__restrict__ coeffs, uint64_t c_stride,
                                                           uint64_t c_bstride, uint64_t *__restrict__ out,
                                                           uint64_t o_stride, uint64_t o_bstride, uint32_t rate_bits,
@@ -250,72 +192,35 @@ __global__ void __launch_bounds__(1 << LOG_T) QP_NTT_OCC k_lde_cosets(const uint
   }
   const uint32_t B = 1u << rate_bits;
   const uint64_t *pw = ptw + ptw_offset(rate_bits);
-  // MTW = false: utw = the coset steps w_N^{t+Tm} (mtw argument), p1 = the
-  // first pass's twiddles w_n^{t brev4(m)}
-  const uint64_t *ut = mtw + t, *p1 = pt + pt_offset(LOG_N) + t;
-  constexpr bool MTW = MODE == 0;
-  // QP_LDE_ALDS = K > 0: the last K shifted coefficients live in LDS past the
-  // transform's words instead of VGPRs across the coset loop (fewer spills;
-  // the launch adds K*T*8 bytes of LDS)
+  // the last LDE_ALDS shifted coefficients live in LDS past the transform's
+  // words instead of VGPRs across the coset loop (the launch adds their bytes)
   uint64_t *alds = lds + ntt_lds_words(1u << LOG_N);
-  if constexpr (QP_LDE_ALDS > 0) {
+  if constexpr (LDE_ALDS > 0) {
 #pragma unroll
-    for (int m = 16 - QP_LDE_ALDS; m < 16; m++) alds[(m - (16 - QP_LDE_ALDS)) * T + t] = a[m];
-  }
-  // coset-independent tables held in registers (modes 2 and 3)
-  uint64_t hu[16], hp[16];
-  if constexpr (MODE >= 2) {
-#pragma unroll
-    for (int m = 0; m < 16; m++) hu[m] = ut[T * m];
-  }
-  if constexpr (MODE == 3) {
-#pragma unroll
-    for (int m = 0; m < 16; m++) hp[m] = p1[T * m];
+    for (int m = 16 - LDE_ALDS; m < 16; m++) alds[(m - (16 - LDE_ALDS)) * T + t] = a[m];
   }
   for (uint32_t s = 0; s < B; s++) {
     uint64_t r[16];
-    if constexpr (MTW) {
 #pragma unroll
-      for (int m = 0; m < 16; m++)
-        r[m] = m >= 16 - QP_LDE_ALDS ? alds[(m - (16 - QP_LDE_ALDS)) * T + t] : a[m];
-      nt::mul_rows<QP_LDE_MULK>(r, [&](int m) { return pw[16 * s + m]; });
-      nt::dft16<false>(r);
-      // merged twiddles w_N^{t(s + B brev4(m))}: row (s, m) of the table, lane t
-      // (a product by w^0 = 1 returns its input unchanged)
-      const uint64_t *ms = mtw + (uint64_t)16 * T * s + t;
-      if (s) r[0] = nt::mul(r[0], ms[0]);
-      nt::mul_rows<QP_LDE_MULK>(r, [&](int m) { return ms[T * m]; });
-    } else {
-      if (s) {
-        // a_m w_N^{s(t+Tm)} from coset s - 1's registers
-        if constexpr (MODE >= 2) {
-          a[0] = nt::mul(a[0], hu[0]);
-          nt::mul_rows<QP_LDE_MULK>(a, [&](int m) { return hu[m]; });
-        } else {
-          a[0] = nt::mul(a[0], ut[0]);
-          nt::mul_rows<QP_LDE_MULK>(a, [&](int m) { return ut[T * m]; });
-        }
-      }
-#pragma unroll
-      for (int m = 0; m < 16; m++) r[m] = a[m];
-      nt::dft16<false>(r);
-      if (t) {
-        if constexpr (MODE == 3)
-          nt::mul_rows<QP_LDE_MULK>(r, [&](int m) { return hp[m]; });
-        else
-          nt::mul_rows<QP_LDE_MULK>(r, [&](int m) { return p1[T * m]; });
-      }
-    }
+    for (int m = 0; m < 16; m++)
+      r[m] = m >= 16 - LDE_ALDS ? alds[(m - (16 - LDE_ALDS)) * T + t] : a[m];
+    nt::mul_rows<0>(r, [&](int m) { return pw[16 * s + m]; });
+    nt::dft16<false>(r);
+    // merged twiddles w_N^{t(s + B brev4(m))}: row (s, m) of the table, lane t
+    // (a product by w^0 = 1 returns its input unchanged)
+    const uint64_t *ms = mtw + (uint64_t)16 * T * s + t;
+    if (s) r[0] = nt::mul(r[0], ms[0]);
+    nt::mul_rows<0>(r, [&](int m) { return ms[T * m]; });
     // wave-local tail: the barrier that keeps this coset's writes from
     // overtaking other waves' reads of the previous coset's words sits here,
     // after this wave's registers are ready, so a wave that finished its
     // stores early transforms the next coset's 16 values instead of idling
-    if constexpr (QP_LDE_WAVELOCAL && QP_LDE_EARLY_SYNC && LOG_N == 13 && LOG_T == 9)
+    if constexpr (LOG_N == 13 && LOG_T == 9)
       if (s) __syncthreads();
 #pragma unroll
     for (int m = 0; m < 16; m++) lds[nt::lp(t) + nt::lp(T * m)] = r[m];
     __syncthreads();
-    if constexpr (QP_LDE_WAVELOCAL && LOG_N == 13 && LOG_T == 9) {
+    if constexpr (LOG_N == 13 && LOG_T == 9) {
       // n = 2^13, T = 512: after the cross-wave pass (stride-32 groups of each
       // 512-element block) wave w holds elements [1024 w, 1024 w + 1024), so the
       // stride-2 pass and the last radix-2 level run on the wave's own LDS
@@ -330,7 +235,7 @@ __global__ void __launch_bounds__(1 << LOG_T) QP_NTT_OCC k_lde_cosets(const uint
         nt::dft16<false>(q);
         if (tt) {
           const uint64_t *ptS = pt + pt_offset(9) + tt;
-          nt::mul_rows<QP_LDE_MULK>(q, [&](int m) { return ptS[m * 32]; });
+          nt::mul_rows<0>(q, [&](int m) { return ptS[m * 32]; });
         }
 #pragma unroll
         for (int m = 0; m < 16; m++) base[nt::lp(m * 32)] = q[m];
@@ -366,7 +271,6 @@ __global__ void __launch_bounds__(1 << LOG_T) QP_NTT_OCC k_lde_cosets(const uint
         dst[g0] = nt::canon(q[0]);
         dst[g0 + 1] = nt::canon(q[1]);
       }
-      if constexpr (!QP_LDE_EARLY_SYNC) __syncthreads();
       continue;
     }
     // the last radix-2^g levels (g = LOG_N mod 4) run in the store loop: each
@@ -376,7 +280,7 @@ __global__ void __launch_bounds__(1 << LOG_T) QP_NTT_OCC k_lde_cosets(const uint
     // the LDS passes (launched with T threads) leave exactly the G levels the
     // store loop runs
     static_assert(nt::lds_levels_left(LOG_N, LOG_T, T) == G, "LDS passes and the store loop disagree");
-    nt::ntt_lds_from<false, false, QP_LDE_MULK>(lds, LOG_N, LOG_T, pt);
+    nt::ntt_lds_from<false, false, 0>(lds, LOG_N, LOG_T, pt);
     uint64_t *dst = dst0 + ((uint64_t)gl::rev_bits(s, rate_bits) << LOG_N);
     if constexpr (G == 0) {
 #pragma unroll
@@ -394,62 +298,6 @@ __global__ void __launch_bounds__(1 << LOG_T) QP_NTT_OCC k_lde_cosets(const uint
         for (uint32_t e = 0; e < S; e++) dst[g0 + e] = nt::canon(r[e]);
       }
     }
-    __syncthreads();
-  }
-}
-
-// Radix-8 form of k_lde_cosets (n = 8 T, T = 2^LOG_T threads): thread t holds
-// a_m = c_{t+Tm} shift^{t+Tm}, m < 8; per coset one pre-twist by
-// w_{8B}^{sm}, an 8-point DFT in registers, the merged twiddle
-// w_N^{t(s + B brev3(m))}, then radix-8 passes in LDS.  Twice the threads per
-// column at the same LDS: 8 waves per SIMD.  Measured (tools/ab_round2_2.sh,
-// profiles/r02_ab_lde_radix8.log): 4.63 vs 4.48 ms per 64-proof launch — the
-// doubled occupancy turns into LDS stalls (+33 % LDS instructions, 2.2x bank-
-// conflict cycles, 3x SQ_WAIT_INST_ANY), so the radix-16 form stays the
-// default (QP_LDE_RADIX8=1 selects this one).
-#ifndef QP_LDE_RADIX8
-#define QP_LDE_RADIX8 0
-#endif
-template <int LOG_T>
-__global__ void __launch_bounds__(1 << LOG_T) __attribute__((amdgpu_waves_per_eu(8)))
-k_lde_cosets8(const uint64_t *__restrict__ coeffs, uint64_t c_stride, uint64_t c_bstride, uint64_t *__restrict__ out,
-              uint64_t o_stride, uint64_t o_bstride, uint32_t rate_bits, uint64_t shift, uint64_t shift_T,
-              const uint64_t *__restrict__ tw, const uint64_t *__restrict__ ptw8) {
-  constexpr uint32_t T = 1u << LOG_T, LOG_N = LOG_T + 3;
-  extern __shared__ __attribute__((aligned(16))) uint64_t lds[];
-  const uint32_t t = threadIdx.x;
-  const uint64_t *src = coeffs + blockIdx.y * c_bstride + (uint64_t)blockIdx.x * c_stride;
-  uint64_t *dst0 = out + blockIdx.y * o_bstride + (uint64_t)blockIdx.x * o_stride;
-  uint64_t a[8];
-#pragma unroll
-  for (int m = 0; m < 8; m++) a[m] = src[t + T * m];
-  {
-    uint64_t f = gl::pow(shift, t);
-#pragma unroll
-    for (int m = 0; m < 8; m++) {
-      a[m] = nt::mul(a[m], f);
-      f = nt::mul(f, shift_T);
-    }
-  }
-  const uint32_t logN = LOG_N + rate_bits, B = 1u << rate_bits;
-  const uint64_t *pt = ptw8 + ptw8_offset(rate_bits);
-  for (uint32_t s = 0; s < B; s++) {
-    uint64_t r[8];
-    r[0] = a[0];
-#pragma unroll
-    for (int m = 1; m < 8; m++) r[m] = nt::mul(a[m], pt[8 * s + m]);
-    nt::dft8<false>(r);
-#pragma unroll
-    for (int m = 0; m < 8; m++) {
-      const uint32_t e = t * (s + (nt::brev3(m) << rate_bits));
-      if (e) r[m] = nt::mul(r[m], nt::tw_pow(tw, e, logN));
-      lds[nt::lp(t) + nt::lp(T * m)] = r[m];
-    }
-    __syncthreads();
-    nt::ntt8_lds_from<false>(lds, LOG_N, LOG_T, tw);
-    uint64_t *dst = dst0 + ((uint64_t)gl::rev_bits(s, rate_bits) << LOG_N);
-#pragma unroll
-    for (int m = 0; m < 8; m++) dst[t + T * m] = nt::canon(lds[nt::lp(t) + nt::lp(T * m)]);
     __syncthreads();
   }
 }
@@ -577,9 +425,7 @@ void intt(const Twiddles &t, const uint64_t *in, uint64_t in_stride, uint64_t *o
                                                          in_bstride, out_bstride);
 }
 
-#ifndef QP_LDE_FEW
-#define QP_LDE_FEW 256
-#endif
+constexpr long LDE_FEW = 256;
 void lde(const Twiddles &t, const uint64_t *coeffs, uint64_t c_stride, uint64_t *out, uint64_t o_stride,
          uint32_t ncols, uint32_t log_n, uint32_t rate_bits, uint64_t shift, uint32_t nbat, uint64_t c_bstride,
          uint64_t o_bstride, hipStream_t s) {
@@ -596,40 +442,21 @@ void lde(const Twiddles &t, const uint64_t *coeffs, uint64_t c_stride, uint64_t 
   }
   // n = 2^14 (the aggregation circuits): 1024 threads x 16 and 135 KB of LDS,
   // one workgroup per CU
-  // fewer columns x proofs than QP_LDE_FEW (QPGPU_LDE_FEW overrides, 0 =
-  // never): one workgroup per coset (k_lde), since one per column would leave
-  // most CUs idle while each walks its 2^rate cosets in turn (small
-  // aggregation batches, FRI layers)
-  const char *fe = getenv("QPGPU_LDE_FEW");
-  const uint64_t few = fe && *fe ? strtoull(fe, nullptr, 10) : QP_LDE_FEW;
+  // fewer columns x proofs than LDE_FEW (path hook lde_few, 0 = never): one
+  // workgroup per coset (k_lde), since one per column would leave most CUs
+  // idle while each walks its 2^rate cosets in turn (small aggregation
+  // batches, FRI layers)
+  const uint64_t few = (uint64_t)path_opt("lde_few", LDE_FEW);
   if (rate_bits >= 1 && rate_bits <= LDE_MAX_RATE && log_n >= LDE_COSETS_MIN_LOG && log_n <= LDE_COSETS_MAX_LOG &&
-      log_n + rate_bits <= TW_LOG && (uint64_t)ncols * nbat >= few &&
-      !getenv_flag("QPGPU_LDE_PERCOSET")) {
+      log_n + rate_bits <= TW_LOG && (uint64_t)ncols * nbat >= few) {
     dim3 g(ncols, nbat);
-    const size_t lds_bytes = (size_t)8 * (qpk::ntt_lds_words(1u << log_n) + QP_LDE_ALDS * (1u << (log_n - 4)));
-    if (QP_LDE_RADIX8 && log_n == 13) {
-      const uint64_t shift_T8 = gl::pow(shift, 1u << (log_n - 3));
-      k_lde_cosets8<10><<<g, 1024, lds_bytes, s>>>(coeffs, c_stride, c_bstride, out, o_stride, o_bstride, rate_bits,
-                                                   shift, shift_T8, t.fwd, t.ptw8);
-      return;
-    }
+    const size_t lds_bytes = (size_t)8 * (qpk::ntt_lds_words(1u << log_n) + LDE_ALDS * (1u << (log_n - 4)));
     const uint32_t T = 1u << (log_n - 4);
     const uint64_t shift_T = gl::pow(shift, T);
-    // QPGPU_LDE_MODE=1..3: the factored forms (A/B)
-    static const int mode = [] {
-      const char *v = getenv("QPGPU_LDE_MODE");
-      return v && *v >= '0' && *v <= '3' ? *v - '0' : 0;
-    }();
-#define QP_LDE_LAUNCH(LT, M, TAB)                                                                                   \
-  k_lde_cosets<LT, M><<<g, 1u << LT, lds_bytes, s>>>(coeffs, c_stride, c_bstride, out, o_stride, o_bstride,        \
-                                                     rate_bits, shift, shift_T, TAB, t.pt_fwd, t.ptw)
-#define QP_LDE_COSETS(LT)                                                                                          \
-  switch (mode) {                                                                                                  \
-    case 1: QP_LDE_LAUNCH(LT, 1, t.utw + t.utw_off[log_n][rate_bits]); break;                                      \
-    case 2: QP_LDE_LAUNCH(LT, 2, t.utw + t.utw_off[log_n][rate_bits]); break;                                      \
-    case 3: QP_LDE_LAUNCH(LT, 3, t.utw + t.utw_off[log_n][rate_bits]); break;                                      \
-    default: QP_LDE_LAUNCH(LT, 0, t.mtw + t.mtw_off[log_n][rate_bits]); break;                                     \
-  }
+    const uint64_t *mtw = t.mtw + t.mtw_off[log_n][rate_bits];
+#define QP_LDE_COSETS(LT)                                                                                   \
+  k_lde_cosets<LT><<<g, 1u << LT, lds_bytes, s>>>(coeffs, c_stride, c_bstride, out, o_stride, o_bstride, \
+                                                  rate_bits, shift, shift_T, mtw, t.pt_fwd, t.ptw)
     switch (log_n) {
       case 10: QP_LDE_COSETS(6); break;
       case 11: QP_LDE_COSETS(7); break;
@@ -638,7 +465,6 @@ void lde(const Twiddles &t, const uint64_t *coeffs, uint64_t c_stride, uint64_t 
       default: QP_LDE_COSETS(10); break;
     }
 #undef QP_LDE_COSETS
-#undef QP_LDE_LAUNCH
     return;
   }
   dim3 grid(1u << rate_bits, ncols, nbat);

@@ -30,17 +30,11 @@ namespace nt {
 
 constexpr uint64_t EPS = 0xFFFFFFFFull;
 
-// QP_NTT_CARRY (default 1): branch-free 32-bit carry chains (field_nc.h); 0:
-// the 64-bit compare-and-branch forms (A/B)
-#ifndef QP_NTT_CARRY
-#define QP_NTT_CARRY 1
-#endif
-// QP_NTT_ADD_MAD=1 (default): the wrap corrections as v_mad_u64_u32 with
-// carry-out (s + e, e = eps on a wrap): 6 instructions instead of the 8-step
-// carry chain.  LDE -4.4 %, iNTT -8 % (profiles/r03_ab_ntt_add_mad.log)
-#ifndef QP_NTT_ADD_MAD
-#define QP_NTT_ADD_MAD 1
-#endif
+// Branch-free 32-bit carry chains (field_nc.h) rather than 64-bit
+// compare-and-branch forms; additions with the wrap corrections as
+// v_mad_u64_u32 with carry-out (s + e, e = eps on a wrap): 6 instructions
+// instead of the 8-step carry chain, LDE -4.4 %, iNTT -8 %
+// (profiles/r03_ab_ntt_add_mad.log)
 __device__ __forceinline__ uint64_t add_mad(uint64_t a, uint64_t b) {
   uint32_t c0, c1;
   const uint32_t lo = __builtin_addc((uint32_t)a, (uint32_t)b, 0u, &c0);
@@ -56,32 +50,9 @@ __device__ __forceinline__ uint64_t add_mad(uint64_t a, uint64_t b) {
   return s3;
 }
 
-__device__ __forceinline__ uint64_t add(uint64_t a, uint64_t b) {
-#if QP_NTT_CARRY
-  if constexpr (QP_NTT_ADD_MAD) return add_mad(a, b);
-  return gfn::add(a, b);
-#else
-  uint64_t s = a + b;
-  if (s < b) {
-    s += EPS;
-    if (s < EPS) s += EPS;
-  }
-  return s;
-#endif
-}
+__device__ __forceinline__ uint64_t add(uint64_t a, uint64_t b) { return add_mad(a, b); }
 
-__device__ __forceinline__ uint64_t sub(uint64_t a, uint64_t b) {
-#if QP_NTT_CARRY
-  return gfn::sub(a, b);
-#else
-  uint64_t d = a - b;
-  if (a < b) {
-    uint64_t d1 = d - EPS;
-    d = d1 > d ? d1 - EPS : d1;  // second wrap when b - a > p (b non-canonical)
-  }
-  return d;
-#endif
-}
+__device__ __forceinline__ uint64_t sub(uint64_t a, uint64_t b) { return gfn::sub(a, b); }
 
 __device__ __forceinline__ uint64_t reduce(uint64_t lo, uint64_t hi) {
   const uint64_t hh = hi >> 32, hl = hi & EPS;
@@ -92,23 +63,14 @@ __device__ __forceinline__ uint64_t reduce(uint64_t lo, uint64_t hi) {
   return r + (r < t1 ? EPS : 0);
 }
 
-// general product: the asm form (5 mads + 8-op reduction, poseidon_fast.h);
-// QP_NTT_MUL_C=1: the C form the compiler schedules itself (A/B)
-#ifndef QP_NTT_MUL_C
-#define QP_NTT_MUL_C 0
-#endif
-__device__ __forceinline__ uint64_t mul(uint64_t a, uint64_t b) {
-  if constexpr (QP_NTT_MUL_C) return pf::mul_c(a, b);
-  else return pf::mul(a, b);
-}
+// general product: the asm form (5 mads + 8-op reduction, poseidon_fast.h)
+__device__ __forceinline__ uint64_t mul(uint64_t a, uint64_t b) { return pf::mul(a, b); }
 
-// r[m] *= tw(m) for m = 1..15 (a group's twiddles); QP_NTT_MULK=1 issues them
-// as five interleaved triples (pf::mulk<3>: each carry is read two products
-// later instead of after hazard pads)
-#ifndef QP_NTT_MULK
-#define QP_NTT_MULK 1
-#endif
-template <bool K = QP_NTT_MULK, class TW>
+// r[m] *= tw(m) for m = 1..15 (a group's twiddles); K = true (the LDS passes)
+// issues them as five interleaved triples (pf::mulk<3>: each carry is read two
+// products later instead of after hazard pads), K = false one at a time (the
+// coset LDE's first pass, at its register cap)
+template <bool K = true, class TW>
 __device__ __forceinline__ void mul_rows(uint64_t r[16], const TW &tw) {
   if constexpr (K) {
 #pragma unroll
@@ -144,11 +106,8 @@ __device__ __forceinline__ uint64_t sub_borrow_eps(uint32_t r0, uint32_t r1, uin
   return ((uint64_t)r1 << 32) | r0;
 }
 
-// QP_POW2_FORM (default 1): mad-based reductions for shifts E in [32, 96)
-// (10 and 9 instructions against 14 and 23 for the reduce()-based forms)
-#ifndef QP_POW2_FORM
-#define QP_POW2_FORM 1
-#endif
+// mad-based reductions for shifts E in [32, 96) (10 and 9 instructions
+// against 14 and 23 for the reduce()-based forms, which the small shifts keep)
 
 // x * 2^E for a compile-time E in [0, 192) (2^96 = -1, 2^192 = 1)
 template <int E>
@@ -157,7 +116,7 @@ __device__ __forceinline__ uint64_t mul_pow2(uint64_t x) {
     return neg(mul_pow2<E - 96>(x));
   } else if constexpr (E == 0) {
     return x;
-  } else if constexpr (QP_POW2_FORM && E >= 32 && E < 64) {
+  } else if constexpr (E >= 32 && E < 64) {
     // x 2^E = lo + 2^64 (h0 + 2^32 h1) = lo + h0 eps - h1  (h1 < 2^31)
     const uint64_t lo = x << E, hi = x >> (64 - E);
     uint64_t t, c;
@@ -170,7 +129,7 @@ __device__ __forceinline__ uint64_t mul_pow2(uint64_t x) {
     asm("v_sub_co_u32_e64 %0, %1, %2, %3" : "=v"(r0), "=s"(c) : "v"((uint32_t)t), "v"((uint32_t)(hi >> 32)));
     asm(QP_CWAIT "v_subb_co_u32_e64 %0, %1, %2, 0, %3" : "=v"(r1), "=s"(c) : "v"((uint32_t)(t >> 32)), "s"(c));
     return sub_borrow_eps(r0, r1, c);
-  } else if constexpr (QP_POW2_FORM && E >= 64) {
+  } else if constexpr (E >= 64) {
     // E = 64 + F: x 2^E = x0 2^F 2^64 + x1 2^F 2^96 = u eps - v with
     // u = x0 2^F, v = x1 2^F (< 2^63); u eps = u0 2^32 - u0 - u1, so
     // x 2^E = (u0 << 32) - S, S = u0 + u1 + v < 2^64
@@ -183,13 +142,8 @@ __device__ __forceinline__ uint64_t mul_pow2(uint64_t x) {
     asm(QP_CWAIT "v_subb_co_u32_e64 %0, %1, %2, %3, %1" : "=v"(r1), "+s"(c) : "v"((uint32_t)u), "v"((uint32_t)(S >> 32)));
     // borrow: the wrapped A - S + 2^64 >= 2^64 - S > 2^63
     return sub_borrow_eps(r0, r1, c);
-  } else if constexpr (E < 64) {
-    return reduce(x << E, x >> (64 - E));
   } else {
-    // x = x1 2^32 + x0: x 2^E = x0 2^E - x1 2^(E-64)   (2^96 = -1)
-    constexpr int F = E - 64;
-    const uint64_t x0 = x & EPS, x1 = x >> 32;
-    return sub(reduce(0, x0 << F), x1 << F);
+    return reduce(x << E, x >> (64 - E));
   }
 }
 
@@ -201,13 +155,10 @@ __device__ __forceinline__ uint64_t mul_w16(uint64_t x) {
   else return mul_pow2<(192 - 12 * J) % 192>(x);
 }
 
-// QP_NTT_ILV=1 (default): a stage's butterflies four at a time, their adds and
-// subs interleaved in one asm block each (add4 / sub4): every carry is read
-// four instructions after it is written, so the gfx950 carry hazard needs no
-// s_nop (a 16-point DFT: 694 VALU + 387 s_nop -> 660 VALU + 113 s_nop, static)
-#ifndef QP_NTT_ILV
-#define QP_NTT_ILV 1
-#endif
+// A stage's butterflies four at a time, their adds and subs interleaved in one
+// asm block each (add4 / sub4): every carry is read four instructions after it
+// is written, so the gfx950 carry hazard needs no s_nop (a 16-point DFT: 694
+// VALU + 387 s_nop -> 660 VALU + 113 s_nop, static)
 // 4 independent Goldilocks adds (non-canonical in and out, as nt::add),
 // interleaved in one asm block: every carry is read 4 instructions after it
 // is written, so no hazard pads
@@ -296,55 +247,32 @@ __device__ __forceinline__ void sub4(const uint64_t a[4], const uint64_t b[4], u
 // radix-2 DIF stage of half-width H on a register array of size 16
 template <bool INV, int H>
 __device__ __forceinline__ void stage16(uint64_t a[16]) {
-  if constexpr (QP_NTT_ILV) {
 #pragma unroll
-    for (int g = 0; g < 8; g += 4) {
-      // butterflies g..g+3: index pairs (lo_i, lo_i + H)
-      int lo[4];
+  for (int g = 0; g < 8; g += 4) {
+    // butterflies g..g+3: index pairs (lo_i, lo_i + H)
+    int lo[4];
 #pragma unroll
-      for (int i = 0; i < 4; i++) lo[i] = ((g + i) / H) * 2 * H + (g + i) % H;
-      uint64_t u[4], v[4], s[4], d[4];
+    for (int i = 0; i < 4; i++) lo[i] = ((g + i) / H) * 2 * H + (g + i) % H;
+    uint64_t u[4], v[4], s[4], d[4];
 #pragma unroll
-      for (int i = 0; i < 4; i++) {
-        u[i] = a[lo[i]];
-        v[i] = a[lo[i] + H];
-      }
-      add4(u, v, s);
-      sub4(u, v, d);
-#pragma unroll
-      for (int i = 0; i < 4; i++) {
-        a[lo[i]] = s[i];
-        switch ((lo[i] % H) * (8 / H)) {
-          case 0: a[lo[i] + H] = d[i]; break;
-          case 1: a[lo[i] + H] = mul_w16<INV, 1>(d[i]); break;
-          case 2: a[lo[i] + H] = mul_w16<INV, 2>(d[i]); break;
-          case 3: a[lo[i] + H] = mul_w16<INV, 3>(d[i]); break;
-          case 4: a[lo[i] + H] = mul_w16<INV, 4>(d[i]); break;
-          case 5: a[lo[i] + H] = mul_w16<INV, 5>(d[i]); break;
-          case 6: a[lo[i] + H] = mul_w16<INV, 6>(d[i]); break;
-          default: a[lo[i] + H] = mul_w16<INV, 7>(d[i]); break;
-        }
-      }
+    for (int i = 0; i < 4; i++) {
+      u[i] = a[lo[i]];
+      v[i] = a[lo[i] + H];
     }
-    return;
-  }
+    add4(u, v, s);
+    sub4(u, v, d);
 #pragma unroll
-  for (int k = 0; k < 16; k += 2 * H) {
-#pragma unroll
-    for (int j = 0; j < H; j++) {
-      const uint64_t u = a[k + j], v = a[k + j + H];
-      a[k + j] = add(u, v);
-      const uint64_t d = sub(u, v);
-      // w_{2H}^j = w_16^{j * 8/H}
-      switch (j * (8 / H)) {
-        case 0: a[k + j + H] = d; break;
-        case 1: a[k + j + H] = mul_w16<INV, 1>(d); break;
-        case 2: a[k + j + H] = mul_w16<INV, 2>(d); break;
-        case 3: a[k + j + H] = mul_w16<INV, 3>(d); break;
-        case 4: a[k + j + H] = mul_w16<INV, 4>(d); break;
-        case 5: a[k + j + H] = mul_w16<INV, 5>(d); break;
-        case 6: a[k + j + H] = mul_w16<INV, 6>(d); break;
-        default: a[k + j + H] = mul_w16<INV, 7>(d); break;
+    for (int i = 0; i < 4; i++) {
+      a[lo[i]] = s[i];
+      switch ((lo[i] % H) * (8 / H)) {
+        case 0: a[lo[i] + H] = d[i]; break;
+        case 1: a[lo[i] + H] = mul_w16<INV, 1>(d[i]); break;
+        case 2: a[lo[i] + H] = mul_w16<INV, 2>(d[i]); break;
+        case 3: a[lo[i] + H] = mul_w16<INV, 3>(d[i]); break;
+        case 4: a[lo[i] + H] = mul_w16<INV, 4>(d[i]); break;
+        case 5: a[lo[i] + H] = mul_w16<INV, 5>(d[i]); break;
+        case 6: a[lo[i] + H] = mul_w16<INV, 6>(d[i]); break;
+        default: a[lo[i] + H] = mul_w16<INV, 7>(d[i]); break;
       }
     }
   }
@@ -363,13 +291,8 @@ __device__ __forceinline__ uint64_t tw_pow(const uint64_t *__restrict__ tw, uint
   return qpk::tw_get(tw, e << (qpk::TW_LOG - log_S));
 }
 
-#ifndef QP_PASS32
-#define QP_PASS32 1
-#endif
-#ifndef QP_LDS_PAD
-#define QP_LDS_PAD 1
-#endif
-__host__ __device__ __forceinline__ constexpr uint32_t lp(uint32_t i) { return QP_LDS_PAD ? i + (i >> 5) : i; }
+// LDS index with one pad word per 32 (bank-conflict-free strided passes)
+__host__ __device__ __forceinline__ constexpr uint32_t lp(uint32_t i) { return i + (i >> 5); }
 
 __device__ __forceinline__ uint32_t brev4(uint32_t m) { return __builtin_bitreverse32(m) >> 28; }
 
@@ -463,7 +386,7 @@ __device__ __forceinline__ void pass32(uint64_t *a, uint32_t n) {
 // return log_S (after the barrier of the last pass), for callers that fold
 // those levels into their output loop (tail_group)
 __host__ __device__ constexpr bool use_pass32(uint32_t log_S, uint32_t n, uint32_t T) {
-  return QP_PASS32 && log_S == 5 && (n >> 4) % 128 == 0 && T % 64 == 0;
+  return log_S == 5 && (n >> 4) % 128 == 0 && T % 64 == 0;
 }
 // the log_S ntt_lds_from<.., false> returns for a block of T threads
 __host__ __device__ constexpr uint32_t lds_levels_left(uint32_t log_n, uint32_t log_S, uint32_t T) {
@@ -471,8 +394,8 @@ __host__ __device__ constexpr uint32_t lds_levels_left(uint32_t log_n, uint32_t 
   return log_S;
 }
 // K: the pass twiddles as interleaved triples (mul_rows); the coset LDE uses
-// single products (QP_LDE_MULK)
-template <bool INV, bool TAIL = true, bool K = QP_NTT_MULK>
+// single products
+template <bool INV, bool TAIL = true, bool K = true>
 __device__ __forceinline__ uint32_t ntt_lds_from(uint64_t *a, uint32_t log_n, uint32_t log_S, const uint64_t *__restrict__ pt) {
   const uint32_t n = 1u << log_n;
   const uint32_t T = blockDim.x;

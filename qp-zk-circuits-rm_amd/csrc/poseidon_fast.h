@@ -10,16 +10,8 @@
 // between its own v_add_co/v_addc pairs).  Around inline asm hipcc adds only a
 // fixed 1-state pad, so every asm statement below that reads a carry written
 // by the preceding one opens with its own s_nop 0.
-//
-// (QP_CARRY_WAIT=0 drops it: A/B only, profiles/r02_ab_carry_wait.log.)
-#ifndef QP_CARRY_WAIT
-#define QP_CARRY_WAIT 1
-#endif
-#if QP_CARRY_WAIT
+// (Dropping it measured no faster, profiles/r02_ab_carry_wait.log.)
 #define QP_CWAIT "s_nop 0\n\t"
-#else
-#define QP_CWAIT ""
-#endif
 //
 // Same function as ps::permute (poseidon.h); arithmetic discipline:
 //   * state NON-canonical in [0, 2^64) (plonky2's GoldilocksField form);
@@ -93,33 +85,20 @@ __device__ __forceinline__ uint64_t reduce_row(uint64_t al, uint64_t ah) {
 }
 
 // a * b mod p, a, b in [0, 2^64), result in [0, 2^64)
-#ifndef QP_MUL_FORM
-#define QP_MUL_FORM 1
-#endif
 __device__ __forceinline__ uint64_t mul(uint64_t a, uint64_t b) {
   const uint32_t a0 = lo32(a), a1 = hi32(a), b0 = lo32(b), b1 = hi32(b);
-  uint64_t W, X;
-  if constexpr (QP_MUL_FORM == 1) {
-    // middle column as one 65-bit sum: T = a0 b1 + L.hi, U = a1 b0 + T with
-    // its carry-out c (worth 2^96), W = a1 b1 + (U.hi | c << 32): one
-    // zero-extension and no separate 64-bit add (the form below needs three
-    // and a v_lshl_add_u64)
-    const uint64_t L = (uint64_t)a0 * b0;
-    const uint64_t T = (uint64_t)a0 * b1 + hi32(L);
-    uint64_t U, cu;
-    uint32_t ce;
-    asm("v_mad_u64_u32 %0, %1, %2, %3, %4" : "=v"(U), "=s"(cu) : "v"(a1), "v"(b0), "v"(T));
-    asm(QP_CWAIT "v_cndmask_b32_e64 %0, 0, 1, %1" : "=v"(ce) : "s"(cu));
-    W = (uint64_t)a1 * b1 + (((uint64_t)ce << 32) | hi32(U));  // < 2^64 (high half of a 128-bit product)
-    X = ((uint64_t)lo32(U) << 32) | lo32(L);
-  } else {
-    const uint64_t L = (uint64_t)a0 * b0;
-    const uint64_t T = (uint64_t)a0 * b1 + hi32(L);
-    const uint64_t U = (uint64_t)a1 * b0 + lo32(T);
-    const uint64_t V = (uint64_t)a1 * b1 + hi32(T);
-    W = V + hi32(U);  // < 2^64: a1 b1 + 2 (2^32 - 1) < 2^64
-    X = ((uint64_t)lo32(U) << 32) | lo32(L);
-  }
+  // middle column as one 65-bit sum: T = a0 b1 + L.hi, U = a1 b0 + T with its
+  // carry-out c (worth 2^96), W = a1 b1 + (U.hi | c << 32): one zero-extension
+  // and no separate 64-bit add (the textbook four-product form, mul_c below,
+  // needs three and a v_lshl_add_u64; profiles/r02_ab_mul_form_dot_halves.log)
+  const uint64_t L = (uint64_t)a0 * b0;
+  const uint64_t T = (uint64_t)a0 * b1 + hi32(L);
+  uint64_t U, cu;
+  uint32_t ce;
+  asm("v_mad_u64_u32 %0, %1, %2, %3, %4" : "=v"(U), "=s"(cu) : "v"(a1), "v"(b0), "v"(T));
+  asm(QP_CWAIT "v_cndmask_b32_e64 %0, 0, 1, %1" : "=v"(ce) : "s"(cu));
+  const uint64_t W = (uint64_t)a1 * b1 + (((uint64_t)ce << 32) | hi32(U));  // < 2^64 (high half)
+  const uint64_t X = ((uint64_t)lo32(U) << 32) | lo32(L);
   // 128-bit product = X + 2^64 W, X = (L0, U0);  ≡ X + eps*w2 - w3
   uint64_t t, c1, c2, c3;
   uint32_t e;
@@ -173,13 +152,11 @@ __device__ __forceinline__ uint64_t sbox_c(uint64_t x) {
 // hazard's two wait states are met by the other products' work instead of
 // s_nop (one product alone needs ~14 pad states).  Same arithmetic as mul():
 // U = a1 b0 + T with carry, W = a1 b1 + (U.hi | c << 32), X = (U.lo, L.lo),
-// then the 8-step reduction.  Measured slower (QP_MULK=1: leaf hash +4 %,
-// e2e -2 %, profiles/r02_ab_mulk.log): at 7 waves/SIMD the pads it removes
-// (8.0k -> 2.9k s_nop per permutation) were nearly free and it adds ~500
-// register-pair moves, so the default keeps one product at a time.
-#ifndef QP_MULK
-#define QP_MULK 0
-#endif
+// then the 8-step reduction.  The NTT passes use it (nt::mul_rows); in the
+// Poseidon S-boxes it measured slower (leaf hash +4 %, e2e -2 %,
+// profiles/r02_ab_mulk.log): at 7 waves/SIMD the pads it removes (8.0k -> 2.9k
+// s_nop per permutation) were nearly free and it adds ~500 register-pair
+// moves, so the S-boxes keep one product at a time.
 #define QP_W2 QP_CWAIT  // K = 2: one explicit wait state before each carry read
 template <int K>
 __device__ __forceinline__ void mulk(const uint64_t *a, const uint64_t *b, uint64_t *r) {
@@ -292,40 +269,15 @@ __device__ __forceinline__ void mulk(const uint64_t *a, const uint64_t *b, uint6
 
 __device__ __forceinline__ uint64_t sbox(uint64_t x) {
   const uint64_t x2 = mul(x, x);
-  if constexpr (QP_MULK) {
-    // x^3 and x^4 are independent: one interleaved pair
-    const uint64_t a[2] = {x2, x2}, b[2] = {x, x2};
-    uint64_t r[2];
-    mulk<2>(a, b, r);
-    return mul(r[0], r[1]);
-  } else {
-    const uint64_t x3 = mul(x2, x);
-    const uint64_t x4 = mul(x2, x2);
-    return mul(x3, x4);
-  }
-}
-
-// three S-boxes with every product interleaved three ways
-__device__ __forceinline__ void sbox3(uint64_t &x, uint64_t &y, uint64_t &z) {
-  uint64_t v[3] = {x, y, z}, v2[3], v3[3], v4[3], v7[3];
-  mulk<3>(v, v, v2);
-  mulk<3>(v2, v, v3);
-  mulk<3>(v2, v2, v4);
-  mulk<3>(v3, v4, v7);
-  x = v7[0];
-  y = v7[1];
-  z = v7[2];
+  const uint64_t x3 = mul(x2, x);
+  const uint64_t x4 = mul(x2, x2);
+  return mul(x3, x4);
 }
 
 // the 12 S-boxes of a full round
 __device__ __forceinline__ void sbox12(uint64_t s[12]) {
-  if constexpr (QP_MULK) {
 #pragma unroll
-    for (int i = 0; i < 12; i += 3) sbox3(s[i], s[i + 1], s[i + 2]);
-  } else {
-#pragma unroll
-    for (int i = 0; i < 12; i++) s[i] = sbox(s[i]);
-  }
+  for (int i = 0; i < 12; i++) s[i] = sbox(s[i]);
 }
 
 // a + c, a in [0, 2^64), c < p
@@ -548,10 +500,7 @@ __device__ __forceinline__ void full_round_dyn(uint64_t s[12], const uint64_t *_
 // dot product for lane 0 and 11 scalar multiply-adds.  Dense constants act on
 // 22-bit limbs (x = l0 + 2^22 l1 + 2^44 l2) through precomputed c 2^(22k) mod
 // p halves, so every accumulator stays < 2^60 and reduces in 4 instructions.
-// Same permutation as the plain rounds (QP_POSEIDON_SPARSE=0 keeps those).
-#ifndef QP_POSEIDON_SPARSE
-#define QP_POSEIDON_SPARSE 1
-#endif
+// Same permutation as the plain rounds (modes 3 and 10 take this form).
 
 __device__ __forceinline__ void limbs22(uint64_t x, uint32_t l[3]) {
   const uint32_t lo = lo32(x), hi = hi32(x);
@@ -621,15 +570,6 @@ __device__ __forceinline__ void mds_init_sparse(uint64_t s[12]) {
   for (int i = 0; i < 12; i++) s[i] = out[i];
 }
 
-template <int T, int J = 1>
-__device__ __forceinline__ void sparse_row0(uint64_t &al, uint64_t &ah, const uint64_t s[12]) {
-  if constexpr (J < 12) {
-    uint32_t L[3];
-    limbs22(s[J], L);
-    mac_limbs<PT_AHAT, (T * 11 + J - 1) * 6>(al, ah, L);
-    sparse_row0<T, J + 1>(al, ah, s);
-  }
-}
 template <int T, int I = 1>
 __device__ __forceinline__ void sparse_col0(uint64_t s[12], const uint32_t l0[3]) {
   if constexpr (I < 12) {
@@ -668,39 +608,29 @@ __device__ __forceinline__ uint64_t sub_small(uint64_t r, uint32_t y0, uint32_t 
   return ((uint64_t)r1 << 32) | r0;
 }
 
-#ifndef QP_PF_DOT_HALVES
-#define QP_PF_DOT_HALVES 1
-#endif
-
 // partial round 4 + T in sparse form (the next round's constants folded in)
 template <int T>
 __device__ __forceinline__ void partial_sparse(uint64_t s[12]) {
   const uint64_t x0 = sbox(s[0]);
   uint32_t l0[3];
   limbs22(x0, l0);
-  if constexpr (QP_PF_DOT_HALVES) {
-    // V = S0 + 2^22 S1 + 2^44 S2 + k,  25 x0 = 25 lo + (25 2^10) 2^22 hi
-    constexpr uint32_t kl = pfp::K0[2 * T], kh = pfp::K0[2 * T + 1];
-    uint64_t S[3];
-    asm("v_mad_u64_u32 %0, vcc, %1, 25, %2" : "=v"(S[0]) : "v"(lo32(x0)), "s"((uint64_t)kl) : "vcc");
-    S[1] = (uint64_t)hi32(x0) * 25600u;
-    S[2] = 0;
-    sparse_row0_h<T>(S, s);
-    sparse_col0<T>(s, l0);
-    // al + 2^32 ah - y:  2^22 S1 = 2^22 S1.lo + 2^32 (2^22 S1.hi);
-    // 2^44 S2 = 2^32 (2^12 S2.lo) + 2^76 S2.hi, 2^76 = 2^32 2^12 - 2^12 (mod p)
-    const uint64_t al = S[0] + (uint64_t)lo32(S[1]) * (1u << 22);
-    uint64_t ah = (uint64_t)kh + (uint64_t)hi32(S[1]) * (1u << 22);
-    ah += (uint64_t)lo32(S[2]) * (1u << 12);
-    ah += (uint64_t)hi32(S[2]) * (1u << 12);
-    s[0] = sub_small(reduce_row(al, ah), hi32(S[2]) << 12, hi32(S[2]) >> 20);
-  } else {
-    uint64_t al = pfp::K0[2 * T], ah = pfp::K0[2 * T + 1];
-    mac_limbs<PT_S0C, 0>(al, ah, l0);
-    sparse_row0<T>(al, ah, s);
-    sparse_col0<T>(s, l0);
-    s[0] = reduce_row(al, ah);
-  }
+  // lane 0's dot product on the S-box output's 32-bit halves (the 22-bit limb
+  // form measured slower: profiles/r02_ab_mul_form_dot_halves.log)
+  // V = S0 + 2^22 S1 + 2^44 S2 + k,  25 x0 = 25 lo + (25 2^10) 2^22 hi
+  constexpr uint32_t kl = pfp::K0[2 * T], kh = pfp::K0[2 * T + 1];
+  uint64_t S[3];
+  asm("v_mad_u64_u32 %0, vcc, %1, 25, %2" : "=v"(S[0]) : "v"(lo32(x0)), "s"((uint64_t)kl) : "vcc");
+  S[1] = (uint64_t)hi32(x0) * 25600u;
+  S[2] = 0;
+  sparse_row0_h<T>(S, s);
+  sparse_col0<T>(s, l0);
+  // al + 2^32 ah - y:  2^22 S1 = 2^22 S1.lo + 2^32 (2^22 S1.hi);
+  // 2^44 S2 = 2^32 (2^12 S2.lo) + 2^76 S2.hi, 2^76 = 2^32 2^12 - 2^12 (mod p)
+  const uint64_t al = S[0] + (uint64_t)lo32(S[1]) * (1u << 22);
+  uint64_t ah = (uint64_t)kh + (uint64_t)hi32(S[1]) * (1u << 22);
+  ah += (uint64_t)lo32(S[2]) * (1u << 12);
+  ah += (uint64_t)hi32(S[2]) * (1u << 12);
+  s[0] = sub_small(reduce_row(al, ah), hi32(S[2]) << 12, hi32(S[2]) >> 20);
 }
 
 // ---- groups of G partial rounds (tools/gen_poseidon_partial.py
@@ -708,9 +638,7 @@ __device__ __forceinline__ void partial_sparse(uint64_t s[12]) {
 // updates are deferred to the end of the group (one reduction per lane per
 // group instead of per round); round t's lane-0 dot then reads the group-start
 // lanes and adds gamma[t][l] x_l for the group's earlier S-box outputs x_l.
-#ifndef QP_PF_GROUP
-#define QP_PF_GROUP 4
-#endif
+constexpr int PF_GROUP = 4;  // partial rounds per group (profiles/r02_ab_poseidon_group4.log)
 struct NoHook {
   __device__ __forceinline__ uint64_t operator()(int, uint64_t v) const { return v; }
 };
@@ -788,12 +716,12 @@ __device__ __forceinline__ void rounds(uint64_t s[12]) {
 #pragma unroll 1
     for (int r = 26; r < 29; r++) full_round_dyn(s, ps::RC_DEV + (r + 1) * 12);
     rounds<3, 29, OUT>(s);
-  } else if constexpr (QP_POSEIDON_SPARSE && (M == 3 || M == 10) && R == 3) {
+  } else if constexpr ((M == 3 || M == 10) && R == 3) {
     sbox12(s);
     mds_init_sparse(s);
     rounds<M, 4, OUT>(s);
-  } else if constexpr (QP_POSEIDON_SPARSE && (M == 3 || M == 10) && R >= 4 && R < 26) {
-    constexpr int T0 = R - 4, G = (22 - T0) < QP_PF_GROUP ? (22 - T0) : QP_PF_GROUP;
+  } else if constexpr ((M == 3 || M == 10) && R >= 4 && R < 26) {
+    constexpr int T0 = R - 4, G = (22 - T0) < PF_GROUP ? (22 - T0) : PF_GROUP;
     if constexpr (G > 1) partial_group<T0, G>(s);
     else partial_sparse<T0>(s);
     rounds<M, R + G, OUT>(s);
@@ -863,27 +791,19 @@ __device__ __forceinline__ void capz_mds(uint64_t s[12], const uint32_t lo[12], 
   }
 }
 
-#ifndef QP_POSEIDON_CAPZ
-#define QP_POSEIDON_CAPZ 1
-#endif
 // permute_nc for s[8..11] == 0 on entry (mode 3), reading only lanes OUT
+// (profiles/r02_ab_capz.log)
 template <uint32_t OUT = 0xFFFu>
 __device__ __forceinline__ void permute_nc_capz(uint64_t s[12]) {
-  if constexpr (!QP_POSEIDON_CAPZ) {
+  uint32_t lo[12], hi[12];
 #pragma unroll
-    for (int i = 0; i < 12; i++) s[i] = add_c(s[i], ps::rc_cx(i));
-    rounds<3, 0, OUT>(s);
-  } else {
-    uint32_t lo[12], hi[12];
-#pragma unroll
-    for (int i = 0; i < 8; i++) {
-      s[i] = sbox(add_c(s[i], ps::rc_cx(i)));
-      lo[i] = lo32(s[i]);
-      hi[i] = hi32(s[i]);
-    }
-    capz_mds(s, lo, hi);
-    rounds<3, 1, OUT>(s);
+  for (int i = 0; i < 8; i++) {
+    s[i] = sbox(add_c(s[i], ps::rc_cx(i)));
+    lo[i] = lo32(s[i]);
+    hi[i] = hi32(s[i]);
   }
+  capz_mds(s, lo, hi);
+  rounds<3, 1, OUT>(s);
 }
 
 // permutation; inputs in [0, 2^64), outputs in [0, 2^64) (canon() lanes read out)

@@ -26,16 +26,8 @@
 #include "kernels.h"
 #include "prover_kernels.h"
 #include "witness_kernels.h"
+#include "paths.h"
 
-// PoW search window per launch (candidates per still-searching proof), log2
-// QP_POW_SCAN 1: one k_pow_scan launch per PoW stage; 0: the windowed k_pow
-// loop with a host check per window (A/B)
-#ifndef QP_POW_SCAN
-#define QP_POW_SCAN 1
-#endif
-#ifndef QP_POW_WINDOW_LOG
-#define QP_POW_WINDOW_LOG 13
-#endif
 
 namespace {
 
@@ -104,7 +96,7 @@ struct qp_prover {
   Tree cs;
   DevBuf sigmas, kis;
   Tree wires, zs, quot;
-  DevBuf chal, apow, prods, qvals, cbuf, openings, open_part, comp, fin, pow_state, pow_found, pow_pos, pow_active, pow_next, qidx,
+  DevBuf chal, apow, prods, qvals, cbuf, openings, open_part, comp, fin, pow_state, pow_found, pow_pos, pow_next, qidx,
       qout, qtab;
   std::vector<DevBuf> fvals, fdig, fcoef;
   size_t qout_words = 0;
@@ -126,13 +118,9 @@ struct qp_prover {
   // device witness generation (witness.hip): schedule + per-proof slot values
   DevBuf wg_gens, wg_lvl, wg_lpos, wg_wslot, wg_wslot_cm, wg_in_slots, wg_pi_slots, wg_vals, wg_in, wg_err, wg_pis;
   uint32_t wg_nslots = 0, wg_nin = 0, wg_nlev = 0;
-  bool quotient_rereads = false;
-  bool quotient_fused = false;  // A/B: QPGPU_QUOTIENT=fused selects k_quotient_fused where it applies
-  bool quotient_onepass = false;  // A/B: QPGPU_QUOTIENT=onepass keeps k_quotient<2> for generic gate lists
   bool has_poseidon_gate = false;
   bool has_random_access = false;
   bool generic_quotient = false;  // a gate outside k_quotient_1r's set (the recursive verifier's RandomAccess)
-  bool pp_generic = false;  // QPGPU_PP_GENERIC=1: the runtime-shape k_pp_rows (A/B)
   uint64_t *h_in = nullptr;  // pinned [max_batch][wg_nin] commit() values
   std::vector<std::vector<uint64_t>> wscratch;  // per-proof slot values when host chains run split
   std::vector<uint32_t> h_werr;
@@ -358,7 +346,6 @@ int setup(qp_prover *P) {
   TRY(P->pow_state.alloc((size_t)B * 24));
   TRY(P->pow_found.alloc(B));
   TRY(P->pow_pos.alloc((B + 1) / 2));
-  TRY(P->pow_active.alloc((B + 1) / 2));
   TRY(P->pow_next.alloc(B));
   {
     std::vector<uint64_t> tab = qpk::quotient_point_tables(P->log_n, P->rate_bits);
@@ -418,16 +405,6 @@ int setup(qp_prover *P) {
   }
   TRY(hipStreamSynchronize(c->stream));
   P->proof_len = proof_size(P);
-  {
-    const char *qv = getenv("QPGPU_QUOTIENT");
-    P->quotient_rereads = qv && !strcmp(qv, "rereads");
-    P->quotient_fused = qv && !strcmp(qv, "fused");
-    // QPGPU_QUOTIENT=onepass: the generic gate list in one k_quotient<2> pass
-    // (A/B) instead of the per-gate launches
-    P->quotient_onepass = qv && !strcmp(qv, "onepass");
-    const char *pv = getenv("QPGPU_PP_GENERIC");
-    P->pp_generic = pv && pv[0] && pv[0] != '0';
-  }
   unsigned hw = std::thread::hardware_concurrency();
   unsigned nthreads = std::min<unsigned>(hw ? hw : 4, 16);
   P->pool.reset(new qh::ThreadPool(nthreads > 1 ? nthreads - 1 : 0));
@@ -611,7 +588,7 @@ int prove_batch(qp_prover *P, const uint64_t *d_wires, const uint64_t *const *wi
 
   // ---- 2. partial products + Z (a9), commitment
   const uint64_t pbs = (uint64_t)nc * P->nchunks * n;
-  if (P->R == 80 && P->qdf == 8 && nc == 2 && !P->pp_generic)
+  if (P->R == 80 && P->qdf == 8 && nc == 2)
     qpk::k_pp_rows_t<80, 8><<<dim3(cdiv(n, 256), nb), 256, 0, s>>>(wv, P->sigmas.p, P->kis.p, P->chal.p, P->prods.p,
                                                                     P->log_n, P->wires.cbs(), pbs, c->tw.fwd);
   else
@@ -673,11 +650,10 @@ int prove_batch(qp_prover *P, const uint64_t *d_wires, const uint64_t *const *wi
     a.num_constants = P->NC;
     a.g = P->gdesc;
     kt_begin(P, 3);
-    qpk::QuotientKernel qk = qpk::QK_1R;
-    if (P->generic_quotient && !P->quotient_onepass && !P->quotient_rereads) qk = qpk::QK_PARTS;
-    else if (P->quotient_rereads || P->generic_quotient) qk = qpk::QK_ONEPASS;  // A/B: QPGPU_QUOTIENT=rereads/onepass
-    else if (P->R == 80 && P->qdf == 8 && P->has_poseidon_gate && P->quotient_fused && !P->has_random_access)
-      qk = qpk::QK_FUSED;
+    // the leaf gate set: one single-read pass; any other gate list (and the
+    // path hook quotient_parts=1): the per-gate launches
+    const qpk::QuotientKernel qk =
+        P->generic_quotient || qpk::path_opt("quotient_parts", 0) ? qpk::QK_PARTS : qpk::QK_1R;
     qpk::quotient_values(a, qk, nb, s);
     kt_end(P, 3, (double)nb * N);
     qpk::quotient_coeffs(c->tw, P->qvals.p, P->cbuf.p, P->quot.coeffs.p, P->log_n, P->rate_bits, nc, nb,
@@ -836,34 +812,16 @@ int prove_batch(qp_prover *P, const uint64_t *d_wires, const uint64_t *const *wi
     TRY(hipStreamSynchronize(s));
     for (uint32_t b = 0; b < nb; b++) P->h_found[b] = P->pow_forced_witness;
   } else {
-#if QP_POW_SCAN
     // Minimal witness per proof in one launch (k_pow_scan): 2048 workgroups
     // claim 256-candidate blocks from per-proof counters, moving on to the
     // next proof once theirs has a hit below the claimed block
     const uint64_t limit = 1ull << std::min<uint32_t>(P->pow_bits + 20, 62);
     TRY(hipMemsetAsync(P->pow_next.p, 0, (size_t)nb * 8, s));
-    // QPGPU_POW_WAVE=1: per-wave claims of 64 candidates (k_pow_scan_w; A/B:
-    // voting 10.8-11.1 k vs 12.9-13.4 k proofs/s with workgroup claims, the
-    // leaf bench unchanged -- four times the atomics on each proof's counter;
-    // profiles/r05_ab_pow_wave.log)
-    const char *pw = getenv("QPGPU_POW_WAVE");
-    // QPGPU_POW_CPT=1/2/4: candidates per thread per claimed block (A/B: no
-    // change, profiles/r05_ab_pow_cpt.log)
-    const char *pc = getenv("QPGPU_POW_CPT");
-    const int cpt = pc && *pc ? atoi(pc) : 1;
-    if (!(pw && pw[0] == '1')) {
-      if (cpt == 4)
-        qpk::k_pow_scan<4><<<2048, 256, 0, s>>>(P->pow_state.p, (const uint32_t *)P->pow_pos.p, P->pow_found.p,
-                                                P->pow_next.p, nb, P->pow_bits, limit);
-      else if (cpt == 2)
-        qpk::k_pow_scan<2><<<2048, 256, 0, s>>>(P->pow_state.p, (const uint32_t *)P->pow_pos.p, P->pow_found.p,
-                                                P->pow_next.p, nb, P->pow_bits, limit);
-      else
-        qpk::k_pow_scan<1><<<2048, 256, 0, s>>>(P->pow_state.p, (const uint32_t *)P->pow_pos.p, P->pow_found.p,
-                                                P->pow_next.p, nb, P->pow_bits, limit);
-    } else
-      qpk::k_pow_scan_w<<<2048, 256, 0, s>>>(P->pow_state.p, (const uint32_t *)P->pow_pos.p, P->pow_found.p,
-                                             P->pow_next.p, nb, P->pow_bits, limit);
+    // (per-wave claims and 2-4 candidates per thread measured no better:
+    // profiles/r05_ab_pow_wave.log, r05_ab_pow_cpt.log; a windowed loop with a
+    // host check per window was the round-1 form)
+    qpk::k_pow_scan<<<2048, 256, 0, s>>>(P->pow_state.p, (const uint32_t *)P->pow_pos.p, P->pow_found.p,
+                                         P->pow_next.p, nb, P->pow_bits, limit);
     TRY(hipGetLastError());
     TRY(hipMemcpyAsync(P->h_found.data(), P->pow_found.p, (size_t)nb * 8, hipMemcpyDeviceToHost, s));
     TRY(hipStreamSynchronize(s));
@@ -872,38 +830,6 @@ int prove_batch(qp_prover *P, const uint64_t *d_wires, const uint64_t *const *wi
         c->err = "proof of work not found";
         return QP_ERR_STATE;
       }
-#else
-    // Minimal witness per proof: every proof still searching scans the same
-    // candidate window [base, base + W) per launch; only those proofs are
-    // launched (compacted list), so a proof stops costing work as soon as its
-    // window holds a hit.  W = 2^13 keeps the overshoot past the minimal
-    // witness ~W/2 (vs an expected 2^pow_bits search); when few proofs remain
-    // W grows so a launch still covers >= 2^21 candidates (idle CUs otherwise).
-    std::vector<uint32_t> active(nb);
-    for (uint32_t b = 0; b < nb; b++) active[b] = b;
-    uint64_t base = 0;
-    while (!active.empty()) {
-      const uint32_t na = (uint32_t)active.size();
-      uint64_t window = 1ull << QP_POW_WINDOW_LOG;
-      while ((uint64_t)na * window < (1ull << 21)) window <<= 1;
-      TRY(hipMemcpyAsync(P->pow_active.p, active.data(), (size_t)na * 4, hipMemcpyHostToDevice, s));
-      qpk::k_pow<<<dim3((uint32_t)(window / 256), na), 256, 0, s>>>(
-          P->pow_state.p, (const uint32_t *)P->pow_pos.p, (const uint32_t *)P->pow_active.p, P->pow_found.p, base,
-          P->pow_bits);
-      TRY(hipGetLastError());
-      TRY(hipMemcpyAsync(P->h_found.data(), P->pow_found.p, (size_t)nb * 8, hipMemcpyDeviceToHost, s));
-      TRY(hipStreamSynchronize(s));
-      std::vector<uint32_t> still;
-      for (uint32_t b : active)
-        if (P->h_found[b] == ~0ull) still.push_back(b);
-      active.swap(still);
-      base += window;
-      if (base > (1ull << 40)) {
-        c->err = "proof of work not found";
-        return QP_ERR_STATE;
-      }
-    }
-#endif
   }
   P->pool->parallel_for(nb, [&](size_t b) {
     ProofState &S = st[b];
@@ -1049,33 +975,20 @@ int gen_witness_batch(qp_prover *P, uint32_t nb) {
   // workgroup size of the witness kernel (one workgroup per proof): 512 for
   // the aggregation circuits (their wide levels run many one-lane
   // permutations: 256-leaf subtree 0.422 -> 0.415 s, witness stage 87 -> 73
-  // ms), 256 for the leaf circuits; QPGPU_WIT_THREADS=256/512 overrides
-  static const int wt_env = [] {
-    const char *e = getenv("QPGPU_WIT_THREADS");
-    return e && !strcmp(e, "512") ? 512 : e && !strcmp(e, "256") ? 256 : 0;
-  }();
-  const unsigned wthreads = wt_env ? (unsigned)wt_env : P->circuit->kind == qp_circuit::AGGREGATION ? 512u : 256u;
-  // QPGPU_WIT_COOP: Poseidon count up to which a level runs its Poseidon
-  // generators one per wave (12 lanes cooperating on one permutation) instead
-  // of one per lane; default 4 per wave, 0 disables
-  static const uint32_t coop_per_wave = [] {
-    const char *e = getenv("QPGPU_WIT_COOP");
-    return e ? (uint32_t)atoi(e) : 4u;
-  }();
-  a.coop_max = coop_per_wave * (wthreads / 64);
-  // QPGPU_WIT_ROW=0: cooperative Poseidons one per wave instead of one per
-  // 16-lane row (read per call)
-  const char *wr = getenv("QPGPU_WIT_ROW");
-  a.row = !(wr && wr[0] == '0');
-  // QPGPU_WIT_MODE=levels|wg: a launch per dependency level over the whole
-  // batch (default for the aggregation circuits: their 55 levels are mostly
-  // one permutation deep, and one workgroup per proof leaves each level at a
-  // one-lane permutation's latency) or one workgroup per proof (the leaf
-  // circuits' default)
-  const int wmode = [] {  // read per call: tests switch modes in one process
-    const char *e = getenv("QPGPU_WIT_MODE");
-    return e && !strcmp(e, "levels") ? 1 : e && !strcmp(e, "wg") ? 0 : -1;
-  }();
+  // ms), 256 for the leaf circuits
+  const unsigned wthreads = P->circuit->kind == qp_circuit::AGGREGATION ? 512u : 256u;
+  // up to 4 Poseidon generators per wave per level run cooperatively (12 lanes
+  // on one permutation) instead of one per lane
+  a.coop_max = 4 * (wthreads / 64);
+  // path hook wit_row=0: cooperative Poseidons one per wave instead of one per
+  // 16-lane row
+  a.row = qpk::path_opt("wit_row", 1) != 0;
+  // a launch per dependency level over the whole batch (default for small
+  // aggregation batches: their 55 levels are mostly one permutation deep, and
+  // one workgroup per proof leaves each level at a one-lane permutation's
+  // latency) or one workgroup per proof (the leaf circuits, large batches);
+  // path hook wit_mode=0|1 forces one
+  const long wmode = qpk::path_opt("wit_mode", -1);
   // (measured: one aggregation proof 11.0 -> 9.4 ms, witness 2.9 -> 1.3 ms;
   // at 32 proofs per launch 3.78 vs 3.88 ms for one workgroup per proof,
   // profiles/r05_ab_witness_levels.log)
@@ -1091,10 +1004,6 @@ int gen_witness_batch(qp_prover *P, uint32_t nb) {
   } else {
     qpk::k_witness_gen<<<nb, wthreads, 0, s>>>(a);
   }
-  // QPGPU_WIT_TWICE=1 (diagnostic): a second pass over the same values (every
-  // write repeats the value already there), to time the kernel with warm caches
-  static const bool twice = getenv("QPGPU_WIT_TWICE") && !strcmp(getenv("QPGPU_WIT_TWICE"), "1");
-  if (twice) qpk::k_witness_gen<<<nb, wthreads, 0, s>>>(a);
   qpk::k_witness_expand<<<dim3((unsigned)std::min<uint64_t>(cdiv(nw, 256), 1024), nb), 256, 0, s>>>(
       P->wg_vals.p, P->wg_nslots, (const uint32_t *)P->wg_wslot_cm.p, nw, P->wires.vals.p, P->wires.cbs(),
       (const uint32_t *)P->wg_pi_slots.p, P->npis, P->wg_pis.p);

@@ -28,7 +28,8 @@ enum GateKindDev : uint32_t {
   GK_COSET_INTERP, GK_COUNT
 };
 // RandomAccessGate width k_quotient_1r evaluates (the recursive verifier's
-// RandomAccessGate::new_from_config shape); other widths take k_quotient<2>
+// RandomAccessGate::new_from_config shape); other widths take the per-gate
+// launches (k_quotient_part)
 constexpr uint32_t RA_QBITS = 4;
 constexpr uint32_t MAX_GATES_DEV = 16;
 
@@ -70,17 +71,9 @@ __global__ void k_pp_rows_t(const uint64_t *wires, const uint64_t *sigmas, const
 template <bool STAGE>
 __global__ void k_z_scan(const uint64_t *prods, uint64_t *zs, uint32_t log_n, uint32_t nc, uint32_t nchunks,
                          uint64_t p_bstride, uint64_t z_bstride);
-template <int PH>
-__global__ void k_quotient(QuotientArgs a);
 __global__ void k_quotient_1r(QuotientArgs a);
-// k_quotient_1r for R = 80 routed wires in chunks of 8 with the Poseidon gate:
-// the sweep rides on the gate's wire reads (every wire read once)
-__global__ void k_quotient_fused(QuotientArgs a);
 template <int PART>
 __global__ void k_quotient_part(QuotientArgs a, uint32_t gi, uint32_t last);
-// the gates of gmask (Poseidon, recursion gates) one after another per point, one launch
-template <bool POS>
-__global__ void k_quotient_rest(QuotientArgs a, uint32_t gmask, uint32_t last);
 // the permutation terms + the gates of gmask that read routed wires only, one pass
 template <int QDF>
 __global__ void k_quotient_prefix(QuotientArgs a, uint32_t gmask, uint32_t last);
@@ -95,10 +88,8 @@ __global__ void k_qintt_radix(const uint64_t *cbuf, uint64_t *coeffs, uint32_t l
 // stage 3 and the qp_quotient seam: the vanishing-polynomial values at every
 // LDE point of nb proofs with the chosen kernel(s) ...
 enum QuotientKernel : uint32_t {
-  QK_1R,       // k_quotient_1r: the leaf gate set, every column read once
-  QK_FUSED,    // k_quotient_fused (A/B)
-  QK_ONEPASS,  // k_quotient<2>: any gate list in one pass (A/B)
-  QK_PARTS     // k_quotient_part: permutation terms, then one launch per gate (any gate list)
+  QK_1R,    // k_quotient_1r: the leaf gate set, every column read once
+  QK_PARTS  // k_quotient_part: permutation terms, then one launch per gate (any gate list)
 };
 void quotient_values(const QuotientArgs &a, QuotientKernel k, uint32_t nb, hipStream_t s);
 // ... and their coset iNTT into nc * qdf * n coefficients per proof (qvals
@@ -141,13 +132,8 @@ void fri_leaf(const uint64_t *vals, uint64_t *dig, uint32_t log_len, uint32_t ab
               uint64_t d_bstride, uint32_t nb, hipStream_t s);
 __global__ void k_fold(const uint64_t *cin, uint64_t *cout, uint32_t log_len, uint32_t ab, uint32_t layer,
                        const uint64_t *chal, uint64_t i_bstride, uint64_t o_bstride, uint32_t log_nz);
-__global__ void k_pow_scan_w(const uint64_t *states, const uint32_t *pos, uint64_t *found, uint64_t *next, uint32_t nb,
-                             uint32_t bits, uint64_t limit);
-template <int CPT>
 __global__ void k_pow_scan(const uint64_t *states, const uint32_t *pos, uint64_t *found, uint64_t *next, uint32_t nb,
                            uint32_t bits, uint64_t limit);
-__global__ void k_pow(const uint64_t *states, const uint32_t *pos, const uint32_t *active, uint64_t *found, uint64_t base,
-                      uint32_t bits);
 __global__ void k_gather_rows_b(const uint64_t *cols, uint64_t stride, uint64_t bstride, uint32_t ncols,
                                 const uint32_t *idx, uint32_t nq, uint32_t shift, uint64_t *out, uint64_t o_bstride);
 __global__ void k_gather_paths_b(const uint64_t *dig, uint64_t d_bstride, uint32_t log_leaves, uint32_t cap_h,

@@ -10,13 +10,14 @@
 //   k_openings             OpeningSet::new: Horner at zeta / g*zeta (a10)
 //   k_fri_compose/_divide  prove_openings: alpha-reduce + divide by (X - z) (a11)
 //   k_fri_leaf, k_fold     fri_committed_trees: leaves of 2^a ext, folding (a11)
-//   k_pow                  fri_proof_of_work: minimal witness (a12)
+//   k_pow_scan             fri_proof_of_work: minimal witness (a12)
 //   k_gather_*             query-round openings (a11)
 #include "field.h"
 #include "poseidon.h"
 #include "poseidon_dev.h"
 #include "poseidon_coop.h"
 #include "prover_kernels.h"
+#include "paths.h"
 #include <stdlib.h>
 #include <algorithm>
 #include "ntt16.h"
@@ -226,24 +227,11 @@ template __global__ void k_z_scan<false>(const uint64_t *, uint64_t *, uint32_t,
 
 #define WV(j) wl[(uint64_t)(j) * N]
 
-// two independent products: QP_Q_MULK=1 issues them interleaved (pf::mulk<2>:
-// each carry is read one product later instead of after hazard pads).
-// Measured no change on the quotient (7.25 / 7.41 vs 7.31 / 7.24 ms per
-// 86-proof launch, profiles/r03_ab_quotient_mulk.log), so off.
-#ifndef QP_Q_MULK
-#define QP_Q_MULK 0
-#endif
+// two independent products (an interleaved pf::mulk<2> form measured no
+// change, profiles/r03_ab_quotient_mulk.log)
 __device__ __forceinline__ void mul2(uint64_t a0, uint64_t b0, uint64_t a1, uint64_t b1, uint64_t &r0, uint64_t &r1) {
-  if constexpr (QP_Q_MULK) {
-    const uint64_t a[2] = {a0, a1}, b[2] = {b0, b1};
-    uint64_t r[2];
-    pf::mulk<2>(a, b, r);
-    r0 = r[0];
-    r1 = r[1];
-  } else {
-    r0 = gfn::mul(a0, b0);
-    r1 = gfn::mul(a1, b1);
-  }
+  r0 = gfn::mul(a0, b0);
+  r1 = gfn::mul(a1, b1);
 }
 
 struct TermAcc {
@@ -283,9 +271,6 @@ struct WireRead {
 template <class RD>
 __device__ __forceinline__ void poseidon_gate_rd(const RD &WR, TermAcc &A);
 
-#ifndef QP_QPOS_SPARSE
-#define QP_QPOS_SPARSE 1
-#endif
 // the partial-round wire check as the grouped rounds' pre-S-box hook: lane 0
 // is checked against the gate's S-box input wire and replaced by it
 template <class RD>
@@ -302,7 +287,7 @@ struct QposHook {
 template <int T, class RD>
 __device__ __forceinline__ void qpos_partial(const RD &WR, TermAcc &A, uint64_t s[12]) {
   if constexpr (T < 22) {
-    constexpr int G = (22 - T) < QP_PF_GROUP ? (22 - T) : QP_PF_GROUP;
+    constexpr int G = (22 - T) < pf::PF_GROUP ? (22 - T) : pf::PF_GROUP;
     if constexpr (G > 1) {
       pf::partial_group<T, G>(s, QposHook<RD>{WR, A});
     } else {
@@ -319,16 +304,6 @@ __device__ __forceinline__ void poseidon_gate(const uint64_t *__restrict__ wl, u
   WireRead rd{wl, N, nullptr, 0};
   poseidon_gate_rd(rd, A);
 }
-// the generic kernel's Poseidon gate as a call (QP_QGEN_POS_CALL=1): its
-// permutation-sized live state gets its own register allocation instead of
-// adding to the gate loop's (inlined, k_quotient<2> spills 432 B per lane)
-#ifndef QP_QGEN_POS_CALL
-#define QP_QGEN_POS_CALL 0
-#endif
-__device__ __noinline__ void poseidon_gate_call(const uint64_t *__restrict__ wl, uint64_t N, TermAcc &A) {
-  poseidon_gate(wl, N, A);
-}
-
 template <class RD>
 __device__ __forceinline__ void poseidon_gate_rd(const RD &WR, TermAcc &A) {
 #undef WV
@@ -358,26 +333,16 @@ __device__ __forceinline__ void poseidon_gate_rd(const RD &WR, TermAcc &A) {
       }
     }
     pf::sbox12(s);
-    if (QP_QPOS_SPARSE && r == 3) {
+    if (r == 3) {
       pf::mds_init_sparse(s);
     } else {
       rc_row(k, r + 1);
       pf::mds_k(s, k);
     }
   }
-  if constexpr (QP_QPOS_SPARSE) {
-    // sparse partial rounds (poseidon_fast.h): lane 0 before each S-box is the
-    // plain form's S-box input, so the wire checks are unchanged
-    qpos_partial<0>(WR, A, s);
-  } else {
-    for (int r = 0; r < 22; r++) {
-      const uint64_t sb = WV(65 + r);
-      A.emit(gfn::sub(s[0], sb));
-      s[0] = gfn::sbox(sb);
-      rc_row(k, 5 + r);
-      pf::mds_k(s, k);
-    }
-  }
+  // sparse partial rounds (poseidon_fast.h): lane 0 before each S-box is the
+  // plain form's S-box input, so the wire checks are unchanged
+  qpos_partial<0>(WR, A, s);
 #pragma unroll
   for (int r = 0; r < 4; r++) {
 #pragma unroll
@@ -412,8 +377,7 @@ __device__ __forceinline__ void alg_mul(uint64_t a0, uint64_t a1, uint64_t b0, u
 }
 
 // (inlined into the per-gate kernel, so TermAcc stays in registers and the
-// alpha-power reads are uniform scalar loads; called out of line by the
-// one-pass generic kernel to bound its size)
+// alpha-power reads are uniform scalar loads)
 __device__ __forceinline__ void recursion_gate_body(uint32_t kind, uint32_t q0, uint32_t q1, uint32_t q2,
                                                     const uint64_t *__restrict__ wl,
                                                     const uint64_t *__restrict__ gc, uint64_t N, TermAcc &A) {
@@ -595,146 +559,7 @@ __device__ __forceinline__ void recursion_gate_body(uint32_t kind, uint32_t q0, 
   }
 }
 
-__device__ __noinline__ void recursion_gate(uint32_t kind, uint32_t q0, uint32_t q1, uint32_t q2,
-                                            const uint64_t *__restrict__ wl, const uint64_t *__restrict__ gc,
-                                            uint64_t N, TermAcc &A) {
-  recursion_gate_body(kind, q0, q1, q2, wl, gc, N, A);
-}
 
-// Two phases with separate register allocation (the Poseidon gate alone is
-// a permutation's worth of live state; fused, the kernel needed 184 VGPRs =
-// 2 waves/SIMD):
-//   PH 0: L_0 terms, partial-product checks, every gate except Poseidon;
-//         raw (non-canonical) alpha sums -> q_out
-//   PH 1: Poseidon gates; adds the PH 0 sums, multiplies by 1/Z_H, canonical.
-//   PH 2: both in one pass (measured faster: 27.6 vs 30.4 ms at batch 256 —
-//         the second pass re-reads the wires; the fused kernel runs at 4
-//         waves/SIMD with a small spill).  PH 0/1 are kept for register-budget
-//         experiments.
-template <int PH>
-#ifndef QP_QUOTIENT_WAVES
-#define QP_QUOTIENT_WAVES 4
-#endif
-// occupancy target of the generic (any gate list) kernel: at 4 waves/SIMD its
-// 128-VGPR budget spills ~400 B per lane for the aggregation circuits' gate set,
-// yet the spill-free 2-wave form (225 VGPRs) measured slower
-// (profiles/r03_ab_quotient_generic_waves.log)
-#ifndef QP_QGEN_WAVES
-#define QP_QGEN_WAVES QP_QUOTIENT_WAVES
-#endif
-__global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(QP_QGEN_WAVES))) k_quotient(QuotientArgs a) {
-  const uint32_t logN = a.log_n + a.rate_bits;
-  const uint64_t N = 1ull << logN;
-  const uint32_t t = blockIdx.x * blockDim.x + threadIdx.x;
-  if (t >= N) return;
-  const uint32_t b = blockIdx.y;
-  const uint64_t *ch = a.chal + b * CHAL_STRIDE;
-  const uint64_t *cs = a.cs_lde + t;                       // [ncs][N]
-  const uint64_t *wl = a.w_lde + b * a.w_bstride + t;      // [W][N]
-  const uint64_t *zl = a.z_lde + b * a.z_bstride;          // [nzs][N]
-  const uint32_t j = gl::rev_bits(t, logN);                // natural point index
-  uint64_t *q = a.q_out + b * a.q_bstride;
-  TermAcc A;
-  A.p0 = a.apow + (uint64_t)b * 2 * APOW_STRIDE;
-  A.p1 = A.p0 + APOW_STRIDE;
-  A.s0 = A.s1 = 0;
-  A.i = 0;
-  const uint32_t R = a.R, qdf = a.qdf, nchunks = (R + qdf - 1) / qdf, npp = nchunks - 1;
-  if (PH != 1) {
-    const uint32_t tn = gl::rev_bits((j + (1u << a.rate_bits)) & (uint32_t)(N - 1), logN);
-    const uint64_t x = a.xtab[t];
-    // L_0(x) (Z_c - 1)
-    const uint64_t l0 = a.l0tab[t];
-    for (uint32_t c = 0; c < 2; c++) A.emit(gfn::mul(l0, gfn::sub(zl[(uint64_t)c * N + t], 1)));
-    // partial-product checks
-    for (uint32_t c = 0; c < 2; c++) {
-      const uint64_t beta = ch[CH_BETA + c], gamma = ch[CH_GAMMA + c];
-      uint64_t bkx = gfn::mul(beta, x);  // beta * k_j * x with k_j = g^j
-      for (uint32_t k = 0; k < nchunks; k++) {
-        uint64_t num = 1, den = 1;
-        for (uint32_t jj = k * qdf; jj < (k + 1) * qdf && jj < R; jj++) {
-          const uint64_t wv = WV(jj);
-          const uint64_t wg = gfn::add_c(wv, gamma);
-          num = gfn::mul(num, gfn::add(wg, bkx));
-          den = gfn::mul(den, gfn::add(wg, gfn::mul(beta, cs[(uint64_t)(a.num_constants + jj) * N])));
-          bkx = gfn::mul(bkx, gl::GEN);
-        }
-        const uint64_t prev = k == 0 ? zl[(uint64_t)c * N + t] : zl[((uint64_t)2 + c * npp + k - 1) * N + t];
-        const uint64_t next = k == nchunks - 1 ? zl[(uint64_t)c * N + tn] : zl[((uint64_t)2 + c * npp + k) * N + t];
-        A.emit(gfn::sub(gfn::mul(prev, num), gfn::mul(next, den)));
-      }
-    }
-  }
-  // gate constraints: every gate's terms start at alpha^(#pre-terms); the
-  // selector filter multiplies each gate's sum once
-  const uint32_t pre = 2 * (1 + nchunks);
-  uint64_t acc0 = A.s0, acc1 = A.s1;  // PH 1 adds the PH 0 sums at the end
-  // constant columns are re-read where used (L1/L2 hits) rather than held in
-  // 16 VGPRs across the Poseidon gate evaluation
-#define CONSTCOL(k) cs[(uint64_t)(k) * N]
-  const uint32_t nsel = a.g.nsel;
-  for (uint32_t gi = 0; gi < a.g.ngates; gi++) {
-    const uint32_t kind = a.g.kind[gi];
-    if (kind == GK_NOOP || (PH == 0 && kind == GK_POSEIDON) || (PH == 1 && kind != GK_POSEIDON)) continue;
-    const uint32_t si = a.g.sel_index[gi];
-    const uint64_t s = CONSTCOL(si);
-    uint64_t f = 1;
-    for (uint32_t jj = a.g.grp_lo[si]; jj < a.g.grp_hi[si]; jj++)
-      if (jj != gi) f = gfn::mul(f, gfn::sub(jj, s));
-    if (nsel > 1) f = gfn::mul(f, gfn::sub(0xFFFFFFFFull, s));
-    A.s0 = A.s1 = 0;
-    A.i = pre;
-    const uint64_t *gc = cs + (uint64_t)nsel * N;
-    if (kind == GK_POSEIDON) {
-      if constexpr (QP_QGEN_POS_CALL) poseidon_gate_call(wl, N, A);
-      else poseidon_gate(wl, N, A);
-    } else {
-      switch (kind) {
-        case GK_CONSTANT:
-          for (uint32_t i = 0; i < a.g.param[gi]; i++) A.emit(gfn::sub(gc[(uint64_t)i * N], WV(i)));
-          break;
-        case GK_PUBLIC_INPUT:
-          for (uint32_t i = 0; i < 4; i++) A.emit(gfn::sub(WV(i), ch[CH_PIH + i]));
-          break;
-        case GK_BASE_SUM: {
-          const uint32_t L = a.g.param[gi];
-          uint64_t acc = 0;
-          for (uint32_t i = L; i-- > 0;) acc = gfn::add(gfn::add(acc, acc), WV(1 + i));
-          A.emit(gfn::sub(acc, WV(0)));
-          for (uint32_t i = 0; i < L; i++) {
-            const uint64_t l = WV(1 + i);
-            A.emit(gfn::mul(l, gfn::sub(l, 1)));
-          }
-          break;
-        }
-        case GK_ARITHMETIC:
-          for (uint32_t i = 0; i < a.g.param[gi]; i++) {
-            const uint64_t comp = gfn::add(gfn::mul(gfn::mul(WV(4 * i), WV(4 * i + 1)), gc[0]),
-                                           gfn::mul(WV(4 * i + 2), gc[N]));
-            A.emit(gfn::sub(WV(4 * i + 3), comp));
-          }
-          break;
-        default:
-          recursion_gate(kind, a.g.param[gi], a.g.param2[gi], a.g.param3[gi], wl, gc, N, A);
-          break;
-      }
-    }
-    acc0 = gfn::add(acc0, gfn::mul(f, A.s0));
-    acc1 = gfn::add(acc1, gfn::mul(f, A.s1));
-  }
-  if (PH == 0) {
-    q[t] = acc0;
-    q[N + t] = acc1;
-  } else {
-    if (PH == 1) {
-      acc0 = gfn::add(acc0, q[t]);
-      acc1 = gfn::add(acc1, q[N + t]);
-    }
-    const uint64_t zh_inv = a.zh_inv[j & ((1u << a.rate_bits) - 1)];
-    q[t] = gfn::canon(gfn::mul(acc0, zh_inv));
-    q[N + t] = gfn::canon(gfn::mul(acc1, zh_inv));
-  }
-}
 // Single-read form (the default): every LDE column is read once per point,
 // wires 0..23 a second time by the Poseidon gate (its inputs and outputs).
 // While wires 0..R-1 stream by, the permutation checks of BOTH challenges
@@ -742,8 +567,9 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(QP_QGE
 // Arithmetic constraints accumulate, each term at its own alpha power (the
 // alpha-weighted sums do not depend on evaluation order); then the Poseidon
 // gate.  Per point: 135 + 24 wire, 84 constants/sigmas and 20 + 2 zs reads
-// against 241 distinct values (the PH 2 form re-read the wires per challenge
-// and per gate: 3.0x the algorithmic HBM bytes, profiles/r01_v5_pmc_hbm_b128.json).
+// against 241 distinct values (a one-pass generic form that re-read the wires
+// per challenge and per gate moved 3.0x the algorithmic HBM bytes,
+// profiles/r01_v5_pmc_hbm_b128.json).
 __device__ __forceinline__ void emit_at(const uint64_t *__restrict__ p0, const uint64_t *__restrict__ p1, uint32_t i,
                                         uint64_t t, uint64_t &s0, uint64_t &s1) {
   uint64_t m0, m1;
@@ -759,13 +585,8 @@ __device__ __forceinline__ uint64_t mul_pow2_rt(uint64_t x, uint32_t e) {
 
 // wires kept in LDS for the Poseidon gate: 16 x 256 lanes x 8 B = 32 KB per
 // workgroup, 5 workgroups per CU (4 waves/SIMD need 4)
-#ifndef QP_QSTASH
-#define QP_QSTASH 16
-#endif
-#ifndef QP_QPREFETCH
-#define QP_QPREFETCH 4
-#endif
-__global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(QP_QUOTIENT_WAVES)))
+constexpr uint32_t QSTASH = 16, QPREFETCH = 4;
+__global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4)))
 k_quotient_1r(QuotientArgs a) {
   const uint32_t logN = a.log_n + a.rate_bits;
   const uint64_t N = 1ull << logN;
@@ -817,12 +638,12 @@ k_quotient_1r(QuotientArgs a) {
   uint64_t sc0 = 0, sc1 = 0, sp0 = 0, sp1 = 0, sb0 = 0, sb1 = 0, sa0 = 0, sa1 = 0;
   uint64_t bs_acc = 0, w0 = 0, wa0 = 0, wa1 = 0, wa2 = 0;
   // the Poseidon gate reads wires 0..23 again after the sweep: the first
-  // QP_QSTASH of them are kept in LDS (per lane, conflict-free [j][lane])
-  __shared__ uint64_t stash[(QP_QSTASH ? QP_QSTASH : 1) * 256];
-  const uint32_t nst = g_pos >= 0 ? (R < QP_QSTASH ? R : QP_QSTASH) : 0;
-  // QP_QPREFETCH wires and sigmas loaded ahead of the sweep (the loads of
-  // iteration jj + QP_QPREFETCH are issued before iteration jj's arithmetic)
-  constexpr uint32_t PF = QP_QPREFETCH;
+  // QSTASH of them are kept in LDS (per lane, conflict-free [j][lane])
+  __shared__ uint64_t stash[QSTASH * 256];
+  const uint32_t nst = g_pos >= 0 ? (R < QSTASH ? R : QSTASH) : 0;
+  // QPREFETCH wires and sigmas loaded ahead of the sweep (the loads of
+  // iteration jj + QPREFETCH are issued before iteration jj's arithmetic)
+  constexpr uint32_t PF = QPREFETCH;
   uint64_t wbuf[PF ? PF : 1], sbuf[PF ? PF : 1];
   if constexpr (PF > 0) {
 #pragma unroll
@@ -979,252 +800,9 @@ k_quotient_1r(QuotientArgs a) {
   q[N + t] = gfn::canon(gfn::mul(acc1, zh_inv));
 }
 
-// ---- k_quotient_fused: k_quotient_1r for the standard layout (80 routed
-// wires in chunks of 8, Poseidon gate on wires 0..134) with every wire read
-// from HBM exactly once.  The Poseidon gate reads its wires in the order
-// 24, 25..28 / 0..7 interleaved, 8..11, 29..64 (full rounds), 65..86
-// (partial), 87..134, 12..23 (outputs); within every chunk of 8 routed wires
-// the highest index comes last.  The reader (FusedRead) copies each routed
-// wire into an LDS slot as the gate reads it and runs the permutation-
-// argument / gate-term sweep over complete chunks at six read points: after
-// wire 7 chunk 0, 39 chunks 3-4, 47 chunk 5, 63 chunks 6-7, 87 (the first
-// read after the partial rounds, whose grouped code has no registers to
-// spare) chunks 8-9, 23 chunks 1-2.  Slots: chunk parity * 8 + j % 8,
-// wires 8..11 at 16..19 (pending from the gate's start to its outputs), so
-// no two pending wires share a slot: 20 slots = 40 KB per 256-lane workgroup.
-// Every term goes to its own alpha power (emit_at), so the chunk order does
-// not change the sums mod p; the base-sum gate's closing term is emitted
-// after all chunks.  In k_quotient_1r the gate re-reads wires 16..79 after
-// the sweep (L2 cannot hold a workgroup's 160 KB of routed wires): 1.28x the
-// algorithmic HBM bytes.  Opt-in (QPGPU_QUOTIENT=fused): bit-exact, but the
-// sweep's temporaries on top of the gate's live state do not fit 128 VGPRs
-// (368 spilled at 4 waves/SIMD, 27 at 3), and at 3 waves it measured slower:
-// 9.43 vs 7.46 ms per 86-proof launch, 1123 vs 1165 proofs/s e2e
-// (profiles/r03_ab_quotient_fused.log).
-constexpr uint32_t QF_SLOTS = 20;
-
-// GEN^(8k): the coset factor k_j = GEN^j at the first wire of chunk k
-constexpr uint64_t qf_mulmod(uint64_t a, uint64_t b) { return (uint64_t)(((unsigned __int128)a * b) % gl::P); }
-constexpr uint64_t qf_pow(uint64_t b, uint32_t e) { return e ? qf_mulmod(b, qf_pow(b, e - 1)) : 1; }
-__device__ const uint64_t QF_GPOW8[10] = {qf_pow(gl::GEN, 0),  qf_pow(gl::GEN, 8),  qf_pow(gl::GEN, 16), qf_pow(gl::GEN, 24),
-                                          qf_pow(gl::GEN, 32), qf_pow(gl::GEN, 40), qf_pow(gl::GEN, 48), qf_pow(gl::GEN, 56),
-                                          qf_pow(gl::GEN, 64), qf_pow(gl::GEN, 72)};
-
-__device__ __forceinline__ uint32_t qf_slot(uint32_t j) {
-  return (j >> 3) == 1 && j < 12 ? 16 + (j - 8) : ((j >> 3) & 1) * 8 + (j & 7);
-}
-
-struct QfState {
-  const uint64_t *cs, *zl, *gc, *ch, *p0, *p1, *gpow8;
-  uint64_t *stash;
-  uint64_t N;
-  uint32_t t, tn, nchunks, npp, num_constants, n_const, n_pi, L, n_ar;
-  uint64_t gamma0, gamma1, beta0, beta1, bx0, bx1;
-  uint64_t z[2], nxk[2];
-  int lastk;
-  uint64_t acc0, acc1, sc0, sc1, sp0, sp1, sb0, sb1, sa0, sa1, bs_acc, w0;
-};
-
-// chunks k0 .. k1-1: their 8 wires from the LDS slots, sigmas from HBM
-// (two loads ahead), the chunk's Z/partial-product check and the per-wire
-// terms of the constant / public-input / base-sum / arithmetic gates
-__device__ __forceinline__ void qf_sweep(QfState &S, uint32_t k0, uint32_t k1) {
-#ifndef QF_FENCE
-#define QF_FENCE 0
-#endif
-  if (QF_FENCE) asm volatile("" ::: "memory");
-  const uint32_t pre = 2 * (1 + S.nchunks);
-#pragma unroll 1
-  for (uint32_t k = k0; k < k1; k++) {
-    const uint32_t j0 = 8 * k;
-    uint64_t num0 = 1, den0 = 1, num1 = 1, den1 = 1;
-    uint64_t bkx0 = gfn::mul(S.bx0, S.gpow8[k]), bkx1 = gfn::mul(S.bx1, S.gpow8[k]);
-    const uint64_t *sgp = S.cs + (uint64_t)(S.num_constants + j0) * S.N;
-    uint64_t sgn0 = sgp[0], sgn1 = sgp[S.N];
-#pragma unroll 1
-    for (uint32_t u = 0; u < 8; u++) {
-      const uint32_t jj = j0 + u;
-      const uint64_t w = S.stash[qf_slot(jj) * blockDim.x + threadIdx.x];
-      const uint64_t sg = sgn0;
-      sgn0 = sgn1;
-      if (u + 2 < 8) sgn1 = sgp[(uint64_t)(u + 2) * S.N];
-      num0 = gfn::mul(num0, gfn::add(gfn::add_c(w, S.gamma0), bkx0));
-      den0 = gfn::mul(den0, gfn::add(gfn::add_c(w, S.gamma0), gfn::mul(S.beta0, sg)));
-      num1 = gfn::mul(num1, gfn::add(gfn::add_c(w, S.gamma1), bkx1));
-      den1 = gfn::mul(den1, gfn::add(gfn::add_c(w, S.gamma1), gfn::mul(S.beta1, sg)));
-      bkx0 = gfn::mul(bkx0, gl::GEN);
-      bkx1 = gfn::mul(bkx1, gl::GEN);
-      if (jj < S.n_const) emit_at(S.p0, S.p1, pre + jj, gfn::sub(S.gc[(uint64_t)jj * S.N], w), S.sc0, S.sc1);
-      if (jj < S.n_pi) emit_at(S.p0, S.p1, pre + jj, gfn::sub(w, S.ch[CH_PIH + jj]), S.sp0, S.sp1);
-      if (S.L) {
-        if (jj == 0) {
-          S.w0 = w;
-        } else if (jj <= S.L) {
-          S.bs_acc = gfn::add(S.bs_acc, mul_pow2_rt(w, jj - 1));
-          emit_at(S.p0, S.p1, pre + jj, gfn::mul(w, gfn::sub(w, 1)), S.sb0, S.sb1);
-        }
-      }
-      if (jj < 4 * S.n_ar && (jj & 3) == 3) {
-        // the op's other three wires from their slots (same chunk)
-        const uint64_t wa0 = S.stash[qf_slot(jj - 3) * blockDim.x + threadIdx.x];
-        const uint64_t wa1 = S.stash[qf_slot(jj - 2) * blockDim.x + threadIdx.x];
-        const uint64_t wa2 = S.stash[qf_slot(jj - 1) * blockDim.x + threadIdx.x];
-        const uint64_t comp = gfn::add(gfn::mul(gfn::mul(wa0, wa1), S.gc[0]), gfn::mul(wa2, S.gc[S.N]));
-        emit_at(S.p0, S.p1, pre + jj / 4, gfn::sub(w, comp), S.sa0, S.sa1);
-      }
-    }
-#pragma unroll
-    for (uint32_t c = 0; c < 2; c++) {
-      const uint64_t prev = k == 0 ? S.z[c]
-                          : S.lastk == (int)k - 1 ? S.nxk[c]
-                                                  : S.zl[((uint64_t)2 + c * S.npp + k - 1) * S.N + S.t];
-      const uint64_t nx = k == S.nchunks - 1 ? S.zl[(uint64_t)c * S.N + S.tn]
-                                             : S.zl[((uint64_t)2 + c * S.npp + k) * S.N + S.t];
-      const uint64_t num = c ? num1 : num0, den = c ? den1 : den0;
-      emit_at(S.p0, S.p1, 2 + c * S.nchunks + k, gfn::sub(gfn::mul(prev, num), gfn::mul(nx, den)), S.acc0, S.acc1);
-      S.nxk[c] = nx;
-    }
-    S.lastk = (int)k;
-  }
-  if (QF_FENCE) asm volatile("" ::: "memory");
-}
-
-struct FusedRead {
-  const uint64_t *__restrict__ wl;
-  uint64_t N;
-  QfState *S;
-  __device__ __forceinline__ uint64_t operator()(uint32_t j) const {
-    const uint64_t w = wl[(uint64_t)j * N];
-    if (j < 80) S->stash[qf_slot(j) * blockDim.x + threadIdx.x] = w;
-#ifndef QF_SITES
-#define QF_SITES 0x3F
-#endif
-    switch (j) {
-      case 7: if (QF_SITES & 1) qf_sweep(*S, 0, 1); break;
-      case 39: if (QF_SITES & 2) qf_sweep(*S, 3, 5); break;
-      case 47: if (QF_SITES & 4) qf_sweep(*S, 5, 6); break;
-      case 63: if (QF_SITES & 8) qf_sweep(*S, 6, 8); break;
-      case 87: if (QF_SITES & 16) qf_sweep(*S, 8, 10); break;  // after the partial rounds (less live state)
-      case 23: if (QF_SITES & 32) qf_sweep(*S, 1, 3); break;
-      default: break;
-    }
-    return w;
-  }
-};
-
-#ifndef QP_QFUSED_WAVES
-#define QP_QFUSED_WAVES 3
-#endif
-__global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(QP_QFUSED_WAVES)))
-k_quotient_fused(QuotientArgs a) {
-  const uint32_t logN = a.log_n + a.rate_bits;
-  const uint64_t N = 1ull << logN;
-  const uint32_t t = blockIdx.x * blockDim.x + threadIdx.x;
-  if (t >= N) return;
-  const uint32_t b = blockIdx.y;
-  __shared__ uint64_t stash[QF_SLOTS * 256];
-  QfState S;
-  S.ch = a.chal + b * CHAL_STRIDE;
-  S.cs = a.cs_lde + t;
-  const uint64_t *wl = a.w_lde + b * a.w_bstride + t;
-  S.zl = a.z_lde + b * a.z_bstride;
-  const uint32_t j = gl::rev_bits(t, logN);
-  uint64_t *q = a.q_out + b * a.q_bstride;
-  S.p0 = a.apow + (uint64_t)b * 2 * APOW_STRIDE;
-  S.p1 = S.p0 + APOW_STRIDE;
-  S.gpow8 = QF_GPOW8;
-  S.stash = stash;
-  S.N = N;
-  S.t = t;
-  S.nchunks = 10;
-  S.npp = 9;
-  S.tn = gl::rev_bits((j + (1u << a.rate_bits)) & (uint32_t)(N - 1), logN);
-  S.gc = S.cs + (uint64_t)a.g.nsel * N;
-  S.num_constants = a.num_constants;
-  int g_const = -1, g_pi = -1, g_bs = -1, g_ar = -1, g_pos = -1;
-  for (uint32_t gi = 0; gi < a.g.ngates; gi++) {
-    switch (a.g.kind[gi]) {
-      case GK_CONSTANT: g_const = (int)gi; break;
-      case GK_PUBLIC_INPUT: g_pi = (int)gi; break;
-      case GK_BASE_SUM: g_bs = (int)gi; break;
-      case GK_ARITHMETIC: g_ar = (int)gi; break;
-      case GK_POSEIDON: g_pos = (int)gi; break;
-      default: break;
-    }
-  }
-  S.n_const = g_const >= 0 ? a.g.param[g_const] : 0;
-  S.n_pi = g_pi >= 0 ? 4 : 0;
-  S.L = g_bs >= 0 ? a.g.param[g_bs] : 0;
-  S.n_ar = g_ar >= 0 ? a.g.param[g_ar] : 0;
-  S.acc0 = S.acc1 = 0;
-  const uint64_t x = a.xtab[t], l0 = a.l0tab[t];
-  for (uint32_t c = 0; c < 2; c++) {
-    S.z[c] = S.zl[(uint64_t)c * N + t];
-    emit_at(S.p0, S.p1, c, gfn::mul(l0, gfn::sub(S.z[c], 1)), S.acc0, S.acc1);
-  }
-  S.beta0 = S.ch[CH_BETA];
-  S.beta1 = S.ch[CH_BETA + 1];
-  S.gamma0 = S.ch[CH_GAMMA];
-  S.gamma1 = S.ch[CH_GAMMA + 1];
-  S.bx0 = gfn::mul(S.beta0, x);
-  S.bx1 = gfn::mul(S.beta1, x);
-  S.lastk = -1;
-  S.sc0 = S.sc1 = S.sp0 = S.sp1 = S.sb0 = S.sb1 = S.sa0 = S.sa1 = 0;
-  S.bs_acc = S.w0 = 0;
-  // the Poseidon gate, sweeping the routed wires as it reads them
-  TermAcc A;
-  A.p0 = S.p0;
-  A.p1 = S.p1;
-  A.s0 = A.s1 = 0;
-  A.i = 2 * (1 + S.nchunks);
-  FusedRead rd{wl, N, &S};
-  poseidon_gate_rd(rd, A);
-  const uint32_t pre = 2 * (1 + S.nchunks);
-  if (S.L && S.L < 80) emit_at(S.p0, S.p1, pre, gfn::sub(S.bs_acc, S.w0), S.sb0, S.sb1);
-  const uint32_t nsel = a.g.nsel;
-  auto filter = [&](int gi) -> uint64_t {
-    const uint32_t si = a.g.sel_index[gi];
-    const uint64_t sv = S.cs[(uint64_t)si * N];
-    uint64_t f = 1;
-    for (uint32_t jg = a.g.grp_lo[si]; jg < a.g.grp_hi[si]; jg++)
-      if (jg != (uint32_t)gi) f = gfn::mul(f, gfn::sub(jg, sv));
-    if (nsel > 1) f = gfn::mul(f, gfn::sub(0xFFFFFFFFull, sv));
-    return f;
-  };
-  uint64_t acc0 = S.acc0, acc1 = S.acc1;
-  if (g_const >= 0) {
-    const uint64_t f = filter(g_const);
-    acc0 = gfn::add(acc0, gfn::mul(f, S.sc0));
-    acc1 = gfn::add(acc1, gfn::mul(f, S.sc1));
-  }
-  if (g_pi >= 0) {
-    const uint64_t f = filter(g_pi);
-    acc0 = gfn::add(acc0, gfn::mul(f, S.sp0));
-    acc1 = gfn::add(acc1, gfn::mul(f, S.sp1));
-  }
-  if (g_bs >= 0) {
-    const uint64_t f = filter(g_bs);
-    acc0 = gfn::add(acc0, gfn::mul(f, S.sb0));
-    acc1 = gfn::add(acc1, gfn::mul(f, S.sb1));
-  }
-  if (g_ar >= 0) {
-    const uint64_t f = filter(g_ar);
-    acc0 = gfn::add(acc0, gfn::mul(f, S.sa0));
-    acc1 = gfn::add(acc1, gfn::mul(f, S.sa1));
-  }
-  {
-    const uint64_t f = filter(g_pos);
-    acc0 = gfn::add(acc0, gfn::mul(f, A.s0));
-    acc1 = gfn::add(acc1, gfn::mul(f, A.s1));
-  }
-  const uint64_t zh_inv = a.zh_inv[j & ((1u << a.rate_bits) - 1)];
-  q[t] = gfn::canon(gfn::mul(acc0, zh_inv));
-  q[N + t] = gfn::canon(gfn::mul(acc1, zh_inv));
-}
-
-// ---- per-gate form of the generic quotient (QPGPU_QUOTIENT unset: the
-// default for gate lists outside the leaf set, i.e. the aggregation circuits).
-// The one-pass kernel above evaluates every gate per point and re-reads the
+// ---- per-gate form of the generic quotient (the default for gate lists
+// outside the leaf set, i.e. the aggregation circuits).  A one-pass kernel
+// evaluating every gate per point (removed; measured in round 4) re-reads the
 // wires gate after gate: with 135 wires x 8 B per point and 1,024 points in
 // flight per CU the working set is far beyond L2, so every gate's reads come
 // from HBM again (30 GB per 32-proof level-1 launch, 6.6x the distinct
@@ -1235,9 +813,6 @@ k_quotient_fused(QuotientArgs a) {
 // alpha-weighted terms do not depend on evaluation order), so the output is
 // bit-identical.  PART 0: permutation terms; 1: one non-Poseidon gate; 2: the
 // Poseidon gate.
-#ifndef QP_QPART_INLINE
-#define QP_QPART_INLINE 1
-#endif
 template <int PART>
 __global__ void __launch_bounds__(256) k_quotient_part(QuotientArgs a, uint32_t gi, uint32_t last) {
   const uint32_t logN = a.log_n + a.rate_bits;
@@ -1336,10 +911,7 @@ __global__ void __launch_bounds__(256) k_quotient_part(QuotientArgs a, uint32_t 
           }
           break;
         default:
-          if constexpr (QP_QPART_INLINE)
-            recursion_gate_body(kind, a.g.param[gi], a.g.param2[gi], a.g.param3[gi], wl, gc, N, A);
-          else
-            recursion_gate(kind, a.g.param[gi], a.g.param2[gi], a.g.param3[gi], wl, gc, N, A);
+          recursion_gate_body(kind, a.g.param[gi], a.g.param2[gi], a.g.param3[gi], wl, gc, N, A);
           break;
       }
     }
@@ -1356,72 +928,6 @@ __global__ void __launch_bounds__(256) k_quotient_part(QuotientArgs a, uint32_t 
     q[N + t] = acc1;
   }
 }
-// ---- k_quotient_rest: every gate of gmask (the ones k_quotient_prefix does
-// not take: Poseidon, Reducing(Extension), RandomAccess, CosetInterpolation,
-// PoseidonMds) in one launch, gate after gate per point with both accumulators
-// in registers, instead of one k_quotient_part launch per gate streaming the
-// accumulators through HBM and each gate's columns from HBM again: a point's
-// columns are re-read within microseconds, while the points in flight (≈64k
-// x 1 KB) fit the 256 MB MALL.  Same alpha indices and filters as the part
-// launches: bit-identical.
-#ifndef QP_QREST_WAVES
-#define QP_QREST_WAVES 4
-#endif
-template <bool POS>
-__global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(QP_QREST_WAVES)))
-k_quotient_rest(QuotientArgs a, uint32_t gmask, uint32_t last) {
-  const uint32_t logN = a.log_n + a.rate_bits;
-  const uint64_t N = 1ull << logN;
-  const uint32_t t = blockIdx.x * blockDim.x + threadIdx.x;
-  if (t >= N) return;
-  const uint32_t b = blockIdx.y;
-  const uint64_t *cs = a.cs_lde + t;
-  const uint64_t *wl = a.w_lde + b * a.w_bstride + t;
-  uint64_t *q = a.q_out + b * a.q_bstride;
-  TermAcc A;
-  A.p0 = a.apow + (uint64_t)b * 2 * APOW_STRIDE;
-  A.p1 = A.p0 + APOW_STRIDE;
-  const uint32_t R = a.R, qdf = a.qdf, nchunks = (R + qdf - 1) / qdf;
-  const uint32_t nsel = a.g.nsel;
-  const uint64_t *gc = cs + (uint64_t)nsel * N;
-  uint64_t acc0 = q[t], acc1 = q[N + t];
-#pragma unroll 1
-  for (uint32_t gi = 0; gi < a.g.ngates; gi++) {
-    if (!((gmask >> gi) & 1)) continue;
-    const uint32_t kind = a.g.kind[gi];
-    const uint32_t si = a.g.sel_index[gi];
-    const uint64_t sv = cs[(uint64_t)si * N];
-    uint64_t f = 1;
-    for (uint32_t jj = a.g.grp_lo[si]; jj < a.g.grp_hi[si]; jj++)
-      if (jj != gi) f = gfn::mul(f, gfn::sub(jj, sv));
-    if (nsel > 1) f = gfn::mul(f, gfn::sub(0xFFFFFFFFull, sv));
-    A.s0 = A.s1 = 0;
-    A.i = 2 * (1 + nchunks);
-    // opaque per iteration: keeps the column addresses of every gate from
-    // being hoisted out of the loop into registers (324 B of spill otherwise)
-    const uint64_t *wli = wl, *gci = gc;
-    asm volatile("" : "+v"(wli), "+v"(gci));
-    if (POS && kind == GK_POSEIDON)
-      poseidon_gate(wli, N, A);
-    else
-      recursion_gate_body(kind, a.g.param[gi], a.g.param2[gi], a.g.param3[gi], wli, gci, N, A);
-    acc0 = gfn::add(acc0, gfn::mul(f, A.s0));
-    acc1 = gfn::add(acc1, gfn::mul(f, A.s1));
-  }
-  if (last) {
-    const uint32_t j = gl::rev_bits(t, logN);
-    const uint64_t zh_inv = a.zh_inv[j & ((1u << a.rate_bits) - 1)];
-    q[t] = gfn::canon(gfn::mul(acc0, zh_inv));
-    q[N + t] = gfn::canon(gfn::mul(acc1, zh_inv));
-  } else {
-    q[t] = acc0;
-    q[N + t] = acc1;
-  }
-}
-
-template __global__ void k_quotient_rest<false>(QuotientArgs, uint32_t, uint32_t);
-template __global__ void k_quotient_rest<true>(QuotientArgs, uint32_t, uint32_t);
-
 // ---- k_quotient_prefix: the permutation terms and every gate of gmask that
 // reads routed wires only (Constant, PublicInput, BaseSum, Arithmetic,
 // ArithmeticExtension, MulExtension) in ONE pass over windows of QP_WIN routed
@@ -1434,10 +940,7 @@ template __global__ void k_quotient_rest<true>(QuotientArgs, uint32_t, uint32_t)
 // factor), a divisor of QP_WIN, so windows hold whole chunks and whole ops.
 constexpr uint32_t QP_WIN = 24;  // multiple of 4 (Arithmetic), 6 (MulExtension), 8 (ArithmeticExtension, chunks)
 template <int QDF>
-#ifndef QP_QPREFIX_WAVES
-#define QP_QPREFIX_WAVES 4
-#endif
-__global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(QP_QPREFIX_WAVES)))
+__global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4)))
 k_quotient_prefix(QuotientArgs a, uint32_t gmask, uint32_t last) {
   static_assert(QP_WIN % QDF == 0, "windows hold whole permutation chunks");
   const uint32_t logN = a.log_n + a.rate_bits;
@@ -1613,9 +1116,6 @@ template __global__ void k_quotient_part<0>(QuotientArgs, uint32_t, uint32_t);
 template __global__ void k_quotient_part<1>(QuotientArgs, uint32_t, uint32_t);
 template __global__ void k_quotient_part<2>(QuotientArgs, uint32_t, uint32_t);
 
-template __global__ void k_quotient<0>(QuotientArgs);
-template __global__ void k_quotient<1>(QuotientArgs);
-template __global__ void k_quotient<2>(QuotientArgs);
 #undef WV
 
 // coset iNTT, stage 1: block s' holds coset s = rev_r(s') values in bit-reversed
@@ -1698,12 +1198,11 @@ void quotient_values(const QuotientArgs &a, QuotientKernel k, uint32_t nb, hipSt
   switch (k) {
     case QK_PARTS: {
       // the permutation terms with the gates that read only routed wires
-      // (k_quotient_prefix: one pass, QPGPU_QPREFIX=0 turns it off), then one
-      // launch per other gate (each streams only its gate's columns), the
+      // (k_quotient_prefix: one pass; path hook qprefix=0 turns it off), then
+      // one launch per other gate (each streams only its gate's columns), the
       // last multiplying by 1/Z_H
       uint32_t gmask = 0;
-      const char *pv = getenv("QPGPU_QPREFIX");
-      if (a.qdf == 8 && !(pv && pv[0] == '0'))
+      if (a.qdf == 8 && path_opt("qprefix", 1))
         for (uint32_t gi = 0; gi < a.g.ngates; gi++) {
           const uint32_t p = a.g.param[gi];
           uint64_t wires = ~0ull;
@@ -1718,46 +1217,19 @@ void quotient_values(const QuotientArgs &a, QuotientKernel k, uint32_t nb, hipSt
           }
           if (wires <= a.R) gmask |= 1u << gi;
         }
-      // QPGPU_QREST=1: the recursion gates in one k_quotient_rest launch after
-      // the others (=2: the Poseidon gate too).  Off by default: per 32-proof
-      // level-1 batch 2.18 ms against 2.05 for their five part launches (2: 3.77
-      // against 1.34 + 2.05), subtree unchanged -- these launches are
-      // instruction-bound, not re-read-bound (profiles/r05_ab_quotient_rest.log)
-      uint32_t rmask = 0;
-      const char *rv = getenv("QPGPU_QREST");
-      const int rmode = rv && *rv ? rv[0] - '0' : 0;
-      if (rmode)
-        for (uint32_t gi = 0; gi < a.g.ngates; gi++) {
-          if ((gmask >> gi) & 1) continue;
-          switch (a.g.kind[gi]) {
-            case GK_POSEIDON:
-              if (rmode == 2) rmask |= 1u << gi;
-              break;
-            case GK_ARITH_EXT: case GK_MUL_EXT: case GK_REDUCING: case GK_REDUCING_EXT:
-            case GK_EXPONENTIATION: case GK_POSEIDON_MDS: case GK_RANDOM_ACCESS: case GK_COSET_INTERP:
-              rmask |= 1u << gi;
-              break;
-            default: break;
-          }
-        }
       int lastg = -1;
       for (uint32_t gi = 0; gi < a.g.ngates; gi++)
-        if (a.g.kind[gi] != GK_NOOP && !(((gmask | rmask) >> gi) & 1)) lastg = (int)gi;
-      const bool rest_last = rmask != 0;
-      if (gmask) k_quotient_prefix<8><<<qg, 256, 0, s>>>(a, gmask, lastg < 0 && !rest_last);
-      else k_quotient_part<0><<<qg, 256, 0, s>>>(a, 0, lastg < 0 && !rest_last);
+        if (a.g.kind[gi] != GK_NOOP && !((gmask >> gi) & 1)) lastg = (int)gi;
+      if (gmask) k_quotient_prefix<8><<<qg, 256, 0, s>>>(a, gmask, lastg < 0);
+      else k_quotient_part<0><<<qg, 256, 0, s>>>(a, 0, lastg < 0);
       for (uint32_t gi = 0; gi < a.g.ngates; gi++) {
-        if (a.g.kind[gi] == GK_NOOP || (((gmask | rmask) >> gi) & 1)) continue;
-        const uint32_t l = (int)gi == lastg && !rest_last;
+        if (a.g.kind[gi] == GK_NOOP || ((gmask >> gi) & 1)) continue;
+        const uint32_t l = (int)gi == lastg;
         if (a.g.kind[gi] == GK_POSEIDON) k_quotient_part<2><<<qg, 256, 0, s>>>(a, gi, l);
         else k_quotient_part<1><<<qg, 256, 0, s>>>(a, gi, l);
       }
-      if (rmask && rmode == 2) k_quotient_rest<true><<<qg, 256, 0, s>>>(a, rmask, 1);
-      else if (rmask) k_quotient_rest<false><<<qg, 256, 0, s>>>(a, rmask, 1);
       break;
     }
-    case QK_ONEPASS: k_quotient<2><<<qg, 256, 0, s>>>(a); break;
-    case QK_FUSED: k_quotient_fused<<<qg, 256, 0, s>>>(a); break;
     case QK_1R: k_quotient_1r<<<qg, 256, 0, s>>>(a); break;
   }
 }
@@ -1896,9 +1368,9 @@ void openings(OpeningsArgs a, uint32_t nb, hipStream_t s) {
     a.ngroups += (a.seg[j].npolys + OPEN_PB - 1) / OPEN_PB;
     a.ntot = std::max(a.ntot, a.seg[j].out_off + a.seg[j].npolys);
   }
-  // QPGPU_OPEN_SLICES=1: one block per group (the former launches' shape)
-  const char *e = getenv("QPGPU_OPEN_SLICES");
-  const uint32_t smax = e && *e ? std::min<uint32_t>((uint32_t)atoi(e), OPEN_MAX_SLICES) : OPEN_MAX_SLICES;
+  // path hook open_slices=1: one block per group (the shape of the large batches)
+  const uint32_t smax = (uint32_t)std::min<long>(std::max<long>(path_opt("open_slices", OPEN_MAX_SLICES), 1),
+                                                 OPEN_MAX_SLICES);
   a.S = 1;
   while (a.S * 2 <= smax && a.S * 2 * T * 8 <= n && (uint64_t)a.ngroups * nb * a.S < 1024) a.S *= 2;
   k_openings_seg<<<dim3(a.ngroups * a.S, nb), T, 0, s>>>(a);
@@ -2057,15 +1529,12 @@ __global__ void __launch_bounds__(256) k_fri_leaf_row(const uint64_t *__restrict
   if (l16 < 4) dig[b * d_bstride + (uint64_t)i * 4 + l16] = psd::canon(x);
 }
 
-// leaves of a FRI layer: the row form up to QP_FRI_ROW_MAX leaves over the
-// batch (QPGPU_FRI_ROW overrides, 0 = never), the one-lane form above
-#ifndef QP_FRI_ROW_MAX
-#define QP_FRI_ROW_MAX 16384
-#endif
+// leaves of a FRI layer: the row form up to FRI_ROW_MAX leaves over the
+// batch (path hook fri_row), the one-lane form above
+constexpr long FRI_ROW_MAX = 16384;
 void fri_leaf(const uint64_t *vals, uint64_t *dig, uint32_t log_len, uint32_t ab, uint64_t v_bstride,
               uint64_t d_bstride, uint32_t nb, hipStream_t s) {
-  const char *e = getenv("QPGPU_FRI_ROW");
-  const uint64_t lim = e && *e ? strtoull(e, nullptr, 10) : QP_FRI_ROW_MAX;
+  const uint64_t lim = (uint64_t)path_opt("fri_row", FRI_ROW_MAX);
   const uint64_t nl = 1ull << (log_len - ab);
   if ((2u << ab) > 4 && nl * nb <= lim)
     k_fri_leaf_row<<<dim3((unsigned)((nl + 15) / 16), nb), 256, 0, s>>>(vals, dig, log_len, ab, v_bstride, d_bstride);
@@ -2127,12 +1596,13 @@ __device__ __forceinline__ bool pow_hit(const uint64_t *__restrict__ pre, uint32
   return (psd::canon(s[7]) >> (64 - bits)) == 0;
 }
 
-// CPT candidates per thread per claimed block (blocks of 256 CPT candidates)
-template <int CPT>
+// one candidate per thread per claimed block of 256 (2 or 4 per thread and
+// per-wave claims measured no better: profiles/r05_ab_pow_cpt.log,
+// r05_ab_pow_wave.log)
 __global__ void __launch_bounds__(256) k_pow_scan(const uint64_t *__restrict__ states, const uint32_t *__restrict__ pos,
                                                   uint64_t *__restrict__ found, uint64_t *__restrict__ next, uint32_t nb,
                                                   uint32_t bits, uint64_t limit) {
-  constexpr uint64_t BLK = 256ull * CPT;
+  constexpr uint64_t BLK = 256;
   __shared__ uint64_t blk;
   __shared__ uint32_t done;
   for (uint32_t i = 0; i < nb; i++) {
@@ -2149,71 +1619,11 @@ __global__ void __launch_bounds__(256) k_pow_scan(const uint64_t *__restrict__ s
       const uint32_t d = done;
       __syncthreads();  // every lane has read blk / done before lane 0 rewrites them
       if (d) break;
-#pragma unroll 1
-      for (int j = 0; j < CPT; j++) {
-        const uint64_t cand = k * BLK + 256ull * j + threadIdx.x;
-        if (pow_hit(pre, pos[b], cand, bits)) atomicMin((unsigned long long *)(found + b), (unsigned long long)cand);
-      }
-    }
-  }
-}
-template __global__ void k_pow_scan<1>(const uint64_t *, const uint32_t *, uint64_t *, uint64_t *, uint32_t, uint32_t,
-                                       uint64_t);
-template __global__ void k_pow_scan<2>(const uint64_t *, const uint32_t *, uint64_t *, uint64_t *, uint32_t, uint32_t,
-                                       uint64_t);
-template __global__ void k_pow_scan<4>(const uint64_t *, const uint32_t *, uint64_t *, uint64_t *, uint32_t, uint32_t,
-                                       uint64_t);
-
-// k_pow_scan with per-wave claims: lane 0 of each wave takes the next 64-candidate
-// chunk of its proof (a vector atomic, broadcast with readfirstlane), so no
-// workgroup barrier stands between a claim and the permutations; waves start
-// spread over the proofs and move on as k_pow_scan's workgroups do.  Same
-// minimal witness (every candidate below the first hit is tested).
-__global__ void __launch_bounds__(256) k_pow_scan_w(const uint64_t *__restrict__ states,
-                                                    const uint32_t *__restrict__ pos, uint64_t *__restrict__ found,
-                                                    uint64_t *__restrict__ next, uint32_t nb, uint32_t bits,
-                                                    uint64_t limit) {
-  const uint32_t lane = threadIdx.x & 63;
-  const uint32_t wave = blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6);
-  for (uint32_t i = 0; i < nb; i++) {
-    const uint32_t b = (wave + i) % nb;
-    const uint64_t *pre = states + b * 24;
-    for (;;) {
-      uint64_t k = 0, f = 0;
-      if (lane == 0) {
-        k = atomicAdd((unsigned long long *)(next + b), 1ull);
-        f = *(const volatile uint64_t *)(found + b);
-      }
-      k = ((uint64_t)__builtin_amdgcn_readfirstlane((uint32_t)(k >> 32)) << 32) |
-          __builtin_amdgcn_readfirstlane((uint32_t)k);
-      f = ((uint64_t)__builtin_amdgcn_readfirstlane((uint32_t)(f >> 32)) << 32) |
-          __builtin_amdgcn_readfirstlane((uint32_t)f);
-      if (k * 64 >= limit || k * 64 >= f) break;  // wave-uniform
-      const uint64_t cand = k * 64 + lane;
+      const uint64_t cand = k * BLK + threadIdx.x;
       if (pow_hit(pre, pos[b], cand, bits)) atomicMin((unsigned long long *)(found + b), (unsigned long long)cand);
     }
   }
 }
-
-__global__ void __launch_bounds__(256) k_pow(const uint64_t *__restrict__ states, const uint32_t *__restrict__ pos,
-                                             const uint32_t *__restrict__ active, uint64_t *__restrict__ found,
-                                             uint64_t base, uint32_t bits) {
-  const uint32_t b = active[blockIdx.y];
-  const uint64_t cand = base + (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  // round 0 precomputed on the host (prover.cpp): s = K + coef * sbox(cand + rc_pos)
-  const uint64_t *pre = states + b * 24;
-  const uint64_t y = pf::sbox(pf::add_c(cand, ps::RC_DEV[pos[b]]));
-  const uint32_t y0 = pf::lo32(y), y1 = pf::hi32(y);
-  uint64_t s[12];
-#pragma unroll
-  for (int r = 0; r < 12; r++) {
-    const uint32_t c = (uint32_t)pre[12 + r];
-    s[r] = pf::reduce_row((uint64_t)y0 * c + (pre[r] & pf::EPS), (uint64_t)y1 * c + (pre[r] >> 32));
-  }
-  pf::rounds<QP_POSEIDON_MODE, 1, 0x80u>(s);  // only lane 7 is read
-  if ((psd::canon(s[7]) >> (64 - bits)) == 0) atomicMin((unsigned long long *)&found[b], (unsigned long long)cand);
-}
-
 // ---------------------------------------------------------------- gathers
 
 // out[b][q][c] = cols[b*bstride + c*stride + idx[b][q] >> shift]

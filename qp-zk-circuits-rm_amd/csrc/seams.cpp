@@ -21,6 +21,7 @@
 #include "field.h"
 #include "kernels.h"
 #include "prover_kernels.h"
+#include "paths.h"
 
 namespace {
 
@@ -33,11 +34,6 @@ struct DMem {  // device allocation owned by one call
 };
 
 inline unsigned cdiv(uint64_t a, unsigned b) { return (unsigned)((a + b - 1) / b); }
-
-bool getenv_flag_eq(const char *name, const char *value) {
-  const char *v = getenv(name);
-  return v && !strcmp(v, value);
-}
 
 }  // namespace
 
@@ -125,7 +121,7 @@ int qp_quotient(qp_ctx *ctx, const qp_batch *cs, const qp_batch *wires, const qp
       ctx->err = "qp_quotient: selector group " + std::to_string(s) + " out of range";
       return QP_ERR_ARG;
     }
-  bool fast = g->num_gates <= 8 && !getenv_flag_eq("QPGPU_QUOTIENT", "generic");
+  bool fast = g->num_gates <= 8 && !qpk::path_opt("quotient_parts", 0);
   uint32_t seen = 0;
   for (uint32_t i = 0; i < g->num_gates; i++) {
     const uint32_t k = g->kind[i], p = g->param[i], p2 = g->param2[i], p3 = g->param3[i];
@@ -238,10 +234,8 @@ int qp_quotient(qp_ctx *ctx, const qp_batch *cs, const qp_batch *wires, const qp
       a.g.grp_hi[i] = g->group_hi[i];
     }
     // the prover's kernels: the single-read one for the leaf gate set, else
-    // the permutation terms and one launch per gate (QPGPU_QUOTIENT=onepass:
-    // any gate list in one pass)
-    const qpk::QuotientKernel qk =
-        fast ? qpk::QK_1R : getenv_flag_eq("QPGPU_QUOTIENT", "onepass") ? qpk::QK_ONEPASS : qpk::QK_PARTS;
+    // the permutation terms and one launch per gate
+    const qpk::QuotientKernel qk = fast ? qpk::QK_1R : qpk::QK_PARTS;
     qpk::quotient_values(a, qk, 1, s);
     qpk::quotient_coeffs(ctx->tw, d_q.p, d_cbuf.p, d_out.p, log_n, rb, nc, 1, 2 * N, 2 * N, (uint64_t)nc * qdf * n, s);
     QP_HIP_TRY(ctx, hipGetLastError());
@@ -407,7 +401,7 @@ int qp_pow_grind(qp_ctx *ctx, const uint64_t *states, const uint32_t *pos, uint3
     QP_HIP_TRY(ctx, hipMemsetAsync(d_next.p, 0, n * 8ull, s));
     // the prover's single-launch minimal-witness search (prover.cpp stage 6)
     const uint64_t limit = 1ull << std::min<uint32_t>(pow_bits + 20, 62);
-    qpk::k_pow_scan<1><<<2048, 256, 0, s>>>(d_pre.p, (const uint32_t *)d_pos.p, d_found.p, d_next.p, n, pow_bits, limit);
+    qpk::k_pow_scan<<<2048, 256, 0, s>>>(d_pre.p, (const uint32_t *)d_pos.p, d_found.p, d_next.p, n, pow_bits, limit);
     QP_HIP_TRY(ctx, hipGetLastError());
     QP_HIP_TRY(ctx, hipMemcpyAsync(found.data(), d_found.p, n * 8ull, hipMemcpyDeviceToHost, s));
     QP_HIP_TRY(ctx, hipStreamSynchronize(s));

@@ -100,31 +100,11 @@ __device__ __forceinline__ void slots_load(uint32_t (&sl)[N], const uint32_t *ws
 #pragma unroll
   for (int i = 0; i < N; i++) sl[i] = ws[j0 + i];
 }
-struct WitPartialHook {
-  uint64_t *v;
-  const uint32_t *sl;  // the 22 partial-round slots
-  bool &ok;
-  __device__ __forceinline__ uint64_t operator()(int T, uint64_t s0) const {
-    wput(v, sl[T], s0, ok);
-    return s0;
-  }
-};
-template <int T>
-__device__ __forceinline__ void wit_partial(uint64_t *v, const uint32_t (&sl)[22], bool &ok, uint64_t s[12]) {
-  if constexpr (T < 22) {
-    constexpr int G = (22 - T) < QP_PF_GROUP ? (22 - T) : QP_PF_GROUP;
-    if constexpr (G > 1) {
-      pf::partial_group<T, G>(s, WitPartialHook{v, sl, ok});
-    } else {
-      wput(v, sl[T], s[0], ok);
-      pf::partial_sparse<T>(s);
-    }
-    wit_partial<T + G>(v, sl, ok, s);
-  }
-}
-// rolled form (QP_WIT_POSEIDON=2): every round a loop iteration with the
-// round constants from memory, plain partial rounds (full MDS): a few
-// thousand instructions of code instead of the unrolled form's ~280 KB
+// Every round a loop iteration with the round constants from memory, plain
+// partial rounds (full MDS): a few thousand instructions of code.  Measured
+// against the unrolled sparse-round form (~280 KB of code) and a first form
+// with a slot lookup per write (tools/gpu_session.sh wit_ab, 256-leaf subtree,
+// profiles/r04_wit_ab.log): rolled 0.566 s, unrolled 0.607 s, plain 0.668 s
 __device__ __noinline__ bool poseidon_witness_rolled(uint64_t *v, const uint32_t *__restrict__ ws) {
   bool in_ok = true, ok = true;
   uint64_t s[12];
@@ -179,65 +159,6 @@ __device__ __noinline__ bool poseidon_witness_rolled(uint64_t *v, const uint32_t
   pf::mds<3, -1>(s);
 #pragma unroll
   for (int i = 0; i < 12; i++) wput(v, sl[i], s[i], ok);
-  return ok;
-}
-
-__device__ __noinline__ bool poseidon_witness(uint64_t *v, const uint32_t *__restrict__ ws) {
-  bool in_ok = true, ok = true;
-  uint64_t s[12];
-  uint32_t sd[4], sa[12], sb[12];
-  for (int i = 0; i < 12; i++) s[i] = rd(v, ws[i], in_ok);
-  const uint64_t swap = rd(v, ws[24], in_ok);
-  slots_load(sd, ws, 25);
-  slots_load(sa, ws, 29);
-  if (!in_ok) return false;
-#pragma unroll
-  for (int i = 0; i < 4; i++) wput(v, sd[i], gl::mul(swap, gl::sub(s[i + 4], s[i])), ok);
-  if (swap == 1)
-    for (int i = 0; i < 4; i++) {
-      const uint64_t t = s[i];
-      s[i] = s[i + 4];
-      s[i + 4] = t;
-    }
-#pragma unroll
-  for (int i = 0; i < 12; i++) s[i] = pf::add_c(s[i], ps::rc_cx(i));
-  // first full rounds: the state entering rounds 1..3 (after their constants)
-  pf::sbox12(s);
-  pf::mds<3, 1>(s);
-  slots_load(sb, ws, 41);
-#pragma unroll
-  for (int i = 0; i < 12; i++) wput(v, sa[i], s[i], ok);
-  pf::sbox12(s);
-  pf::mds<3, 2>(s);
-  slots_load(sa, ws, 53);
-#pragma unroll
-  for (int i = 0; i < 12; i++) wput(v, sb[i], s[i], ok);
-  pf::sbox12(s);
-  pf::mds<3, 3>(s);
-  uint32_t sp[22];
-  slots_load(sp, ws, 65);
-#pragma unroll
-  for (int i = 0; i < 12; i++) wput(v, sa[i], s[i], ok);
-  pf::sbox12(s);
-  pf::mds_init_sparse(s);
-  slots_load(sa, ws, 87);
-  wit_partial<0>(v, sp, ok, s);
-  // second full rounds: the state entering rounds 26..29, then the output
-#pragma unroll
-  for (int r = 0; r < 4; r++) {
-    slots_load(sb, ws, r < 3 ? 99 + 12 * r : 12);
-#pragma unroll
-    for (int i = 0; i < 12; i++) wput(v, sa[i], s[i], ok);
-    pf::sbox12(s);
-    if (r == 0) pf::mds<3, 27>(s);
-    else if (r == 1) pf::mds<3, 28>(s);
-    else if (r == 2) pf::mds<3, 29>(s);
-    else pf::mds<3, -1>(s);
-#pragma unroll
-    for (int i = 0; i < 12; i++) sa[i] = sb[i];
-  }
-#pragma unroll
-  for (int i = 0; i < 12; i++) wput(v, sa[i], s[i], ok);
   return ok;
 }
 
@@ -310,51 +231,6 @@ __device__ __noinline__ bool poseidon_coop(uint64_t *v, const uint32_t *__restri
   return ok;
 }
 
-// the first form (ps:: plain rounds, a lookup per write), QP_WIT_POSEIDON=0
-__device__ __noinline__ bool poseidon_witness_plain(const DevGenD &g, uint64_t *v, const uint32_t *wslot, uint32_t W) {
-  const uint32_t *ws = wslot + (uint64_t)g.row * W;
-  bool in_ok = true;
-  uint64_t s[12];
-  for (int i = 0; i < 12; i++) s[i] = rd(v, ws[i], in_ok);
-  const uint64_t swap = rd(v, ws[24], in_ok);
-  if (!in_ok) return false;
-  bool ok = true;
-  for (int i = 0; i < 4; i++) ok &= wset(v, ws[25 + i], gl::mul(swap, gl::sub(s[i + 4], s[i])));
-  if (swap == 1)
-    for (int i = 0; i < 4; i++) {
-      const uint64_t t = s[i];
-      s[i] = s[i + 4];
-      s[i + 4] = t;
-    }
-  int rc = 0;
-  for (int r = 0; r < 4; r++, rc++) {
-    for (int i = 0; i < 12; i++) s[i] = gl::add(s[i], ps::rc(rc * 12 + i));
-    if (r)
-      for (int i = 0; i < 12; i++) ok &= wset(v, ws[29 + (r - 1) * 12 + i], s[i]);
-    for (int i = 0; i < 12; i++) s[i] = ps::sbox(s[i]);
-    ps::mds(s);
-  }
-  for (int r = 0; r < 22; r++, rc++) {
-    for (int i = 0; i < 12; i++) s[i] = gl::add(s[i], ps::rc(rc * 12 + i));
-    ok &= wset(v, ws[65 + r], s[0]);
-    s[0] = ps::sbox(s[0]);
-    ps::mds(s);
-  }
-  for (int r = 0; r < 4; r++, rc++) {
-    for (int i = 0; i < 12; i++) s[i] = gl::add(s[i], ps::rc(rc * 12 + i));
-    for (int i = 0; i < 12; i++) ok &= wset(v, ws[87 + r * 12 + i], s[i]);
-    for (int i = 0; i < 12; i++) s[i] = ps::sbox(s[i]);
-    ps::mds(s);
-  }
-  for (int i = 0; i < 12; i++) ok &= wset(v, ws[12 + i], s[i]);
-  return ok;
-}
-
-// measured (tools/gpu_session.sh wit_ab, 256-leaf subtree, profiles/r04_wit_ab.log):
-// rolled 0.566 s, unrolled 0.607 s, plain 0.668 s
-#ifndef QP_WIT_POSEIDON
-#define QP_WIT_POSEIDON 2
-#endif
 
 __device__ bool run_gen(const DevGenD &g, uint64_t *__restrict__ v, const uint32_t *__restrict__ wslot, uint32_t W, uint32_t limbs,
                         uint32_t zslot, uint32_t num_consts) {
@@ -522,9 +398,7 @@ __device__ bool run_gen(const DevGenD &g, uint64_t *__restrict__ v, const uint32
     }
     case WG_POSEIDON:
       // PoseidonGenerator (gates/poseidon.rs), wire layout SURVEY.md A.5
-      if constexpr (QP_WIT_POSEIDON == 2) return poseidon_witness_rolled(v, wslot + (uint64_t)g.row * W);
-      else if constexpr (QP_WIT_POSEIDON == 1) return poseidon_witness(v, wslot + (uint64_t)g.row * W);
-      else return poseidon_witness_plain(g, v, wslot, W);
+      return poseidon_witness_rolled(v, wslot + (uint64_t)g.row * W);
     default:
       return false;
   }

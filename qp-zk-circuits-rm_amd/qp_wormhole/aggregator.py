@@ -82,13 +82,9 @@ class _LevelProver:
         self.max_batch = max_batch
         if not nprov:
             nprov = _agg_provers() if max_batch > 1 else 1
-        # QP_AGG_PRIORITY=1: the level provers' streams at the greatest priority,
-        # so their latency-bound launches dispatch ahead of concurrent leaf kernels
-        high = os.environ.get("QP_AGG_PRIORITY", "0") not in ("", "0")
+        # (a high-priority stream for the level provers changed nothing next to
+        # concurrent leaf provers: profiles/r05_configs3_pipelined_ab.log)
         ctxs = [Context(device) for _ in range(nprov)]
-        if high:
-            for c in ctxs:
-                c.set_priority(True)
         self.provers = [Prover(c, self.circuit, max_batch=max_batch) for c in ctxs]
         # the provers split the process's host budget (qp_prover_set_host_threads:
         # each would otherwise take min(hardware threads, 16))

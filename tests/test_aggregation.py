@@ -103,7 +103,7 @@ def test_host_chains_cut_the_device_schedule(ref, agg_circuit, monkeypatch):
     over inputs alone at least 64 permutations deep -- here the inner proofs'
     transcript sponges -- and the constants they read run on the host, the
     rest of the schedule on the device, 149 dependency levels down to 55;
-    QPGPU_HOST_CHAIN=0 keeps every generator on the device.  The leaf circuits
+    QPGPU_PATHS=host_chain=0 keeps every generator on the device.  The leaf circuits
     have no such chain.  (Device == host-witness bytes either way:
     test_gpu_aggregation.)"""
     import qp_wormhole
@@ -111,12 +111,12 @@ def test_host_chains_cut_the_device_schedule(ref, agg_circuit, monkeypatch):
     assert set(g) <= {"poseidon", "constant"} and g["poseidon"] >= 2 * 64
     assert chains == 2  # the two inner proofs' transcripts
     assert agg_circuit.witness_levels == 55
-    monkeypatch.setenv("QPGPU_HOST_CHAIN", "0")
+    monkeypatch.setenv("QPGPU_PATHS", "host_chain=0")
     c0 = qp_wormhole.Circuit.aggregation(ref[0], 2)
     g0, n0, ch0 = c0.host_chains()
     assert g0 == {} and ch0 == 0 and c0.witness_levels == 149 and n0 < nslots
     assert c0.num_generators == agg_circuit.num_generators
-    monkeypatch.delenv("QPGPU_HOST_CHAIN")
+    monkeypatch.delenv("QPGPU_PATHS")
     for circ in (qp_wormhole.Circuit.wormhole(False), qp_wormhole.Circuit.voting()):
         assert circ.host_chains()[0] == {}
 

@@ -217,16 +217,16 @@ def test_device_witness_equals_host_witness_levels_1_and_2(reference_leaves):
 
 def test_host_chains_off_gives_the_same_proofs(reference_leaves, monkeypatch):
     """The device witness with the input-only Poseidon chains on the host
-    (default) and with every generator on the device (QPGPU_HOST_CHAIN=0, a
+    (default) and with every generator on the device (QPGPU_PATHS=host_chain=0, a
     circuit built under it: 149 dependency levels instead of 55) prove the
     same bytes, which verify."""
     import qp_wormhole
     cb, vo, leaves = reference_leaves
     chunks = [leaves, leaves[::-1]]
     c1 = qp_wormhole.Circuit.aggregation(cb, 2)
-    monkeypatch.setenv("QPGPU_HOST_CHAIN", "0")
+    monkeypatch.setenv("QPGPU_PATHS", "host_chain=0")
     c0 = qp_wormhole.Circuit.aggregation(cb, 2)
-    monkeypatch.delenv("QPGPU_HOST_CHAIN")
+    monkeypatch.delenv("QPGPU_PATHS")
     assert c1.host_chains()[0] and not c0.host_chains()[0] and c0.witness_levels > c1.witness_levels
     out = []
     for c in (c1, c0):
@@ -257,12 +257,10 @@ def test_device_witness_zk_aggregation(reference_leaves):
     p.free()
 
 
-@pytest.mark.parametrize("env", [{"QPGPU_WIT_MODE": "wg"}, {"QPGPU_WIT_MODE": "levels"}, {"QPGPU_MERKLE_COOP": "0"},
-                                 {"QPGPU_QPREFIX": "0"}, {"QPGPU_LEAF_T": "0"}, {"QPGPU_MERKLE_ROW": "0"},
-                                 {"QPGPU_FRI_ROW": "0"}, {"QPGPU_OPEN_SLICES": "1"}, {"QPGPU_LDE_FEW": "0"},
-                                 {"QPGPU_WIT_ROW": "0"}, {"QPGPU_WIT_ROW": "0", "QPGPU_WIT_MODE": "wg"},
-                                 {"QPGPU_QREST": "1"}, {"QPGPU_QREST": "2"}, {"QPGPU_POW_WAVE": "1"}])
-def test_latency_paths_prove_the_same_bytes(reference_leaves, monkeypatch, env):
+@pytest.mark.parametrize("paths", ["wit_mode=0", "wit_mode=1", "merkle_coop=0", "qprefix=0", "leaf_t=0",
+                                   "merkle_row=0", "fri_row=0", "open_slices=1", "lde_few=0", "wit_row=0",
+                                   "wit_row=0,wit_mode=0"])
+def test_latency_paths_prove_the_same_bytes(reference_leaves, monkeypatch, paths):
     """The small-batch paths (device witness one launch per dependency level or
     one workgroup per proof, cooperative Merkle levels in the row or wave form,
     the prefix quotient kernel, the compile-time leaf hash, row-form FRI
@@ -273,14 +271,13 @@ def test_latency_paths_prove_the_same_bytes(reference_leaves, monkeypatch, env):
     circ = qp_wormhole.Circuit.aggregation(cb, 2)
     chunks = [leaves, leaves[::-1], [leaves[1], leaves[1]]]
     out = []
-    for e in ({}, env):
-        for k, v in e.items():
-            monkeypatch.setenv(k, v)
+    for hook in (None, paths):  # QPGPU_PATHS (csrc/paths.h): force the alternative path
+        if hook:
+            monkeypatch.setenv("QPGPU_PATHS", hook)
         p = qp_wormhole.Prover(qp_wormhole.Context(0), circ, max_batch=3)
         out.append((p.prove_aggregation(vo, chunks[:1]), p.prove_aggregation(vo, chunks)))
         p.free()
-        for k in e:
-            monkeypatch.delenv(k)
+        monkeypatch.delenv("QPGPU_PATHS", raising=False)
     assert out[0] == out[1]
 
 

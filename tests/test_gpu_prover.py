@@ -117,22 +117,22 @@ def test_wormhole_prover_api():
         qp_wormhole.WormholeProver().prove()
 
 
-def test_fused_quotient_kernel_bit_exact(env, monkeypatch):
-    """The opt-in k_quotient_fused (QPGPU_QUOTIENT=fused, read when a prover
-    is created) sweeps the routed wires out of order from LDS slots while the
-    Poseidon gate reads them; its proofs equal the default kernel's."""
+def test_per_gate_quotient_launches_bit_exact(env, monkeypatch):
+    """The per-gate quotient launches (k_quotient_prefix + k_quotient_part, the
+    aggregation circuits' path; path hook quotient_parts=1 forces them) on the
+    leaf circuit: the same proofs as the single-read kernel, for a satisfied
+    witness and one with a corrupted routed wire (nonzero gate and permutation
+    terms everywhere)."""
     import qp_wormhole
     ctx, circ, prover = env
     w = circ.commit(WI.test_inputs())
-    # a satisfied witness and one with a corrupted routed wire (nonzero
-    # gate and permutation terms everywhere)
     wires = np.stack([w.wires(), w.wires()])
     wires[1, 41, 5] ^= 1
     pis = np.stack([w.public_inputs(), w.public_inputs()])
     ref = prover.prove_wires(wires, pis)
-    monkeypatch.setenv("QPGPU_QUOTIENT", "fused")
-    fused = qp_wormhole.Prover(ctx, circ, max_batch=4)
+    monkeypatch.setenv("QPGPU_PATHS", "quotient_parts=1")
+    parts = qp_wormhole.Prover(ctx, circ, max_batch=4)
     try:
-        assert fused.prove_wires(wires, pis) == ref
+        assert parts.prove_wires(wires, pis) == ref
     finally:
-        fused.free()
+        parts.free()

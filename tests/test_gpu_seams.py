@@ -71,9 +71,9 @@ def test_quotient_matches_oracle(ctx, circuit):
 
 @pytest.mark.gpu
 def test_quotient_generic_kernel_matches_oracle(ctx, circuit, monkeypatch):
-    """The any-gate-list kernel (QPGPU_QUOTIENT=generic forces it) on the Wormhole circuit."""
+    """The any-gate-list kernels (path hook quotient_parts=1 forces them) on the Wormhole circuit."""
     import qp_wormhole
-    monkeypatch.setenv("QPGPU_QUOTIENT", "generic")
+    monkeypatch.setenv("QPGPU_PATHS", "quotient_parts=1")
     rng = np.random.default_rng(43)
     g = qp_wormhole.gate_desc(circuit)
     n = circuit.n
