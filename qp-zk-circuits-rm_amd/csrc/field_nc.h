@@ -75,4 +75,35 @@ __device__ __forceinline__ uint64_t mul(uint64_t a, uint64_t b) { return pf::mul
 
 __device__ __forceinline__ uint64_t sbox(uint64_t x) { return pf::sbox(x); }
 
+// Lazily reduced sum of products (the quotient's alpha-weighted constraint
+// sums): sum_i a_i b_i held as lo + 2^64 hi + 2^128 top, top counting the
+// carries out of 2^128 (fewer than 2^32 terms), reduced once by value().  One
+// product-accumulate is 4 mads + 1 cndmask + 3 addc, against a reduced
+// product and a reduced add (13 + 6) per term.
+struct Acc3 {
+  uint64_t lo = 0, hi = 0;
+  uint32_t top = 0;
+  __device__ __forceinline__ void mac(uint64_t a, uint64_t b) {
+    const uint32_t a0 = pf::lo32(a), a1 = pf::hi32(a), b0 = pf::lo32(b), b1 = pf::hi32(b);
+    // L = a0 b0 + lo, carry-out cl worth 2^64; the rest of the product is then
+    // the exact high part of a b + lo - cl 2^64 < 2^128, so W < 2^64
+    uint64_t L, cl, U, cu, c;
+    asm("v_mad_u64_u32 %0, %1, %2, %3, %4" : "=v"(L), "=s"(cl) : "v"(a0), "v"(b0), "v"(lo));
+    const uint64_t T = (uint64_t)a0 * b1 + pf::hi32(L);
+    asm("v_mad_u64_u32 %0, %1, %2, %3, %4" : "=v"(U), "=s"(cu) : "v"(a1), "v"(b0), "v"(T));
+    uint32_t ce;
+    asm(QP_CWAIT "v_cndmask_b32_e64 %0, 0, 1, %1" : "=v"(ce) : "s"(cu));
+    const uint64_t W = (uint64_t)a1 * b1 + (((uint64_t)ce << 32) | pf::hi32(U));
+    lo = ((uint64_t)pf::lo32(U) << 32) | pf::lo32(L);
+    // hi += W + cl; top += the carry out
+    uint32_t h0 = pf::lo32(hi), h1 = pf::hi32(hi);
+    asm("v_addc_co_u32_e64 %0, %1, %2, %3, %4" : "=v"(h0), "=s"(c) : "v"(h0), "v"(pf::lo32(W)), "s"(cl));
+    asm(QP_CWAIT "v_addc_co_u32_e64 %0, %1, %2, %3, %1" : "=v"(h1), "+s"(c) : "v"(h1), "v"(pf::hi32(W)));
+    asm(QP_CWAIT "v_addc_co_u32_e64 %0, %1, %2, 0, %1" : "=v"(top), "+s"(c) : "v"(top));
+    hi = ((uint64_t)h1 << 32) | h0;
+  }
+  // 2^128 = 2^96 2^32 = -2^32 (mod p)
+  __device__ __forceinline__ uint64_t value() const { return sub(reduce(lo, hi), (uint64_t)top << 32); }
+};
+
 }  // namespace gfn

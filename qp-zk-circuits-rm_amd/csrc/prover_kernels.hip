@@ -234,18 +234,20 @@ __device__ __forceinline__ void mul2(uint64_t a0, uint64_t b0, uint64_t a1, uint
   r1 = gfn::mul(a1, b1);
 }
 
+// sum_i t_i alpha_c^i for both challenges, lazily reduced (gfn::Acc3: one
+// reduction per sum instead of per term)
 struct TermAcc {
   const uint64_t *__restrict__ p0;  // alpha_0^i
   const uint64_t *__restrict__ p1;  // alpha_1^i
-  uint64_t s0, s1;
+  gfn::Acc3 s0, s1;
   uint32_t i;
   __device__ __forceinline__ void emit(uint64_t t) {
-    uint64_t m0, m1;
-    mul2(t, p0[i], t, p1[i], m0, m1);
-    s0 = gfn::add(s0, m0);
-    s1 = gfn::add(s1, m1);
+    s0.mac(t, p0[i]);
+    s1.mac(t, p1[i]);
     i++;
   }
+  __device__ __forceinline__ uint64_t sum0() const { return s0.value(); }
+  __device__ __forceinline__ uint64_t sum1() const { return s1.value(); }
 };
 
 // Poseidon gate constraints (plonky2 PoseidonGate): the MDS of
@@ -578,6 +580,12 @@ __device__ __forceinline__ void emit_at(const uint64_t *__restrict__ p0, const u
   s1 = gfn::add(s1, m1);
 }
 
+__device__ __forceinline__ void emit_at(const uint64_t *__restrict__ p0, const uint64_t *__restrict__ p1, uint32_t i,
+                                        uint64_t t, gfn::Acc3 &s0, gfn::Acc3 &s1) {
+  s0.mac(t, p0[i]);
+  s1.mac(t, p1[i]);
+}
+
 // x * 2^e, 0 <= e < 64, x in [0, 2^64) -> [0, 2^64)
 __device__ __forceinline__ uint64_t mul_pow2_rt(uint64_t x, uint32_t e) {
   return e ? gfn::reduce(x << e, x >> (64 - e)) : x;
@@ -622,20 +630,22 @@ k_quotient_1r(QuotientArgs a) {
   const uint32_t n_pi = g_pi >= 0 ? 4 : 0;
   const uint32_t L = g_bs >= 0 ? a.g.param[g_bs] : 0;
   const uint32_t n_ar = g_ar >= 0 ? a.g.param[g_ar] : 0;
-  // vanishing terms 0..pre-1 go straight into the totals
-  uint64_t acc0 = 0, acc1 = 0;
+  // vanishing terms 0..pre-1 go straight into the totals (lazily reduced sums:
+  // gfn::Acc3, one reduction per sum)
+  gfn::Acc3 pz0, pz1;
   const uint64_t x = a.xtab[t], l0 = a.l0tab[t];
   uint64_t z[2], prev[2];
   for (uint32_t c = 0; c < 2; c++) {
     z[c] = zl[(uint64_t)c * N + t];
     prev[c] = z[c];
-    emit_at(p0, p1, c, gfn::mul(l0, gfn::sub(z[c], 1)), acc0, acc1);
+    emit_at(p0, p1, c, gfn::mul(l0, gfn::sub(z[c], 1)), pz0, pz1);
   }
   const uint64_t beta0 = ch[CH_BETA], beta1 = ch[CH_BETA + 1], gamma0 = ch[CH_GAMMA], gamma1 = ch[CH_GAMMA + 1];
   uint64_t bkx0 = gfn::mul(beta0, x), bkx1 = gfn::mul(beta1, x);
   uint64_t num0 = 1, den0 = 1, num1 = 1, den1 = 1;
   // per-gate alpha sums (multiplied by the gate's filter at the end)
-  uint64_t sc0 = 0, sc1 = 0, sp0 = 0, sp1 = 0, sb0 = 0, sb1 = 0, sa0 = 0, sa1 = 0;
+  uint64_t sc0 = 0, sc1 = 0, sp0 = 0, sp1 = 0;
+  gfn::Acc3 sb0, sb1, sa0, sa1;  // the BaseSum and Arithmetic gates' terms
   uint64_t bs_acc = 0, w0 = 0, wa0 = 0, wa1 = 0, wa2 = 0;
   // the Poseidon gate reads wires 0..23 again after the sweep: the first
   // QSTASH of them are kept in LDS (per lane, conflict-free [j][lane])
@@ -684,7 +694,7 @@ k_quotient_1r(QuotientArgs a) {
       for (uint32_t c = 0; c < 2; c++) {
         const uint64_t nx = k == nchunks - 1 ? zl[(uint64_t)c * N + tn] : zl[((uint64_t)2 + c * npp + k) * N + t];
         const uint64_t num = c ? num1 : num0, den = c ? den1 : den0;
-        emit_at(p0, p1, 2 + c * nchunks + k, gfn::sub(gfn::mul(prev[c], num), gfn::mul(nx, den)), acc0, acc1);
+        emit_at(p0, p1, 2 + c * nchunks + k, gfn::sub(gfn::mul(prev[c], num), gfn::mul(nx, den)), pz0, pz1);
         prev[c] = nx;
       }
       num0 = den0 = num1 = den1 = 1;
@@ -696,8 +706,16 @@ k_quotient_1r(QuotientArgs a) {
         w0 = w;
       } else if (jj <= L) {
         bs_acc = gfn::add(bs_acc, mul_pow2_rt(w, jj - 1));
-        emit_at(p0, p1, pre + jj, gfn::mul(w, gfn::sub(w, 1)), sb0, sb1);
-        if (jj == L) emit_at(p0, p1, pre, gfn::sub(bs_acc, w0), sb0, sb1);
+        {
+          const uint64_t tb = gfn::mul(w, gfn::sub(w, 1));
+          sb0.mac(tb, p0[pre + jj]);
+          sb1.mac(tb, p1[pre + jj]);
+        }
+        if (jj == L) {
+          const uint64_t tb = gfn::sub(bs_acc, w0);
+          sb0.mac(tb, p0[pre]);
+          sb1.mac(tb, p1[pre]);
+        }
       }
     }
     if (jj < 4 * n_ar) {
@@ -712,6 +730,7 @@ k_quotient_1r(QuotientArgs a) {
       }
     }
   }
+  uint64_t acc0 = pz0.value(), acc1 = pz1.value();
   // selector filters: prod_{j in group, j != gate}(j - s) * (UNUSED - s)
   auto filter = [&](int gi) -> uint64_t {
     const uint32_t si = a.g.sel_index[gi];
@@ -734,13 +753,13 @@ k_quotient_1r(QuotientArgs a) {
   }
   if (g_bs >= 0) {
     const uint64_t f = filter(g_bs);
-    acc0 = gfn::add(acc0, gfn::mul(f, sb0));
-    acc1 = gfn::add(acc1, gfn::mul(f, sb1));
+    acc0 = gfn::add(acc0, gfn::mul(f, sb0.value()));
+    acc1 = gfn::add(acc1, gfn::mul(f, sb1.value()));
   }
   if (g_ar >= 0) {
     const uint64_t f = filter(g_ar);
-    acc0 = gfn::add(acc0, gfn::mul(f, sa0));
-    acc1 = gfn::add(acc1, gfn::mul(f, sa1));
+    acc0 = gfn::add(acc0, gfn::mul(f, sa0.value()));
+    acc1 = gfn::add(acc1, gfn::mul(f, sa1.value()));
   }
   if (g_ra >= 0) {
     // RandomAccessGate (the aggregation circuits' recursive verifier): per copy
@@ -787,13 +806,12 @@ k_quotient_1r(QuotientArgs a) {
     TermAcc A;
     A.p0 = p0;
     A.p1 = p1;
-    A.s0 = A.s1 = 0;
     A.i = pre;
     WireRead rd{wl, N, stash, nst};
     poseidon_gate_rd(rd, A);
     const uint64_t f = filter(g_pos);
-    acc0 = gfn::add(acc0, gfn::mul(f, A.s0));
-    acc1 = gfn::add(acc1, gfn::mul(f, A.s1));
+    acc0 = gfn::add(acc0, gfn::mul(f, A.sum0()));
+    acc1 = gfn::add(acc1, gfn::mul(f, A.sum1()));
   }
   const uint64_t zh_inv = a.zh_inv[j & ((1u << a.rate_bits) - 1)];
   q[t] = gfn::canon(gfn::mul(acc0, zh_inv));
@@ -828,7 +846,6 @@ __global__ void __launch_bounds__(256) k_quotient_part(QuotientArgs a, uint32_t 
   TermAcc A;
   A.p0 = a.apow + (uint64_t)b * 2 * APOW_STRIDE;
   A.p1 = A.p0 + APOW_STRIDE;
-  A.s0 = A.s1 = 0;
   A.i = 0;
   const uint32_t R = a.R, qdf = a.qdf, nchunks = (R + qdf - 1) / qdf, npp = nchunks - 1;
   uint64_t acc0, acc1;
@@ -855,8 +872,8 @@ __global__ void __launch_bounds__(256) k_quotient_part(QuotientArgs a, uint32_t 
         A.emit(gfn::sub(gfn::mul(prev, num), gfn::mul(next, den)));
       }
     }
-    acc0 = A.s0;
-    acc1 = A.s1;
+    acc0 = A.sum0();
+    acc1 = A.sum1();
   } else {
     const uint32_t kind = a.g.kind[gi];
     const uint32_t si = a.g.sel_index[gi], nsel = a.g.nsel;
@@ -915,8 +932,8 @@ __global__ void __launch_bounds__(256) k_quotient_part(QuotientArgs a, uint32_t 
           break;
       }
     }
-    acc0 = gfn::add(q[t], gfn::mul(f, A.s0));
-    acc1 = gfn::add(q[N + t], gfn::mul(f, A.s1));
+    acc0 = gfn::add(q[t], gfn::mul(f, A.sum0()));
+    acc1 = gfn::add(q[N + t], gfn::mul(f, A.sum1()));
   }
   if (last) {
     const uint32_t j = gl::rev_bits(t, logN);
@@ -974,12 +991,10 @@ k_quotient_prefix(QuotientArgs a, uint32_t gmask, uint32_t last) {
   // one accumulator pair: a gate's terms enter multiplied by its selector
   // filter, prod over the gate's group of (j - s), j != gate, times (UNUSED -
   // s) with several groups (per-gate sums would hold 12 more registers)
-  uint64_t acc0 = 0, acc1 = 0;
+  gfn::Acc3 lz0, lz1;  // lazily reduced (gfn::Acc3)
   auto emit = [&](uint32_t i, uint64_t term) {
-    uint64_t m0, m1;
-    mul2(term, p0[i], term, p1[i], m0, m1);
-    acc0 = gfn::add(acc0, m0);
-    acc1 = gfn::add(acc1, m1);
+    lz0.mac(term, p0[i]);
+    lz1.mac(term, p1[i]);
   };
   auto filter = [&](int gi) -> uint64_t {
     if (gi < 0) return 0;
@@ -1095,6 +1110,7 @@ k_quotient_prefix(QuotientArgs a, uint32_t gmask, uint32_t last) {
       bs_pw = gfn::mul(bs_pw, 1ull << (base == 0 ? QP_WIN - 1 : QP_WIN));  // 2^(first limb of the next window)
     }
   }
+  uint64_t acc0 = lz0.value(), acc1 = lz1.value();
   if (gi_bs >= 0) {
     uint64_t m0, m1, d = gfn::sub(bs_acc, wire0);
     mul2(d, p0[gb], d, p1[gb], m0, m1);

@@ -62,6 +62,11 @@ for s in "$@"; do
            echo "=== gpus2 rc=$?" | tee -a gpurun_out/session.log; tail -5 gpurun_out/gpus2.log ;;
     shapes) step shapes 900 python -u bench.py --steps 2 --warmup 1 --cpu-sample 0 --configs3 0 --agg-leaves 0 ;;
     benchfull) step benchfull 900 python -u bench.py --steps 20 --warmup 5 ;;
+    qlazy) step pytest_q 900 python -u -m pytest tests/test_gpu_seams.py tests/test_gpu_reference_proof.py tests/test_gpu_prover.py tests/test_gpu_aggregation.py tests/test_gpu_seam_prove.py -x -q --timeout 400 --timeout-method thread &&
+           step bench5 600 python -u bench.py --steps 5 --warmup 1 --cpu-sample 0 --ref-shapes 0 &&
+           step agg_subtree 300 python -u tools/agg_subtree.py 256 2 &&
+           step pmc_sqq 300 rocprofv3 --pmc SQ_WAVES SQ_INSTS_VALU SQ_ACTIVE_INST_VALU SQ_WAVE_CYCLES SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_BUSY_CYCLES SQ_WAIT_ANY --kernel-include-regex "k_quotient|k_lde_cosets" --output-format csv -d gpurun_out/pmc_sqq -o run -- python3 bench.py --steps 1 --warmup 1 --cpu-sample 0 --provers 1 --batch 128 --configs3 0 --agg-leaves 0 --ref-shapes 0 &&
+           step pmc_sqq_sum 120 python3 tools/pmc_sq_summary.py gpurun_out/pmc_sqq gpurun_out/pmc_sqq.json && rm -rf gpurun_out/pmc_sqq ;;
     bench5) step bench5 600 python -u bench.py --steps 5 --warmup 1 --cpu-sample 0 ;;
     agg_ab) step agg_dev2 300 python -u tools/agg_subtree.py 256 2 &&
             step agg_dev1 300 env QP_AGG_PROVERS=1 python -u tools/agg_subtree.py 256 2 &&
