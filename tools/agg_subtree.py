@@ -3,8 +3,7 @@ tool): `leaves` leaf proofs (the reference's own two, alternating) -> one root
 through aggregate_to_tree (branching 2), one untimed pass that builds and
 caches the level circuits, then `reps` timed passes with per-level seconds and
 the device stage times of the level provers.  Variants come from the
-environment (QP_AGG_PROVERS, QP_AGG_WITNESS, QPGPU_QUOTIENT, QPGPU_LDE_MODE,
-QPGPU_HOST_CHAIN).
+environment (QP_AGG_PROVERS, QP_AGG_SPLIT, QP_AGG_WITNESS, QPGPU_PATHS).
 python tools/agg_subtree.py [leaves] [reps]"""
 import json
 import os
@@ -59,6 +58,13 @@ def main():
             return None
     th0 = throttle()
     res = []
+    # trace markers (bench.py's): a spin kernel just outside each end of the
+    # timed passes, so tools/kernel_summary.py and tools/agg_trace.py cut a
+    # rocprofv3 kernel trace to them
+    import torch
+    torch.cuda.synchronize()
+    torch.cuda._sleep(1000)
+    torch.cuda.synchronize()
     for _ in range(reps):
         levels.clear()
         t = time.perf_counter()
@@ -67,6 +73,9 @@ def main():
         # this job OMP_NUM_THREADS cores)
         res.append({"seconds": time.perf_counter() - t,
                     "levels": [(n, round(s * 1e3, 1), round(c * 1e3, 1)) for n, s, c in levels]})
+    torch.cuda.synchronize()
+    torch.cuda._sleep(1000)
+    torch.cuda.synchronize()
     # per level circuit (insertion order = level order): degree, proofs per
     # level prover batch and its device stage times per run
     per_level = []
@@ -83,8 +92,8 @@ def main():
             for k, v in p.stage_times().items():
                 stages[k] = stages.get(k, 0.0) + v / reps
     rvd, rp = root.circuit_data.verifier_data(), root.proof.to_bytes()
-    env = {k: os.environ.get(k) for k in ("QP_AGG_PROVERS", "QP_AGG_WITNESS", "QPGPU_QUOTIENT", "QPGPU_LDE_MODE",
-                                        "QPGPU_HOST_CHAIN", "QP_AGG_THREADS", "OMP_NUM_THREADS")}
+    env = {k: os.environ.get(k) for k in ("QP_AGG_PROVERS", "QP_AGG_SPLIT", "QP_AGG_WITNESS", "QPGPU_PATHS",
+                                        "QP_AGG_THREADS", "OMP_NUM_THREADS")}
     th1 = throttle()
     cg = None
     if th0 and th1:

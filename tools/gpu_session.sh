@@ -67,6 +67,10 @@ for s in "$@"; do
            step agg_subtree 300 python -u tools/agg_subtree.py 256 2 &&
            step pmc_sqq 300 rocprofv3 --pmc SQ_WAVES SQ_INSTS_VALU SQ_ACTIVE_INST_VALU SQ_WAVE_CYCLES SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_BUSY_CYCLES SQ_WAIT_ANY --kernel-include-regex "k_quotient|k_lde_cosets" --output-format csv -d gpurun_out/pmc_sqq -o run -- python3 bench.py --steps 1 --warmup 1 --cpu-sample 0 --provers 1 --batch 128 --configs3 0 --agg-leaves 0 --ref-shapes 0 &&
            step pmc_sqq_sum 120 python3 tools/pmc_sq_summary.py gpurun_out/pmc_sqq gpurun_out/pmc_sqq.json && rm -rf gpurun_out/pmc_sqq ;;
+    aggprofd) step prof_aggd 300 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/prof_aggd -o run -- python3 tools/agg_subtree.py 256 1 &&
+              step aggd_sum 120 python3 tools/agg_trace.py gpurun_out/prof_aggd/run_kernel_trace.csv gpurun_out/agg_trace_default.json 5 &&
+              step aggd_ksum 120 python3 tools/kernel_summary.py gpurun_out/prof_aggd/run_kernel_trace.csv gpurun_out/agg_kernel_summary_default.json "agg_subtree 256, default (4 concurrent sub-trees), timed pass" &&
+              cp gpurun_out/prof_aggd/run_kernel_stats.csv gpurun_out/agg_default_kernel_stats.csv && rm -rf gpurun_out/prof_aggd ;;
     bench5) step bench5 600 python -u bench.py --steps 5 --warmup 1 --cpu-sample 0 ;;
     agg_ab) step agg_dev2 300 python -u tools/agg_subtree.py 256 2 &&
             step agg_dev1 300 env QP_AGG_PROVERS=1 python -u tools/agg_subtree.py 256 2 &&
