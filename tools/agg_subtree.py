@@ -62,6 +62,7 @@ def main():
     # timed passes, so tools/kernel_summary.py and tools/agg_trace.py cut a
     # rocprofv3 kernel trace to them
     import torch
+    torch.zeros(1, device="cuda").add_(1)  # torch's own context and stream, as in bench.py
     torch.cuda.synchronize()
     torch.cuda._sleep(1000)
     torch.cuda.synchronize()
