@@ -29,13 +29,13 @@ def main():
     lo, hi = (marks[0][1], marks[-1][0]) if len(marks) >= 2 else (rows[0][0], max(r[1] for r in rows))
     sel = [r for r in rows if r[0] >= lo and r[1] <= hi and r[2] != MARKER]
     window = (hi - lo) / 1e6
-    busy = union_ms([(a, b) for a, b, _, _ in sel]) / window
+    busy = union_ms([(a, b) for a, b, _, _ in sel]) / (hi - lo)  # union_ms: same unit as its input
     nsl = int(window / sl) + 1
     slices = []
     for k in range(nsl):
         a0, b0 = lo + k * sl * 1e6, lo + (k + 1) * sl * 1e6
         iv = [(max(a, a0), min(b, b0)) for a, b, _, _ in sel if b > a0 and a < b0]
-        slices.append(round(union_ms(iv) / min(sl, (hi - a0) / 1e6), 3) if iv else 0.0)
+        slices.append(round(union_ms(iv) / min(sl * 1e6, hi - a0), 3) if iv else 0.0)
     per = defaultdict(lambda: [0.0, 0])
     for a, b, n, g in sel:
         per[(n, g)][0] += (b - a) / 1e6

@@ -71,6 +71,15 @@ for s in "$@"; do
               step aggd_sum 120 python3 tools/agg_trace.py gpurun_out/prof_aggd/run_kernel_trace.csv gpurun_out/agg_trace_default.json 5 &&
               step aggd_ksum 120 python3 tools/kernel_summary.py gpurun_out/prof_aggd/run_kernel_trace.csv gpurun_out/agg_kernel_summary_default.json "agg_subtree 256, default (4 concurrent sub-trees), timed pass" &&
               cp gpurun_out/prof_aggd/run_kernel_stats.csv gpurun_out/agg_default_kernel_stats.csv && rm -rf gpurun_out/prof_aggd ;;
+    ldeocc) for r in 1 2; do
+             step prof_lde_def_$r 300 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/prof_lde_def_$r -o run -- python3 tools/kbench.py 86 3 &&
+             step prof_lde_lds1_$r 300 env QPGPU_LIB=qp-zk-circuits-rm_amd/qp_wormhole/variants/libqpgpu_lds1.so rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/prof_lde_lds1_$r -o run -- python3 tools/kbench.py 86 3 || exit 1
+           done; for d in gpurun_out/prof_lde_*; do grep -h "k_lde_cosets\|k_intt\|Name" $d/run_kernel_stats.csv > $d.stats; rm -rf $d; done ;;
+    ldeocc_sq) for v in def lds1; do
+             if [ $v = def ]; then unset QPGPU_LIB; else export QPGPU_LIB=qp-zk-circuits-rm_amd/qp_wormhole/variants/libqpgpu_$v.so; fi
+             step pmc_lde_sq_$v 120 rocprofv3 --pmc SQ_WAVES SQ_INSTS_VALU SQ_ACTIVE_INST_VALU SQ_WAVE_CYCLES SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_BUSY_CYCLES SQ_WAIT_ANY --kernel-include-regex k_lde_cosets --output-format csv -d gpurun_out/pmc_lde_sq_$v -o run -- python3 tools/kbench.py 86 1 &&
+             step pmc_lde_sum_$v 60 python3 tools/pmc_sq_summary.py gpurun_out/pmc_lde_sq_$v gpurun_out/pmc_lde_sq_$v.json && rm -rf gpurun_out/pmc_lde_sq_$v || exit 1
+           done; unset QPGPU_LIB ;;
     bench5) step bench5 600 python -u bench.py --steps 5 --warmup 1 --cpu-sample 0 ;;
     agg_ab) step agg_dev2 300 python -u tools/agg_subtree.py 256 2 &&
             step agg_dev1 300 env QP_AGG_PROVERS=1 python -u tools/agg_subtree.py 256 2 &&
