@@ -132,6 +132,17 @@ struct qp_prover {
 
 namespace qpk {
 
+void perm_challenges(uint64_t *ch, const uint64_t *beta, const uint64_t *gamma, uint32_t nc, uint32_t R, uint32_t qdf) {
+  const uint32_t last = R % qdf ? R % qdf : qdf;
+  for (uint32_t c = 0; c < nc && c < 2; c++) {
+    const uint64_t bi = gl::inv(beta[c]);
+    ch[CH_BETA_INV + c] = bi;
+    ch[CH_GAMMA_B + c] = gl::mul(gamma[c], bi);
+    ch[CH_BETA_QDF + c] = gl::pow(beta[c], qdf);
+    ch[CH_BETA_LAST + c] = gl::pow(beta[c], last);
+  }
+}
+
 // proof-independent point tables of the quotient, leaf order t (point
 // x = g w_N^rev(t)): xtab[t] = x, l0tab[t] = L_0(x) = Z_H(x) / (n (x - 1))
 // (one batch inversion here instead of a field inversion per point per proof)
@@ -236,6 +247,10 @@ int setup(qp_prover *P) {
   P->pow_bits = cd.config.pow_bits;
   P->npis = cd.num_public_inputs;
   P->arity = cd.fri_arity_bits;
+  if (P->arity.size() > qpk::MAX_FRI_LAYERS) {
+    c->err = "more FRI layers than the challenge block holds";
+    return QP_ERR_ARG;
+  }
   uint32_t tot = 0;
   for (auto a : P->arity) tot += a;
   P->final_len = 1u << (P->log_n - tot);
@@ -581,6 +596,7 @@ int prove_batch(qp_prover *P, const uint64_t *d_wires, const uint64_t *const *wi
     uint64_t *ch = P->h_chal.data() + b * qpk::CHAL_STRIDE;
     for (uint32_t i = 0; i < nc; i++) ch[qpk::CH_BETA + i] = S.t.get();
     for (uint32_t i = 0; i < nc; i++) ch[qpk::CH_GAMMA + i] = S.t.get();
+    qpk::perm_challenges(ch, ch + qpk::CH_BETA, ch + qpk::CH_GAMMA, nc, P->R, P->qdf);
     for (int i = 0; i < 4; i++) ch[qpk::CH_PIH + i] = S.pih[i];
   });
   if ((rc = push_chal(P, nb))) return rc;

@@ -16,8 +16,15 @@ void pow_prestate(const uint64_t st12[12], uint32_t pos, uint64_t pre[24]);
 // per-proof challenge block (device, u64 words)
 enum : uint32_t {
   CH_BETA = 0, CH_GAMMA = 2, CH_ALPHA = 4, CH_PIH = 6, CH_ZETA = 10, CH_ZETA_NEXT = 12, CH_ZETA_INV = 14,
-  CH_ZETA_NEXT_INV = 16, CH_FRI_ALPHA = 18, CH_ALPHA_POW_NC = 20, CH_FRI_BETA = 22, CHAL_STRIDE = 40
+  CH_ZETA_NEXT_INV = 16, CH_FRI_ALPHA = 18, CH_ALPHA_POW_NC = 20, CH_FRI_BETA = 22,
+  // the permutation argument scaled by 1 / beta (k_quotient_1r): (w + gamma +
+  // beta s) = beta (w / beta + gamma / beta + s), the beta^len of a chunk's
+  // products applied once per chunk (len = qdf, or the last chunk's R mod qdf)
+  CH_BETA_INV = 32, CH_GAMMA_B = 34, CH_BETA_QDF = 36, CH_BETA_LAST = 38, CHAL_STRIDE = 40
 };
+constexpr uint32_t MAX_FRI_LAYERS = (CH_BETA_INV - CH_FRI_BETA) / 2;
+// the permutation-argument words of the challenge block for challenges beta, gamma
+void perm_challenges(uint64_t *ch, const uint64_t *beta, const uint64_t *gamma, uint32_t nc, uint32_t R, uint32_t qdf);
 constexpr uint32_t OPEN_STRIDE = 520;  // 257 ext openings per proof (+pad)
 constexpr uint32_t APOW_STRIDE = 256;  // alpha_c^i, i < #vanishing terms (per challenge)
 

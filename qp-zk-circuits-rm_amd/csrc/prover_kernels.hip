@@ -640,11 +640,16 @@ k_quotient_1r(QuotientArgs a) {
     prev[c] = z[c];
     emit_at(p0, p1, c, gfn::mul(l0, gfn::sub(z[c], 1)), pz0, pz1);
   }
-  const uint64_t beta0 = ch[CH_BETA], beta1 = ch[CH_BETA + 1], gamma0 = ch[CH_GAMMA], gamma1 = ch[CH_GAMMA + 1];
-  uint64_t bkx0 = gfn::mul(beta0, x), bkx1 = gfn::mul(beta1, x);
+  // permutation factors divided by beta_c: w / beta_c + gamma_c / beta_c + s
+  // (s = k_j x or sigma_j), the chunk's beta_c^len restored once per chunk
+  // (CH_BETA_INV..CH_BETA_LAST): the k_j x steps are shared by both challenges
+  // and the sigma values need no product (7 products per wire, not 8)
+  const uint64_t binv0 = ch[CH_BETA_INV], binv1 = ch[CH_BETA_INV + 1];
+  const uint64_t gamb0 = ch[CH_GAMMA_B], gamb1 = ch[CH_GAMMA_B + 1];
+  uint64_t kx = x;  // k_j x, k_j = g^j
   uint64_t num0 = 1, den0 = 1, num1 = 1, den1 = 1;
   // per-gate alpha sums (multiplied by the gate's filter at the end)
-  uint64_t sc0 = 0, sc1 = 0, sp0 = 0, sp1 = 0;
+  uint64_t sc0 = 0, sc1 = 0, sp0 = 0, sp1 = 0;  // 2 and 4 terms: reduced as they come
   gfn::Acc3 sb0, sb1, sa0, sa1;  // the BaseSum and Arithmetic gates' terms
   uint64_t bs_acc = 0, w0 = 0, wa0 = 0, wa1 = 0, wa2 = 0;
   // the Poseidon gate reads wires 0..23 again after the sweep: the first
@@ -680,21 +685,23 @@ k_quotient_1r(QuotientArgs a) {
       sg = cs[(uint64_t)(a.num_constants + jj) * N];
     }
     if (jj < nst) stash[jj * blockDim.x + threadIdx.x] = w;
-    // permutation argument, both challenges (k_j = g^j folded into bkx)
+    // permutation argument, both challenges
     {
-      uint64_t bs0, bs1;
-      mul2(beta0, sg, beta1, sg, bs0, bs1);
-      const uint64_t wg0 = gfn::add_c(w, gamma0), wg1 = gfn::add_c(w, gamma1);
-      mul2(num0, gfn::add(wg0, bkx0), den0, gfn::add(wg0, bs0), num0, den0);
-      mul2(num1, gfn::add(wg1, bkx1), den1, gfn::add(wg1, bs1), num1, den1);
-      mul2(bkx0, gl::GEN, bkx1, gl::GEN, bkx0, bkx1);
+      uint64_t wb0, wb1;
+      mul2(w, binv0, w, binv1, wb0, wb1);
+      const uint64_t wg0 = gfn::add_c(wb0, gamb0), wg1 = gfn::add_c(wb1, gamb1);
+      mul2(num0, gfn::add(wg0, kx), den0, gfn::add(wg0, sg), num0, den0);
+      mul2(num1, gfn::add(wg1, kx), den1, gfn::add(wg1, sg), num1, den1);
+      kx = gfn::mul(kx, gl::GEN);
     }
     if ((jj + 1) % qdf == 0 || jj + 1 == R) {
       const uint32_t k = jj / qdf;
+      const uint32_t bw = k == nchunks - 1 ? CH_BETA_LAST : CH_BETA_QDF;
       for (uint32_t c = 0; c < 2; c++) {
         const uint64_t nx = k == nchunks - 1 ? zl[(uint64_t)c * N + tn] : zl[((uint64_t)2 + c * npp + k) * N + t];
         const uint64_t num = c ? num1 : num0, den = c ? den1 : den0;
-        emit_at(p0, p1, 2 + c * nchunks + k, gfn::sub(gfn::mul(prev[c], num), gfn::mul(nx, den)), pz0, pz1);
+        const uint64_t d = gfn::sub(gfn::mul(prev[c], num), gfn::mul(nx, den));
+        emit_at(p0, p1, 2 + c * nchunks + k, gfn::mul(d, ch[bw + c]), pz0, pz1);
         prev[c] = nx;
       }
       num0 = den0 = num1 = den1 = 1;
@@ -1017,8 +1024,10 @@ k_quotient_prefix(QuotientArgs a, uint32_t gmask, uint32_t last) {
   const bool need_k0 = gi_c >= 0 || gi_ar >= 0 || gi_ae >= 0 || gi_me >= 0;
   const bool need_k1 = (gi_c >= 0 && n_c > 1) || gi_ar >= 0 || gi_ae >= 0;
   const uint64_t k0 = need_k0 ? gc[0] : 0, k1 = need_k1 ? gc[N] : 0;
-  const uint64_t beta0 = ch[CH_BETA], beta1 = ch[CH_BETA + 1], gam0 = ch[CH_GAMMA], gam1 = ch[CH_GAMMA + 1];
-  uint64_t bkx0 = gfn::mul(beta0, x), bkx1 = gfn::mul(beta1, x);
+  // permutation factors divided by beta_c, as k_quotient_1r (CH_BETA_INV..)
+  const uint64_t binv0 = ch[CH_BETA_INV], binv1 = ch[CH_BETA_INV + 1];
+  const uint64_t gam0 = ch[CH_GAMMA_B], gam1 = ch[CH_GAMMA_B + 1];
+  uint64_t kx = x;
   uint64_t bs_acc = 0, bs_pw = 1, wire0 = 0, bss0 = 0, bss1 = 0;
   for (uint32_t base = 0; base < R; base += QP_WIN) {
     const uint32_t nw = R - base < QP_WIN ? R - base : QP_WIN;
@@ -1044,20 +1053,21 @@ k_quotient_prefix(QuotientArgs a, uint32_t gmask, uint32_t last) {
       for (uint32_t i = 0; i < QDF; i++) {
         if (c + i >= nw) break;
         const uint64_t s = cs[(uint64_t)(a.num_constants + base + c + i) * N];
-        const uint64_t wg0 = gfn::add_c(w[c + i], gam0), wg1 = gfn::add_c(w[c + i], gam1);
-        num0 = gfn::mul(num0, gfn::add(wg0, bkx0));
-        num1 = gfn::mul(num1, gfn::add(wg1, bkx1));
-        den0 = gfn::mul(den0, gfn::add(wg0, gfn::mul(beta0, s)));
-        den1 = gfn::mul(den1, gfn::add(wg1, gfn::mul(beta1, s)));
-        bkx0 = gfn::mul(bkx0, gl::GEN);
-        bkx1 = gfn::mul(bkx1, gl::GEN);
+        const uint64_t wg0 = gfn::add_c(gfn::mul(w[c + i], binv0), gam0);
+        const uint64_t wg1 = gfn::add_c(gfn::mul(w[c + i], binv1), gam1);
+        num0 = gfn::mul(num0, gfn::add(wg0, kx));
+        num1 = gfn::mul(num1, gfn::add(wg1, kx));
+        den0 = gfn::mul(den0, gfn::add(wg0, s));
+        den1 = gfn::mul(den1, gfn::add(wg1, s));
+        kx = gfn::mul(kx, gl::GEN);
       }
+      const uint32_t bw = k == nchunks - 1 ? CH_BETA_LAST : CH_BETA_QDF;
 #pragma unroll
       for (uint32_t cc = 0; cc < 2; cc++) {
         const uint64_t prev = k == 0 ? zl[(uint64_t)cc * N + t] : zl[((uint64_t)2 + cc * npp + k - 1) * N + t];
         const uint64_t next = k == nchunks - 1 ? zl[(uint64_t)cc * N + tn] : zl[((uint64_t)2 + cc * npp + k) * N + t];
         emit(2 + cc * nchunks + k,
-             gfn::sub(gfn::mul(prev, cc ? num1 : num0), gfn::mul(next, cc ? den1 : den0)));
+             gfn::mul(gfn::sub(gfn::mul(prev, cc ? num1 : num0), gfn::mul(next, cc ? den1 : den0)), ch[bw + cc]));
       }
     }
     // Arithmetic ops (4 wires), ArithmeticExtension ops (8), MulExtension ops (6)

@@ -185,6 +185,7 @@ int qp_quotient(qp_ctx *ctx, const qp_batch *cs, const qp_batch *wires, const qp
         p = gl::mul(p, gl::canon(alphas[c]));
       }
     }
+    qpk::perm_challenges(chal.data(), chal.data() + qpk::CH_BETA, chal.data() + qpk::CH_GAMMA, 2, R, qdf);
     for (int i = 0; i < 4; i++) chal[qpk::CH_PIH + i] = gl::canon(pi_hash[i]);
     DMem d_tab, d_chal, d_apow, d_q, d_cbuf, d_out;
     QP_HIP_TRY(ctx, d_tab.alloc(tab.size()));
