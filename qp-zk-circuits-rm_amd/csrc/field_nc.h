@@ -102,6 +102,18 @@ struct Acc3 {
     asm(QP_CWAIT "v_addc_co_u32_e64 %0, %1, %2, 0, %1" : "=v"(top), "+s"(c) : "v"(top));
     hi = ((uint64_t)h1 << 32) | h0;
   }
+  // += x 2^e (0 <= e < 64) as the 128-bit integer it is: no reduction
+  __device__ __forceinline__ void add_shifted(uint64_t x, uint32_t e) {
+    const uint64_t xl = x << e, xh = e ? x >> (64 - e) : 0;
+    uint32_t c0, c1, c2, c3, c4;
+    const uint32_t l0 = __builtin_addc(pf::lo32(lo), pf::lo32(xl), 0u, &c0);
+    const uint32_t l1 = __builtin_addc(pf::hi32(lo), pf::hi32(xl), c0, &c1);
+    const uint32_t h0 = __builtin_addc(pf::lo32(hi), pf::lo32(xh), c1, &c2);
+    const uint32_t h1 = __builtin_addc(pf::hi32(hi), pf::hi32(xh), c2, &c3);
+    top = __builtin_addc(top, 0u, c3, &c4);
+    lo = ((uint64_t)l1 << 32) | l0;
+    hi = ((uint64_t)h1 << 32) | h0;
+  }
   // 2^128 = 2^96 2^32 = -2^32 (mod p)
   __device__ __forceinline__ uint64_t value() const { return sub(reduce(lo, hi), (uint64_t)top << 32); }
 };

@@ -651,7 +651,8 @@ k_quotient_1r(QuotientArgs a) {
   // per-gate alpha sums (multiplied by the gate's filter at the end)
   uint64_t sc0 = 0, sc1 = 0, sp0 = 0, sp1 = 0;  // 2 and 4 terms: reduced as they come
   gfn::Acc3 sb0, sb1, sa0, sa1;  // the BaseSum and Arithmetic gates' terms
-  uint64_t bs_acc = 0, w0 = 0, wa0 = 0, wa1 = 0, wa2 = 0;
+  uint64_t w0 = 0, wa0 = 0, wa1 = 0, wa2 = 0;
+  gfn::Acc3 bs_acc;  // sum of limb_i 2^i as a wide integer, reduced once
   // the Poseidon gate reads wires 0..23 again after the sweep: the first
   // QSTASH of them are kept in LDS (per lane, conflict-free [j][lane])
   __shared__ uint64_t stash[QSTASH * 256];
@@ -712,14 +713,14 @@ k_quotient_1r(QuotientArgs a) {
       if (jj == 0) {
         w0 = w;
       } else if (jj <= L) {
-        bs_acc = gfn::add(bs_acc, mul_pow2_rt(w, jj - 1));
+        bs_acc.add_shifted(w, jj - 1);
         {
           const uint64_t tb = gfn::mul(w, gfn::sub(w, 1));
           sb0.mac(tb, p0[pre + jj]);
           sb1.mac(tb, p1[pre + jj]);
         }
         if (jj == L) {
-          const uint64_t tb = gfn::sub(bs_acc, w0);
+          const uint64_t tb = gfn::sub(bs_acc.value(), w0);
           sb0.mac(tb, p0[pre]);
           sb1.mac(tb, p1[pre]);
         }
