@@ -188,6 +188,9 @@ def parse():
     ap.add_argument("--configs3-steps", type=int, default=4,
                     help="configs[3] also as K batches back to back (leaves of batch k+1 overlapping the "
                          "aggregation of batch k); 0 or 1: the single-batch record only")
+    ap.add_argument("--configs3-parts", type=int, default=4,
+                    help="configs[3] also with the batch's leaves proved in this many parts, each part's sub-tree "
+                         "aggregated as soon as its leaves exist (0 or 1: skip)")
     ap.add_argument("--configs3", type=int, default=1,
                     help="after the headline, time BASELINE configs[3] as one pipeline (every rank: its batch of "
                          "leaves -> its subtree root; roots gathered over RCCL; rank 0: the tree root); 0 = skip")
@@ -565,7 +568,7 @@ def voting_pass(qp_wormhole, local, batch=1024, nprov=6):
                     "timed region"}
 
 
-def configs3(args, circuit, prover, provers, cin, per, NP, B, dist, world, rank, local, torch):
+def configs3(args, circuit, prover, provers, cin, cin_inputs, per, NP, B, dist, world, rank, local, torch):
     """BASELINE configs[3] ("Batch 2048 proofs sharded 8xMI355X, RCCL-gather leaves
     into recursive aggregator"; aggregator.rs:74-92, tree.rs:55-103) timed as one
     pipeline (qp_wormhole.distributed.pipeline_aggregate_step): every rank proves
@@ -615,6 +618,53 @@ def configs3(args, circuit, prover, provers, cin, per, NP, B, dist, world, rank,
         tt = torch.tensor([dt], dtype=torch.float64, device=dev)
         dist.all_reduce(tt, op=dist.ReduceOp.MAX)
         dt = float(tt.item())
+    # one batch with its leaves proved in `parts` consecutive parts (the
+    # sub-trees' leaf ranges) and each part's sub-tree aggregated as soon as its
+    # leaves exist (pipeline_aggregate_step_streamed): the same root
+    strm = None
+    P = args.configs3_parts
+    if P > 1 and ns % P == 0 and ns // P >= 2:
+        from qp_wormhole.distributed import pipeline_aggregate_step_streamed
+        m = ns // P
+        pin = []
+        for q in range(P):
+            sub = [inp for i in range(NP) for inp in cin_inputs[i]][q * m:(q + 1) * m]
+            pp = [m // NP + (1 if i < m % NP else 0) for i in range(NP)]
+            pf = [sum(pp[:i]) for i in range(NP)]
+            pin.append([(provers[i].inputs_array(sub[pf[i]:pf[i] + pp[i]]), pp[i]) for i in range(NP)])
+
+        def prove_part(q):
+            outs = [None] * NP
+
+            def run(i):
+                arr, k = pin[q][i]
+                outs[i] = provers[i].prove_inputs_array(arr, k) if k else []
+            th = [threading.Thread(target=run, args=(i,)) for i in range(NP)]
+            for t in th:
+                t.start()
+            for t in th:
+                t.join()
+            if any(o is None for o in outs):
+                raise RuntimeError("a leaf prover thread failed")
+            return [p for o in outs for p in o]
+
+        def sstep():
+            return pipeline_aggregate_step_streamed(prove_part, P, m, cb, vo, 2, dist, device=dev, gpu=local)
+        sstep()  # untimed (the parts' smaller leaf batches)
+        if dist is not None:
+            dist.barrier()
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        sroot, stm = sstep()
+        torch.cuda.synchronize()
+        if dist is not None:
+            dist.barrier()
+        sdt = time.perf_counter() - t0
+        if dist is not None:
+            tt = torch.tensor([sdt], dtype=torch.float64, device=dev)
+            dist.all_reduce(tt, op=dist.ReduceOp.MAX)
+            sdt = float(tt.item())
+        strm = (sroot, stm, sdt)
     # the same as a stream of batches: batch k+1's leaves proved while batch k
     # is aggregated (pipeline_aggregate_steps), K batches timed end to end
     pipe = None
@@ -657,11 +707,24 @@ def configs3(args, circuit, prover, provers, cin, per, NP, B, dist, world, rank,
                      "note": "K batches back to back, batch k+1's leaves proved on the leaf provers' streams "
                              "while batch k is aggregated on the level provers' (the subtree's narrow top "
                              "levels are latency-bound); leaves_s overlaps the previous batch's subtree"}
+    streamed = None
+    if strm is not None:
+        sroot, stm, sdt = strm
+        stops = sroot if isinstance(sroot, list) else [sroot]
+        streamed = {"parts": P, "seconds": sdt, "value": leaves / sdt,
+                    "unit": "leaf proofs/s (proved and aggregated into one root)",
+                    "root_verified": all(verified(t) for t in stops),
+                    "same_root_as_batch_step": [t.proof.to_bytes() for t in stops] == [t.proof.to_bytes()
+                                                                                         for t in tops],
+                    "stages_rank0_s": {k: round(v, 4) for k, v in stm.items() if isinstance(v, float)},
+                    "note": f"the batch's leaves proved in {P} parts (the sub-trees' leaf ranges, {ns // P} "
+                            "leaves each over the same provers) on a producer thread, each part's sub-tree "
+                            "aggregated as soon as its leaves exist; leaves_s = when the last part was proved"}
     return {"workload": f"{leaves}_leaves_as_{world}x{ns}_per_gpu_subtrees_branching2",
             "value": leaves / dt, "unit": "leaf proofs/s (proved and aggregated into one root)"
             if len(tops) == 1 else f"leaf proofs/s (proved and aggregated into {len(tops)} top proofs)",
             "seconds": dt, "leaves": leaves, "aggregation_proofs": leaves - len(tops),
-            "stages_rank0_s": tm, "pipelined": pipelined,
+            "stages_rank0_s": tm, "pipelined": pipelined, "streamed": streamed,
             "root_verified" if len(tops) == 1 else "top_proofs_verified": ok,
             "top_circuit_degree_bits": _common_degree_bits(tops[0].circuit_data.common),
             "root_public_inputs": sum(len(t.proof.public_inputs) for t in tops),
@@ -836,7 +899,8 @@ def main():
     # leaves -> per-GPU subtree root -> RCCL gather of the roots -> tree root on rank 0
     c3 = None
     if not voting and args.configs3 and args.mode == "e2e":
-        c3 = configs3(args, circuit, prover, provers, cin, per, NP, B, dist, world, rank, local, torch)
+        c3 = configs3(args, circuit, prover, provers, cin, [inputs[first[i]:first[i] + per[i]] for i in range(NP)],
+                      per, NP, B, dist, world, rank, local, torch)
     # standard_recursion_zk_config (the reference's cargo-bench and aggregator config):
     # under no_random it proves the same circuit without salts, one prover, one batch
     zk = None

@@ -289,6 +289,67 @@ class CircuitTooLarge(ValueError):
         self.proofs = proofs
 
 
+def _too_large(config, backend, inner_common, proofs):
+    """The degree of the first circuit a level over `proofs` would build that
+    exceeds the GPU prover (full chunks of k and a shorter tail), else None."""
+    if backend is not None:
+        return None
+    k = config.tree_branching_factor
+    sizes = ([k] if len(proofs) >= k else []) + ([len(proofs) % k] if len(proofs) % k else [])
+    for size in sizes:
+        c = aggregation_circuit(inner_common, size)
+        if c.degree_bits > GPU_MAX_DEGREE_BITS:
+            return c.degree_bits
+    return None
+
+
+def _levels(proofs, config, device, backend, prover=None, nprov=0):
+    """Levels down to one proof; returns (proofs, None) or (the last level
+    proven, the message of the circuit that was too large)."""
+    while len(proofs) > 1:
+        cd = proofs[0].circuit_data
+        db = _too_large(config, backend, cd.common, proofs)
+        if db is not None:
+            return proofs, (f"the next level's aggregation circuit is 2^{db} rows (its public inputs: every "
+                            f"leaf's); the GPU prover proves up to 2^{GPU_MAX_DEGREE_BITS}")
+        proofs = aggregate_level([p.proof for p in proofs], cd.common, cd.verifier_only, config, device,
+                                 backend, prover, nprov)
+    return proofs, None
+
+
+def _sub_trees(part_leaves, parts, common_data, verifier_only, config, device, backend):
+    """`parts` independent sub-trees, one thread and one device prover each,
+    with no level barrier between them, so one sub-tree's host phases and
+    latency-bound launches overlap the others' kernels; part_leaves(i) gives
+    sub-tree i's leaf proofs (it may block until they exist).  Returns the
+    sub-tree roots in order (CircuitTooLarge if a level is beyond the GPU)."""
+    # one device prover per sub-tree, the same count for every thread (so no
+    # thread rebuilds a level prover another thread has just built)
+    nprov = max(parts, _agg_provers())
+    res = [None] * parts
+    errors = []
+
+    def run(i):
+        try:
+            lv = aggregate_level(part_leaves(i), common_data, verifier_only, config, device, backend, i, nprov)
+            res[i] = _levels(lv, config, device, backend, i, nprov)
+        except BaseException as e:  # re-raised on the calling thread
+            errors.append(e)
+
+    th = [threading.Thread(target=run, args=(i,)) for i in range(parts)]
+    for t in th:
+        t.start()
+    for t in th:
+        t.join()
+    if errors:
+        raise errors[0]
+    msg = next((r[1] for r in res if r[1]), None)
+    proofs = [p for r in res for p in r[0]]
+    if msg:
+        raise CircuitTooLarge(msg, proofs)
+    return proofs
+
+
 def aggregate_to_tree(leaf_proofs, common_data: bytes, verifier_only: bytes,
                       config: Optional[TreeAggregationConfig] = None, device: int = 0,
                       backend=None) -> AggregatedProof:
@@ -298,73 +359,47 @@ def aggregate_to_tree(leaf_proofs, common_data: bytes, verifier_only: bytes,
     root of 2048 leaves registers 32,768 and needs 2^15 rows): a level whose
     circuit exceeds the GPU prover's 2^GPU_MAX_DEGREE_BITS raises
     CircuitTooLarge carrying the proofs of the level below (not with a CPU
-    backend)."""
+    backend).  Large trees run as concurrent sub-trees (_subtree_parts: the
+    same chunks as the level-by-level order, so the same proofs)."""
     config = config or TreeAggregationConfig.default()
-
-    def check(inner_common, proofs):
-        # every circuit the level builds: full chunks of k and a shorter tail
-        if backend is not None:
-            return None
-        k = config.tree_branching_factor
-        sizes = ([k] if len(proofs) >= k else []) + ([len(proofs) % k] if len(proofs) % k else [])
-        for size in sizes:
-            c = aggregation_circuit(inner_common, size)
-            if c.degree_bits > GPU_MAX_DEGREE_BITS:
-                return c.degree_bits
-        return None
-
-    db = check(common_data, leaf_proofs)
+    db = _too_large(config, backend, common_data, leaf_proofs)
     if db is not None:
         raise CircuitTooLarge(f"level-1 aggregation circuit is 2^{db} rows", [])
-
-    def levels(proofs, prover=None, nprov=0):
-        """Levels down to one proof; returns (proofs, None) or (the last level
-        proven, the message of the circuit that was too large)."""
-        while len(proofs) > 1:
-            cd = proofs[0].circuit_data
-            db = check(cd.common, proofs)
-            if db is not None:
-                return proofs, (f"the next level's aggregation circuit is 2^{db} rows (its public inputs: every "
-                                f"leaf's); the GPU prover proves up to 2^{GPU_MAX_DEGREE_BITS}")
-            proofs = aggregate_level([p.proof for p in proofs], cd.common, cd.verifier_only, config, device,
-                                     backend, prover, nprov)
-        return proofs, None
-
     parts = _subtree_parts(len(leaf_proofs), config.tree_branching_factor) if backend is None else 1
     if parts > 1:
-        # independent sub-trees (consecutive leaf ranges of k^m leaves, the
-        # same chunks as the level-by-level order), one thread and one device
-        # prover each: no level barrier between them, so one sub-tree's host
-        # phases and latency-bound launches overlap the other's kernels
         m = len(leaf_proofs) // parts
-        # one device prover per sub-tree, the same count for every thread (so
-        # no thread rebuilds a level prover another thread has just built)
-        nprov = max(parts, _agg_provers())
-        res = [None] * parts
-        errors = []
-
-        def run(i):
-            try:
-                lv = aggregate_level(leaf_proofs[i * m:(i + 1) * m], common_data, verifier_only, config, device,
-                                     backend, i, nprov)
-                res[i] = levels(lv, i, nprov)
-            except BaseException as e:  # re-raised on the calling thread
-                errors.append(e)
-
-        th = [threading.Thread(target=run, args=(i,)) for i in range(parts)]
-        for t in th:
-            t.start()
-        for t in th:
-            t.join()
-        if errors:
-            raise errors[0]
-        msg = next((r[1] for r in res if r[1]), None)
-        proofs = [p for r in res for p in r[0]]
-        if msg:
-            raise CircuitTooLarge(msg, proofs)
+        proofs = _sub_trees(lambda i: leaf_proofs[i * m:(i + 1) * m], parts, common_data, verifier_only, config,
+                            device, backend)
     else:
         proofs = aggregate_level(leaf_proofs, common_data, verifier_only, config, device, backend)
-    proofs, msg = levels(proofs)
+    proofs, msg = _levels(proofs, config, device, backend)
+    if msg:
+        raise CircuitTooLarge(msg, proofs)
+    assert len(proofs) == 1
+    return proofs[0]
+
+
+def aggregate_to_tree_streamed(part_leaves, parts: int, common_data: bytes, verifier_only: bytes,
+                               config: Optional[TreeAggregationConfig] = None, device: int = 0,
+                               backend=None) -> AggregatedProof:
+    """aggregate_to_tree over leaves that arrive one complete sub-tree at a
+    time: part_leaves(i) blocks until sub-tree i's leaf proofs exist (a
+    producer proving them in order), and each sub-tree is aggregated on its
+    own thread as soon as they do, while the producer proves the next part's
+    leaves -- so the sub-trees' latency-bound upper levels overlap the later
+    leaves' kernels instead of idling the GPU at the end.  The parts are the
+    consecutive leaf ranges of aggregate_to_tree's sub-trees, so the root is
+    the same proof (same chunks, same order).  parts must be a power of the
+    branching factor."""
+    config = config or TreeAggregationConfig.default()
+    k = config.tree_branching_factor
+    p = parts
+    while p % k == 0 and p > 1:
+        p //= k
+    if parts < 1 or p != 1:
+        raise ValueError(f"{parts} parts are not a power of the branching factor {k}")
+    proofs = _sub_trees(part_leaves, parts, common_data, verifier_only, config, device, backend)
+    proofs, msg = _levels(proofs, config, device, backend)
     if msg:
         raise CircuitTooLarge(msg, proofs)
     assert len(proofs) == 1

@@ -181,21 +181,28 @@ def aggregate_subtrees(local_proofs, common: bytes, verifier_only: bytes, branch
     (a dict) receives the seconds of the stages: subtree_s, gather_s, top_s."""
     import time
     from .aggregator import TreeAggregationConfig, aggregate_to_tree
-    from .prover import ProofWithPublicInputs
-    world, rank = (dist.get_world_size(), dist.get_rank()) if dist is not None else (1, 0)
     if dist is not None:
         check_subtree_shards(len(local_proofs), branching, dist, device)
     elif log_exact(len(local_proofs), branching) in (None, 0):
         raise ValueError(f"{len(local_proofs)} local proofs are not a power (>= 1) of the branching factor "
                          f"{branching}")
     depth = log_exact(len(local_proofs), branching)
-    wdepth = log_exact(world, branching)
     tm = timings if timings is not None else {}
     t0 = time.perf_counter()
     sub = aggregate_to_tree(local_proofs, common, verifier_only, TreeAggregationConfig.new(branching, depth),
                             gpu, backend)
+    tm["subtree_s"] = time.perf_counter() - t0
+    return _roots_to_top(sub, branching, dist, device, gpu, dst, backend, tm)
+
+
+def _roots_to_top(sub, branching: int, dist, device, gpu: int, dst: int, backend, tm):
+    """Each rank's subtree root -> rank dst (one gather of world proofs), which
+    aggregates them into the tree root (aggregate_subtrees' last two stages)."""
+    import time
+    from .aggregator import TreeAggregationConfig, aggregate_to_tree
+    from .prover import ProofWithPublicInputs
+    world, rank = (dist.get_world_size(), dist.get_rank()) if dist is not None else (1, 0)
     t1 = time.perf_counter()
-    tm["subtree_s"] = t1 - t0
     if dist is not None:
         roots = gather_proofs([sub.proof.to_bytes()], len(sub.proof.to_bytes()), dist, device=device, dst=dst)
     else:
@@ -211,7 +218,7 @@ def aggregate_subtrees(local_proofs, common: bytes, verifier_only: bytes, branch
     from .aggregator import CircuitTooLarge
     try:
         root = aggregate_to_tree([ProofWithPublicInputs(r, []) for r in roots], cd.common, cd.verifier_only,
-                                 TreeAggregationConfig.new(branching, wdepth), gpu, backend)
+                                 TreeAggregationConfig.new(branching, log_exact(world, branching)), gpu, backend)
     except CircuitTooLarge as e:
         # the top of a deep tree (e.g. 2048 leaves: the root registers 32,768
         # public inputs, 2^15 rows) is beyond the GPU prover: the proofs of the
@@ -220,6 +227,65 @@ def aggregate_subtrees(local_proofs, common: bytes, verifier_only: bytes, branch
         tm["top_stopped"] = str(e)
     tm["top_s"] = time.perf_counter() - t2
     return root
+
+
+def pipeline_aggregate_step_streamed(prove_part, parts: int, part_leaves: int, common: bytes,
+                                     verifier_only: bytes, branching: int, dist=None, device="cpu", gpu: int = 0,
+                                     dst: int = 0, backend=None):
+    """pipeline_aggregate_step with the rank's leaves proved in `parts`
+    consecutive parts (prove_part(i) -> the part's part_leaves serialized
+    proofs, called in order on a producer thread) and each part's sub-tree
+    aggregated as soon as its leaves exist (aggregator.aggregate_to_tree_streamed),
+    while the next part's leaves are proved: the sub-trees' latency-bound upper
+    levels overlap the later parts' leaf kernels.  The same leaves and chunks as
+    pipeline_aggregate_step, so the same root.  Returns (root on dst / None,
+    stage seconds: leaves_s = when the last part's leaves were done, subtree_s
+    = the local root, gather_s, top_s)."""
+    import threading
+    import time
+    from .aggregator import TreeAggregationConfig, aggregate_to_tree_streamed
+    n_local = parts * part_leaves
+    if dist is not None:
+        check_subtree_shards(n_local, branching, dist, device)
+    elif log_exact(n_local, branching) in (None, 0) or log_exact(parts, branching) is None:
+        raise ValueError(f"{parts} parts of {part_leaves} leaves do not form a {branching}-ary tree")
+    ready = [threading.Event() for _ in range(parts)]
+    got = [None] * parts
+    errors = []
+    tm = {}
+    t0 = time.perf_counter()
+
+    def producer():
+        try:
+            for i in range(parts):
+                got[i] = prove_part(i)
+                if len(got[i]) != part_leaves:
+                    raise ValueError(f"part {i}: {len(got[i])} leaf proofs, expected {part_leaves}")
+                ready[i].set()
+            tm["leaves_s"] = time.perf_counter() - t0
+        except BaseException as e:  # re-raised on the calling thread
+            errors.append(e)
+            for ev in ready:
+                ev.set()
+
+    def leaves_of(i):
+        ready[i].wait()
+        if errors:
+            raise RuntimeError("the leaf producer failed") from errors[0]
+        return got[i]
+
+    th = threading.Thread(target=producer, daemon=True)
+    th.start()
+    try:
+        sub = aggregate_to_tree_streamed(leaves_of, parts, common, verifier_only,
+                                         TreeAggregationConfig.new(branching, log_exact(n_local, branching)), gpu,
+                                         backend)
+    finally:
+        th.join()
+    if errors:
+        raise errors[0]
+    tm["subtree_s"] = time.perf_counter() - t0
+    return _roots_to_top(sub, branching, dist, device, gpu, dst, backend, tm), tm
 
 
 def pipeline_aggregate_step(prove_leaves, common: bytes, verifier_only: bytes, branching: int, dist=None,

@@ -410,3 +410,34 @@ def test_configs3_pipelined_leaf_failure_stops_every_rank():
         assert p.exitcode == 0
     assert got[1] == "leaf failure on rank 1"
     assert got[0] == "another rank's leaf step failed"
+
+
+def test_configs3_streamed_step_equals_the_batch_step():
+    """pipeline_aggregate_step_streamed (leaves proved part by part on a
+    producer thread, each part's sub-tree aggregated as soon as its leaves
+    exist) gives the same root as pipeline_aggregate_step over the same leaves:
+    the same chunks in the same order (oracle backend, one rank)."""
+    from agg_oracle_backend import oracle_backend
+    from current_circuit_vd import current_circuit_verifier_data
+    from oracle_lib import golden, lib as olib
+    from qp_wormhole.distributed import pipeline_aggregate_step, pipeline_aggregate_step_streamed
+    from test_oracle_golden import current_common_bytes
+    cb = current_common_bytes()
+    vd = current_circuit_verifier_data(cb)[0]
+    vo = vd[:len(vd) - len(cb)]
+    fx = [golden("dummy_proof.bin"), golden("dummy_proof_zk.bin")]
+    leaves = [fx[0], fx[1], fx[1], fx[0]]
+    calls = []
+
+    def prove_part(i):
+        calls.append(i)
+        return leaves[2 * i:2 * i + 2]
+    root_s, tm = pipeline_aggregate_step_streamed(prove_part, 2, 2, cb, vo, 2, backend=oracle_backend)
+    root_b, _ = pipeline_aggregate_step(lambda: leaves, cb, vo, 2, backend=oracle_backend)
+    assert calls == [0, 1]
+    assert root_s.proof.to_bytes() == root_b.proof.to_bytes()
+    rvd = root_s.circuit_data.verifier_data()
+    assert olib().ora_verify(rvd, len(rvd), root_s.proof.to_bytes(), len(root_s.proof.to_bytes())) == 0
+    assert sorted(tm) == ["gather_s", "leaves_s", "subtree_s", "top_s"]
+    with pytest.raises(ValueError):
+        pipeline_aggregate_step_streamed(prove_part, 3, 2, cb, vo, 2, backend=oracle_backend)
