@@ -303,7 +303,7 @@ def _too_large(config, backend, inner_common, proofs):
     return None
 
 
-def _levels(proofs, config, device, backend, prover=None, nprov=0):
+def _levels_down(proofs, config, device, backend, prover=None, nprov=0):
     """Levels down to one proof; returns (proofs, None) or (the last level
     proven, the message of the circuit that was too large)."""
     while len(proofs) > 1:
@@ -332,7 +332,7 @@ def _sub_trees(part_leaves, parts, common_data, verifier_only, config, device, b
     def run(i):
         try:
             lv = aggregate_level(part_leaves(i), common_data, verifier_only, config, device, backend, i, nprov)
-            res[i] = _levels(lv, config, device, backend, i, nprov)
+            res[i] = _levels_down(lv, config, device, backend, i, nprov)
         except BaseException as e:  # re-raised on the calling thread
             errors.append(e)
 
@@ -372,7 +372,7 @@ def aggregate_to_tree(leaf_proofs, common_data: bytes, verifier_only: bytes,
                             device, backend)
     else:
         proofs = aggregate_level(leaf_proofs, common_data, verifier_only, config, device, backend)
-    proofs, msg = _levels(proofs, config, device, backend)
+    proofs, msg = _levels_down(proofs, config, device, backend)
     if msg:
         raise CircuitTooLarge(msg, proofs)
     assert len(proofs) == 1
@@ -399,7 +399,7 @@ def aggregate_to_tree_streamed(part_leaves, parts: int, common_data: bytes, veri
     if parts < 1 or p != 1:
         raise ValueError(f"{parts} parts are not a power of the branching factor {k}")
     proofs = _sub_trees(part_leaves, parts, common_data, verifier_only, config, device, backend)
-    proofs, msg = _levels(proofs, config, device, backend)
+    proofs, msg = _levels_down(proofs, config, device, backend)
     if msg:
         raise CircuitTooLarge(msg, proofs)
     assert len(proofs) == 1
