@@ -188,7 +188,7 @@ def parse():
     ap.add_argument("--configs3-steps", type=int, default=4,
                     help="configs[3] also as K batches back to back (leaves of batch k+1 overlapping the "
                          "aggregation of batch k); 0 or 1: the single-batch record only")
-    ap.add_argument("--configs3-parts", type=int, default=4,
+    ap.add_argument("--configs3-parts", type=int, default=0,
                     help="configs[3] also with the batch's leaves proved in this many parts, each part's sub-tree "
                          "aggregated as soon as its leaves exist (0 or 1: skip)")
     ap.add_argument("--configs3", type=int, default=1,
