@@ -190,10 +190,30 @@ def aggregation_circuit(inner_common: bytes, branching: int) -> Circuit:
 _pool = None
 
 
+def _cores_per_rank() -> int:
+    """The cores this process may use (affinity mask, capped by a cgroup v2 cpu.max
+    quota) divided among the node's local ranks (LOCAL_WORLD_SIZE)."""
+    try:
+        n = len(os.sched_getaffinity(0))
+    except (AttributeError, OSError):
+        n = os.cpu_count() or 4
+    try:
+        q, per = open("/sys/fs/cgroup/cpu.max").read().split()[:2]
+        if q != "max":
+            n = min(n, max(1, int(int(q) / int(per))))
+    except (OSError, ValueError):
+        pass
+    return max(1, n // max(1, int(os.environ.get("LOCAL_WORLD_SIZE", "1"))))
+
+
 def _host_budget() -> int:
-    """Host threads aggregation may use: QP_AGG_THREADS, else the process's CPU
-    budget (OMP_NUM_THREADS on the GPU boxes), at most 16."""
-    n = int(os.environ.get("QP_AGG_THREADS") or os.environ.get("OMP_NUM_THREADS") or min(os.cpu_count() or 4, 16))
+    """Host threads aggregation may use: QP_AGG_THREADS, else the larger of
+    OMP_NUM_THREADS (the GPU boxes' per-job share) and this rank's share of the
+    usable cores (torchrun sets OMP_NUM_THREADS=1 for its workers when the
+    environment has none), at most 16."""
+    if os.environ.get("QP_AGG_THREADS"):
+        return max(1, min(int(os.environ["QP_AGG_THREADS"]), 16))
+    n = max(int(os.environ.get("OMP_NUM_THREADS") or 0), _cores_per_rank())
     return max(1, min(n, 16))
 
 
