@@ -39,7 +39,7 @@ VALU_PEAK_WAVE_INSTR_S = 1024 * 2.4e9 / 2
 # measured per-build inputs of the roofline fields, written by the profiling
 # session of this build (tools/gpu_session.sh prof3 / pmc_*; tools/kernel_summary.py,
 # tools/pmc_sq_summary.py, tools/pmc_summary.py)
-PROFILE_TAG = "r05"
+PROFILE_TAG = "r06"
 PMC_FILE = os.path.join(ROOT, "profiles", f"{PROFILE_TAG}_pmc_hbm_b128.json")
 PMC_SQ_FILE = os.path.join(ROOT, "profiles", f"{PROFILE_TAG}_pmc_sq_b128.json")
 KSUM_FILE = os.path.join(ROOT, "profiles", f"{PROFILE_TAG}_kernel_summary_3provers.json")

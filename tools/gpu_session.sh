@@ -19,7 +19,7 @@ step() {  # step <name> <timeout> <cmd...>
 pmc() {  # pmc <name> <counters...>
   local name=$1; shift
   step "pmc_$name" 300 rocprofv3 --pmc "$@" --output-format csv -d "gpurun_out/pmc_$name" -o run -- \
-    python3 bench.py --steps 1 --warmup 1 --cpu-sample 0 --provers 1 --batch 128
+    python3 bench.py --steps 1 --warmup 1 --cpu-sample 0 --provers 1 --batch 128 --configs3 0 --ref-shapes 0
 }
 for s in "$@"; do
   case $s in
@@ -223,6 +223,20 @@ for s in "$@"; do
              step pv4_$r 300 python -u bench.py --steps 10 --warmup 1 --cpu-sample 0 --agg-leaves 0 --configs3 0 --provers 4 &&
              step pv2_$r 300 python -u bench.py --steps 10 --warmup 1 --cpu-sample 0 --agg-leaves 0 --configs3 0 --provers 2 || exit 1
              done ;;
+    final6) step pytest_gpu 900 python -u -m pytest tests -m gpu -x -v --timeout 400 --timeout-method thread &&
+            step smoke 300 python -c "import __graft_entry__ as g; g.smoke()" &&
+            step bench 900 python -u bench.py &&
+            step rocprof_bench 900 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/prof_bench -o run -- python3 bench.py --steps 2 --warmup 1 --cpu-sample 0 --ref-shapes 0 &&
+            step rocprof_bench1 600 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/prof_bench1 -o run -- python3 bench.py --steps 2 --warmup 1 --cpu-sample 0 --provers 1 --ref-shapes 0 &&
+            pmc fetch FETCH_SIZE && pmc write WRITE_SIZE &&
+            pmc sq SQ_WAVES SQ_INSTS_VALU SQ_ACTIVE_INST_VALU SQ_WAVE_CYCLES SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_BUSY_CYCLES SQ_WAIT_ANY &&
+            step pmc_calib 600 bash tools/pmc_calib.sh &&
+            step prof_agg 300 env QP_AGG_PROVERS=1 QP_AGG_SPLIT=1 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/prof_agg -o run -- python3 tools/agg_subtree.py 256 1 &&
+            step prof_aggd 300 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/prof_aggd -o run -- python3 tools/agg_subtree.py 256 1 &&
+            step leaf_ubench 300 tools/leaf_ubench 86 5 &&
+            step agg_subtree 300 python -u tools/agg_subtree.py 256 3 &&
+            step bench_voting 600 python -u bench.py --circuit voting &&
+            step final_summaries 300 bash tools/final_summaries.sh r06 ;;
     final5) step pytest_gpu 900 python -u -m pytest tests -m gpu -x -v --timeout 400 --timeout-method thread &&
             step smoke 300 python -c "import __graft_entry__ as g; g.smoke()" &&
             step bench 900 python -u bench.py &&
