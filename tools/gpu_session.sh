@@ -80,6 +80,15 @@ for s in "$@"; do
              step pmc_lde_sq_$v 120 rocprofv3 --pmc SQ_WAVES SQ_INSTS_VALU SQ_ACTIVE_INST_VALU SQ_WAVE_CYCLES SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_BUSY_CYCLES SQ_WAIT_ANY --kernel-include-regex k_lde_cosets --output-format csv -d gpurun_out/pmc_lde_sq_$v -o run -- python3 tools/kbench.py 86 1 &&
              step pmc_lde_sum_$v 60 python3 tools/pmc_sq_summary.py gpurun_out/pmc_lde_sq_$v gpurun_out/pmc_lde_sq_$v.json && rm -rf gpurun_out/pmc_lde_sq_$v || exit 1
            done; unset QPGPU_LIB ;;
+    powocc) for r in 1 2; do for v in pow6 pow5 pow7; do
+             if [ $v = pow6 ]; then unset QPGPU_LIB; else export QPGPU_LIB=qp-zk-circuits-rm_amd/qp_wormhole/variants/libqpgpu_$v.so; fi
+             step prof_${v}_$r 300 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/prof_${v}_$r -o run -- python3 bench.py --steps 2 --warmup 1 --cpu-sample 0 --provers 1 --configs3 0 --agg-leaves 0 --ref-shapes 0 &&
+             grep -h "k_pow_scan\|Name" gpurun_out/prof_${v}_$r/run_kernel_stats.csv > gpurun_out/prof_${v}_$r.stats && rm -rf gpurun_out/prof_${v}_$r || exit 1
+           done; done; unset QPGPU_LIB
+           for v in pow6 pow5; do
+             if [ $v = pow6 ]; then unset QPGPU_LIB; else export QPGPU_LIB=qp-zk-circuits-rm_amd/qp_wormhole/variants/libqpgpu_$v.so; fi
+             step vot_$v 600 python -u bench.py --circuit voting --agg-leaves 0 --configs3 0 --ref-shapes 0 --cpu-sample 0 || exit 1
+           done; unset QPGPU_LIB ;;
     bench5) step bench5 600 python -u bench.py --steps 5 --warmup 1 --cpu-sample 0 ;;
     agg_ab) step agg_dev2 300 python -u tools/agg_subtree.py 256 2 &&
             step agg_dev1 300 env QP_AGG_PROVERS=1 python -u tools/agg_subtree.py 256 2 &&
