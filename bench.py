@@ -202,6 +202,9 @@ def parse():
     ap.add_argument("--launch-selftest", choices=["ok", "fail-rank1"], default=None,
                     help="test the --gpus N launcher without a GPU: every rank joins a gloo group and rank 0 prints "
                          "the ranks it saw (fail-rank1: rank 1 exits non-zero first)")
+    ap.add_argument("--rehearse-shared-gpu", action="store_true",
+                    help="rehearse the --gpus N path on a one-GPU box: every rank proves on cuda:0, the process "
+                         "group is gloo over host tensors (not RCCL); the line says rehearsal (not a measurement)")
     return ap.parse_args()
 
 
@@ -289,7 +292,7 @@ def check_world(args, world, torch):
         print(f"bench.py: WORLD_SIZE {world} != --gpus {args.gpus}", file=sys.stderr, flush=True)
         sys.exit(3)
     ndev = torch.cuda.device_count()
-    if ndev < args.gpus:
+    if ndev < (1 if args.rehearse_shared_gpu else args.gpus):
         print(f"bench.py: --gpus {args.gpus} but this node has {ndev} GPU(s)", file=sys.stderr, flush=True)
         sys.exit(3)
 
@@ -568,7 +571,7 @@ def voting_pass(qp_wormhole, local, batch=1024, nprov=6):
                     "timed region"}
 
 
-def configs3(args, circuit, prover, provers, cin, cin_inputs, per, NP, B, dist, world, rank, local, torch):
+def configs3(args, circuit, prover, provers, cin, cin_inputs, per, NP, B, dist, world, rank, local, torch, cdev):
     """BASELINE configs[3] ("Batch 2048 proofs sharded 8xMI355X, RCCL-gather leaves
     into recursive aggregator"; aggregator.rs:74-92, tree.rs:55-103) timed as one
     pipeline (qp_wormhole.distributed.pipeline_aggregate_step): every rank proves
@@ -599,7 +602,7 @@ def configs3(args, circuit, prover, provers, cin, cin_inputs, per, NP, B, dist, 
             raise RuntimeError("a leaf prover thread failed")
         return [p for o in outs for p in o][:ns]
 
-    dev = f"cuda:{local}"
+    dev = cdev  # collective tensors (the rank's GPU; host tensors under --rehearse-shared-gpu)
 
     def step():
         return pipeline_aggregate_step(prove_leaves, cb, vo, 2, dist, device=dev, gpu=local)
@@ -745,11 +748,15 @@ def main():
     local = int(os.environ.get("LOCAL_RANK", "0"))
     import torch
     check_world(args, world, torch)
+    rehearse = args.rehearse_shared_gpu
+    if rehearse:
+        local = 0  # every rank's provers on the one GPU
+    cdev = "cpu" if rehearse else f"cuda:{local}"
     dist = None
     if world > 1:
         import torch.distributed as dist
         torch.cuda.set_device(local)
-        dist.init_process_group("nccl")
+        dist.init_process_group("gloo" if rehearse else "nccl")
         if dist.get_world_size() != args.gpus:
             print(f"bench.py: process group of {dist.get_world_size()} ranks != --gpus {args.gpus}",
                   file=sys.stderr, flush=True)
@@ -795,7 +802,7 @@ def main():
 
     def steps(k, pipelined):
         # leaf proofs -> aggregator rank over RCCL (raw gather) after every step
-        return run_steps(prove_share, NP, k, dist=dist, slot=prover.proof_size, device=f"cuda:{local}",
+        return run_steps(prove_share, NP, k, dist=dist, slot=prover.proof_size, device=cdev,
                          pipelined=pipelined, on_leaves=on_leaves)
 
     proofs = steps(args.warmup, False) if args.warmup else None
@@ -822,7 +829,7 @@ def main():
         dist.barrier()
     dt = time.perf_counter() - t0
     if dist is not None:
-        tt = torch.tensor([dt], dtype=torch.float64, device=f"cuda:{local}")
+        tt = torch.tensor([dt], dtype=torch.float64, device=cdev)
         dist.all_reduce(tt, op=dist.ReduceOp.MAX)
         dt = float(tt.item())
     # kernel statistics summed over the provers (HIP events on each prover's stream)
@@ -900,7 +907,7 @@ def main():
     c3 = None
     if not voting and args.configs3 and args.mode == "e2e":
         c3 = configs3(args, circuit, prover, provers, cin, [inputs[first[i]:first[i] + per[i]] for i in range(NP)],
-                      per, NP, B, dist, world, rank, local, torch)
+                      per, NP, B, dist, world, rank, local, torch, cdev)
     # standard_recursion_zk_config (the reference's cargo-bench and aggregator config):
     # under no_random it proves the same circuit without salts, one prover, one batch
     zk = None
@@ -945,6 +952,8 @@ def main():
             "n_gpus": world,
             "rccl_world_size": dist.get_world_size() if dist is not None else 1,
             "process_group_backend": dist.get_backend() if dist is not None else None,
+            "rehearsal": "shared-GPU rehearsal of the N-rank path (gloo, every rank on cuda:0): not a measurement"
+                         if rehearse else None,
             "leaf_proofs_gathered_per_step": gathered[-1] if gathered else None,
             "steps": args.steps,
             "warmup": args.warmup,
