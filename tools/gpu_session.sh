@@ -80,6 +80,19 @@ for s in "$@"; do
              step pmc_lde_sq_$v 120 rocprofv3 --pmc SQ_WAVES SQ_INSTS_VALU SQ_ACTIVE_INST_VALU SQ_WAVE_CYCLES SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_BUSY_CYCLES SQ_WAIT_ANY --kernel-include-regex k_lde_cosets --output-format csv -d gpurun_out/pmc_lde_sq_$v -o run -- python3 tools/kbench.py 86 1 &&
              step pmc_lde_sum_$v 60 python3 tools/pmc_sq_summary.py gpurun_out/pmc_lde_sq_$v gpurun_out/pmc_lde_sq_$v.json && rm -rf gpurun_out/pmc_lde_sq_$v || exit 1
            done; unset QPGPU_LIB ;;
+    pinned) V=qp-zk-circuits-rm_amd/qp_wormhole/variants/libqpgpu_pageable.so
+            for r in 1 2; do
+              step pin_agg_new_$r 300 python -u tools/agg_subtree.py 256 2 &&
+              step pin_agg_old_$r 300 env QPGPU_LIB=$V python -u tools/agg_subtree.py 256 2 || exit $?
+            done
+            step pin_bench_new 300 python -u bench.py --steps 5 --cpu-sample 0 --ref-shapes 0 &&
+            step pin_bench_old 300 env QPGPU_LIB=$V python -u bench.py --steps 5 --cpu-sample 0 --ref-shapes 0 ;;
+    hwq) for r in 1 2; do
+           step hwq_s4_q4_$r 300 python -u tools/agg_subtree.py 256 2 &&
+           step hwq_s8_q4_$r 300 env QP_AGG_SPLIT=8 python -u tools/agg_subtree.py 256 2 &&
+           step hwq_s8_q8_$r 300 env QP_AGG_SPLIT=8 GPU_MAX_HW_QUEUES=8 python -u tools/agg_subtree.py 256 2 &&
+           step hwq_s4_q8_$r 300 env GPU_MAX_HW_QUEUES=8 python -u tools/agg_subtree.py 256 2 || exit $?
+         done ;;
     powocc) for r in 1 2; do for v in pow6 pow5 pow7; do
              if [ $v = pow6 ]; then unset QPGPU_LIB; else export QPGPU_LIB=qp-zk-circuits-rm_amd/qp_wormhole/variants/libqpgpu_$v.so; fi
              step prof_${v}_$r 300 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/prof_${v}_$r -o run -- python3 bench.py --steps 2 --warmup 1 --cpu-sample 0 --provers 1 --configs3 0 --agg-leaves 0 --ref-shapes 0 &&
