@@ -80,6 +80,14 @@ for s in "$@"; do
              step pmc_lde_sq_$v 120 rocprofv3 --pmc SQ_WAVES SQ_INSTS_VALU SQ_ACTIVE_INST_VALU SQ_WAVE_CYCLES SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_BUSY_CYCLES SQ_WAIT_ANY --kernel-include-regex k_lde_cosets --output-format csv -d gpurun_out/pmc_lde_sq_$v -o run -- python3 tools/kbench.py 86 1 &&
              step pmc_lde_sum_$v 60 python3 tools/pmc_sq_summary.py gpurun_out/pmc_lde_sq_$v gpurun_out/pmc_lde_sq_$v.json && rm -rf gpurun_out/pmc_lde_sq_$v || exit 1
            done; unset QPGPU_LIB ;;
+    bsync) V=qp-zk-circuits-rm_amd/qp_wormhole/variants/libqpgpu_bsync.so
+           for r in 1 2; do
+             step bs_agg_def_$r 300 python -u tools/agg_subtree.py 256 2 &&
+             step bs_agg_blk_$r 300 env QPGPU_LIB=$V python -u tools/agg_subtree.py 256 2 &&
+             step bs_agg8_blk_$r 300 env QP_AGG_SPLIT=8 QPGPU_LIB=$V python -u tools/agg_subtree.py 256 2 || exit $?
+           done
+           step bs_bench_def 300 python -u bench.py --steps 5 --cpu-sample 0 --ref-shapes 0 &&
+           step bs_bench_blk 300 env QPGPU_LIB=$V python -u bench.py --steps 5 --cpu-sample 0 --ref-shapes 0 ;;
     check) step pytest_gpu 900 python -u -m pytest tests -m gpu -x -v --timeout 400 --timeout-method thread &&
            step smoke 300 python -c "import __graft_entry__ as g; g.smoke()" &&
            step bench 900 python -u bench.py ;;
