@@ -88,6 +88,7 @@ for s in "$@"; do
            done
            step bs_bench_def 300 python -u bench.py --steps 5 --cpu-sample 0 --ref-shapes 0 &&
            step bs_bench_blk 300 env QPGPU_LIB=$V python -u bench.py --steps 5 --cpu-sample 0 --ref-shapes 0 ;;
+    hipapi) step prof_hipapi 300 rocprofv3 --hip-trace --kernel-trace --stats --output-format csv -d gpurun_out/prof_hipapi -o run -- python3 tools/agg_subtree.py 256 1 ;;
     check) step pytest_gpu 900 python -u -m pytest tests -m gpu -x -v --timeout 400 --timeout-method thread &&
            step smoke 300 python -c "import __graft_entry__ as g; g.smoke()" &&
            step bench 900 python -u bench.py ;;
