@@ -43,6 +43,24 @@ class Prover:
         ln = ctypes.c_size_t()
         lib().qp_prover_proof_size(self.h, ctypes.byref(ln))
         self.proof_size = ln.value
+        self._out = self._mv = self._lens = None
+
+    def _out_buffers(self, nb):
+        """The output rows ([nb][proof_size]) and lengths the prove calls write:
+        kept across calls (a prover proves one batch at a time), so a call neither
+        zero-fills a fresh buffer nor copies it whole before splitting it."""
+        need = self.proof_size * nb
+        if self._out is None or len(self._out) < need:
+            self._out = (ctypes.c_char * need)()
+            self._mv = memoryview(self._out).cast("B")
+        if self._lens is None or len(self._lens) < nb:
+            self._lens = (ctypes.c_size_t * nb)()
+        return self._out, self._lens
+
+    def _proofs(self, nb):
+        """The nb serialized proofs of the last call, one copy each."""
+        mv, ps, lens = self._mv, self.proof_size, self._lens
+        return [mv[i * ps:i * ps + lens[i]].tobytes() for i in range(nb)]
 
     def verifier_data(self):
         ln = ctypes.c_size_t()
@@ -54,11 +72,9 @@ class Prover:
     def prove_witnesses(self, witnesses):
         nb = len(witnesses)
         arr = (ctypes.c_void_p * nb)(*[w.h.value for w in witnesses])
-        out = ctypes.create_string_buffer(self.proof_size * nb)
-        lens = (ctypes.c_size_t * nb)()
+        out, lens = self._out_buffers(nb)
         self.ctx.check(lib().qp_prover_prove(self.h, arr, nb, out, self.proof_size, lens), "qp_prover_prove")
-        raw = out.raw
-        return [raw[i * self.proof_size:i * self.proof_size + lens[i]] for i in range(nb)]
+        return self._proofs(nb)
 
     def inputs_array(self, inputs):
         """CircuitInputs / VoteCircuitData list -> contiguous C-ABI struct array."""
@@ -68,14 +84,12 @@ class Prover:
         return arr
 
     def prove_inputs_array(self, arr, nb):
-        out = ctypes.create_string_buffer(self.proof_size * nb)
-        lens = (ctypes.c_size_t * nb)()
+        out, lens = self._out_buffers(nb)
         fn = lib().qp_prover_prove_voting_inputs if self.circuit.kind == "voting" else \
             lib().qp_prover_prove_wormhole_inputs
         self.ctx.check(fn(self.h, ctypes.cast(arr, ctypes.c_void_p), nb, out, self.proof_size, lens),
                        "qp_prover_prove_inputs")
-        raw = out.raw
-        return [raw[i * self.proof_size:i * self.proof_size + lens[i]] for i in range(nb)]
+        return self._proofs(nb)
 
     def prove_inputs(self, inputs):
         """End to end: commit(inputs) + prove() for a list of CircuitInputs (Wormhole)
@@ -114,33 +128,27 @@ class Prover:
             arr[i].proofs, arr[i].lens, arr[i].nproofs = ctypes.cast(pa, ctypes.c_void_p), \
                 ctypes.cast(la, ctypes.c_void_p), len(ps)
             arr[i].zk_randomness = ctypes.cast(zp, ctypes.c_void_p) if zp else None
-        out = ctypes.create_string_buffer(self.proof_size * nb)
-        lens = (ctypes.c_size_t * nb)()
+        out, lens = self._out_buffers(nb)
         self.ctx.check(lib().qp_prover_prove_aggregation(self.h, ctypes.cast(arr, ctypes.c_void_p), nb, out,
                                                          self.proof_size, lens), "qp_prover_prove_aggregation")
-        raw = out.raw
-        return [raw[i * self.proof_size:i * self.proof_size + lens[i]] for i in range(nb)]
+        return self._proofs(nb)
 
     def prove_wires(self, wires, pis):
         wires = np.ascontiguousarray(wires, dtype=np.uint64)
         pis = np.ascontiguousarray(pis, dtype=np.uint64)
         nb = wires.shape[0]
-        out = ctypes.create_string_buffer(self.proof_size * nb)
-        lens = (ctypes.c_size_t * nb)()
+        out, lens = self._out_buffers(nb)
         self.ctx.check(lib().qp_prover_prove_wires(self.h, wires, pis, nb, out, self.proof_size, lens),
                        "qp_prover_prove_wires")
-        raw = out.raw
-        return [raw[i * self.proof_size:i * self.proof_size + lens[i]] for i in range(nb)]
+        return self._proofs(nb)
 
     def prove_wires_dev(self, d_wires_ptr, pis, nproofs):
         """wires already resident on the device (device pointer [nproofs][W][n])."""
         pis = np.ascontiguousarray(pis, dtype=np.uint64)
-        out = ctypes.create_string_buffer(self.proof_size * nproofs)
-        lens = (ctypes.c_size_t * nproofs)()
+        out, lens = self._out_buffers(nproofs)
         self.ctx.check(lib().qp_prover_prove_wires_dev(self.h, d_wires_ptr, pis, nproofs, out, self.proof_size, lens),
                        "qp_prover_prove_wires_dev")
-        raw = out.raw
-        return [raw[i * self.proof_size:i * self.proof_size + lens[i]] for i in range(nproofs)]
+        return self._proofs(nproofs)
 
     def set_timing(self, enable=True):
         lib().qp_prover_set_timing(self.h, int(enable))

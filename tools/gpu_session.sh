@@ -89,6 +89,19 @@ for s in "$@"; do
            step bs_bench_def 300 python -u bench.py --steps 5 --cpu-sample 0 --ref-shapes 0 &&
            step bs_bench_blk 300 env QPGPU_LIB=$V python -u bench.py --steps 5 --cpu-sample 0 --ref-shapes 0 ;;
     hipapi) step prof_hipapi 300 rocprofv3 --hip-trace --kernel-trace --stats --output-format csv -d gpurun_out/prof_hipapi -o run -- python3 tools/agg_subtree.py 256 1 ;;
+    votprof) step prof_vot 300 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/prof_vot -o run -- python3 bench.py --circuit voting --steps 2 --warmup 1 --cpu-sample 0 --ref-shapes 0 &&
+             step vot_ksum 120 python3 tools/kernel_summary.py gpurun_out/prof_vot/run_kernel_trace.csv gpurun_out/vot_kernel_summary.json "bench voting batch 1024, 6 provers" &&
+             step vot_trace 120 python3 tools/agg_trace.py gpurun_out/prof_vot/run_kernel_trace.csv gpurun_out/vot_trace.json ;;
+    pyout) P=qp-zk-circuits-rm_amd/qp_wormhole/prover.py
+           cp $P /tmp/prover_new.py
+           for r in 1 2; do
+             cp gpurun_ab_tmp/prover_old.py $P
+             step py_old_w_$r 300 python -u bench.py --steps 5 --cpu-sample 0 --ref-shapes 0 --configs3 0 --agg-leaves 0 &&
+             step py_old_v_$r 300 python -u bench.py --circuit voting --steps 5 --cpu-sample 0 --ref-shapes 0 || { cp /tmp/prover_new.py $P; exit 1; }
+             cp /tmp/prover_new.py $P
+             step py_new_w_$r 300 python -u bench.py --steps 5 --cpu-sample 0 --ref-shapes 0 --configs3 0 --agg-leaves 0 &&
+             step py_new_v_$r 300 python -u bench.py --circuit voting --steps 5 --cpu-sample 0 --ref-shapes 0 || exit $?
+           done ;;
     check) step pytest_gpu 900 python -u -m pytest tests -m gpu -x -v --timeout 400 --timeout-method thread &&
            step smoke 300 python -c "import __graft_entry__ as g; g.smoke()" &&
            step bench 900 python -u bench.py ;;
