@@ -102,6 +102,15 @@ for s in "$@"; do
              step py_new_w_$r 300 python -u bench.py --steps 5 --cpu-sample 0 --ref-shapes 0 --configs3 0 --agg-leaves 0 &&
              step py_new_v_$r 300 python -u bench.py --circuit voting --steps 5 --cpu-sample 0 --ref-shapes 0 || exit $?
            done ;;
+    pyagg) P=qp-zk-circuits-rm_amd/qp_wormhole/prover.py
+           cp $P /tmp/prover_new.py
+           for r in 1 2; do
+             cp gpurun_ab_tmp/prover_old.py $P
+             step pa_old_$r 300 python -u tools/agg_subtree.py 256 2 || { cp /tmp/prover_new.py $P; exit 1; }
+             cp /tmp/prover_new.py $P
+             step pa_new_$r 300 python -u tools/agg_subtree.py 256 2 || exit $?
+           done
+           step pa_bench 300 python -u bench.py --steps 5 --cpu-sample 0 --ref-shapes 0 ;;
     check) step pytest_gpu 900 python -u -m pytest tests -m gpu -x -v --timeout 400 --timeout-method thread &&
            step smoke 300 python -c "import __graft_entry__ as g; g.smoke()" &&
            step bench 900 python -u bench.py ;;
