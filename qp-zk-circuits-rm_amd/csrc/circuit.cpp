@@ -124,6 +124,7 @@ Target CircuitBuilder::arithmetic(F c0, F c1, Target m0, Target m1, Target adden
     if (hm1 && gl::mul(m1c, c0) == 1) return m0;
   }
   auto key = std::make_tuple(c0, c1, m0.v, m1.v, addend.v);
+  if (arith_cache_.empty()) arith_cache_.reserve(1u << 16);
   auto it = arith_cache_.find(key);
   if (it != arith_cache_.end()) return it->second;
   // find_slot for ArithmeticGate with constants (c0, c1)
@@ -328,6 +329,39 @@ struct UF {
     if (a != b) p[std::max(a, b)] = std::min(a, b);
   }
 };
+
+// lists of uint32 appended row by row into one offsets and one values array
+// (the build's per-generator lists without an allocation per list)
+struct Rows {
+  std::vector<uint32_t> off{0}, val;
+  struct Span {
+    uint32_t *b, *e;
+    uint32_t *begin() const { return b; }
+    uint32_t *end() const { return e; }
+    size_t size() const { return (size_t)(e - b); }
+  };
+  void push(uint32_t v) { val.push_back(v); }
+  void close() { off.push_back((uint32_t)val.size()); }
+  void close_unique() {  // the open row sorted, duplicates dropped
+    const auto b = val.begin() + off.back();
+    std::sort(b, val.end());
+    val.erase(std::unique(b, val.end()), val.end());
+    close();
+  }
+  Span operator[](size_t r) { return {val.data() + off[r], val.data() + off[r + 1]}; }
+};
+
+// counting sort: for keys k[i] < nkeys (i in order), off[k] .. off[k + 1] of
+// the returned index list holds the i with key k, ascending
+void group_by_key(const std::vector<uint32_t> &keys, size_t nkeys, std::vector<uint32_t> &off,
+                  std::vector<uint32_t> &idx) {
+  off.assign(nkeys + 1, 0);
+  for (uint32_t k : keys) off[k + 1]++;
+  for (size_t k = 0; k < nkeys; k++) off[k + 1] += off[k];
+  idx.resize(keys.size());
+  std::vector<uint32_t> cur(off.begin(), off.end() - 1);
+  for (size_t i = 0; i < keys.size(); i++) idx[cur[keys[i]]++] = (uint32_t)i;
+}
 }  // namespace
 
 CircuitData CircuitBuilder::build() {
@@ -467,18 +501,23 @@ CircuitData CircuitBuilder::build() {
   }
   // ---- sigma polynomials: each partition's routed wires form a cycle
   {
-    std::vector<std::vector<uint32_t>> members(nparts);
+    // each partition's routed wires in (row, col) order
+    std::vector<uint32_t> mkeys((size_t)n * R), moff, midx;
     for (uint32_t row = 0; row < n; row++)
-      for (uint32_t col = 0; col < R; col++) members[part[row * W + col]].push_back(row * W + col);
+      for (uint32_t col = 0; col < R; col++) mkeys[(size_t)row * R + col] = part[row * W + col];
+    group_by_key(mkeys, nparts, moff, midx);
     const uint64_t w = gl::root_of_unity(cd.degree_bits);
     std::vector<F> wpow(n);
     wpow[0] = 1;
     for (uint32_t i = 1; i < n; i++) wpow[i] = gl::mul(wpow[i - 1], w);
     cd.constants_sigmas.assign((size_t)(cd.num_constants + R) * n, 0);
     F *sig = cd.constants_sigmas.data() + (size_t)cd.num_constants * n;
-    for (auto &m : members) {
-      for (size_t i = 0; i < m.size(); i++) {
-        uint32_t src = m[i], dst = m[(i + 1) % m.size()];
+    auto wire_of = [&](uint32_t k) { return (k / R) * W + k % R; };  // mkeys index -> row * W + col
+    for (size_t p = 0; p < nparts; p++) {
+      const uint32_t *m = midx.data() + moff[p];
+      const size_t msz = moff[p + 1] - moff[p];
+      for (size_t i = 0; i < msz; i++) {
+        uint32_t src = wire_of(m[i]), dst = wire_of(m[(i + 1) % msz]);
         uint32_t srow = src / W, scol = src % W, drow = dst / W, dcol = dst % W;
         sig[(size_t)scol * n + srow] = gl::mul(cd.k_is[dcol], wpow[drow]);
       }
@@ -498,58 +537,58 @@ CircuitData CircuitBuilder::build() {
   {
     auto pt = [&](Target t) { return part[tindex(t)]; };
     auto wpt = [&](uint32_t row, uint32_t col) { return part[row * W + col]; };
-    std::vector<std::vector<uint32_t>> gin(gens_.size()), gout(gens_.size());
+    Rows gin, gout;  // per generator: the partitions it reads (sorted, unique) / writes
     for (size_t gi = 0; gi < gens_.size(); gi++) {
       const Gen &g = gens_[gi];
       switch (g.kind) {
         case GEN_CONSTANT:
-          for (uint32_t j = 0; j < ncg; j++) gout[gi].push_back(wpt(g.row, j));
+          for (uint32_t j = 0; j < ncg; j++) gout.push(wpt(g.row, j));
           break;
         case GEN_ARITH:
-          for (uint32_t j = 0; j < 3; j++) gin[gi].push_back(wpt(g.row, 4 * g.op + j));
-          gout[gi].push_back(wpt(g.row, 4 * g.op + 3));
+          for (uint32_t j = 0; j < 3; j++) gin.push(wpt(g.row, 4 * g.op + j));
+          gout.push(wpt(g.row, 4 * g.op + 3));
           break;
         case GEN_POSEIDON:
-          for (uint32_t j = 0; j < 12; j++) gin[gi].push_back(wpt(g.row, j));
-          gin[gi].push_back(wpt(g.row, 24));
+          for (uint32_t j = 0; j < 12; j++) gin.push(wpt(g.row, j));
+          gin.push(wpt(g.row, 24));
           for (uint32_t j = 12; j < W; j++)
-            if (j != 24) gout[gi].push_back(wpt(g.row, j));
+            if (j != 24) gout.push(wpt(g.row, j));
           break;
         case GEN_BASE_SPLIT:
-          gin[gi].push_back(wpt(g.row, 0));
-          for (uint32_t j = 1; j <= base_sum_limbs_; j++) gout[gi].push_back(wpt(g.row, j));
+          gin.push(wpt(g.row, 0));
+          for (uint32_t j = 1; j <= base_sum_limbs_; j++) gout.push(wpt(g.row, j));
           break;
         case GEN_EQUALITY:
-          gin[gi].push_back(pt(g.a));
-          gin[gi].push_back(pt(g.b));
-          gout[gi].push_back(pt(g.c));
-          gout[gi].push_back(pt(g.d));
+          gin.push(pt(g.a));
+          gin.push(pt(g.b));
+          gout.push(pt(g.c));
+          gout.push(pt(g.d));
           break;
         case GEN_WIRE_SPLIT:
-          gin[gi].push_back(pt(g.a));
-          for (uint32_t j = 0; j < g.op; j++) gout[gi].push_back(wpt(g.row + j, 0));
+          gin.push(pt(g.a));
+          for (uint32_t j = 0; j < g.op; j++) gout.push(wpt(g.row + j, 0));
           break;
         case GEN_EXT_DIV:
-          for (Target t : {g.a, g.b, g.c, g.d}) gin[gi].push_back(pt(t));
-          gout[gi].push_back(pt(g.e));
-          gout[gi].push_back(pt(g.f));
+          for (Target t : {g.a, g.b, g.c, g.d}) gin.push(pt(t));
+          gout.push(pt(g.e));
+          gout.push(pt(g.f));
           break;
         case GEN_RANDOM_ACCESS:
-          gin[gi].push_back(wpt(g.row, ra_wire_index(g.op)));
-          for (uint32_t i = 0; i < RA_VEC; i++) gin[gi].push_back(wpt(g.row, ra_wire_item(i, g.op)));
-          gout[gi].push_back(wpt(g.row, ra_wire_claimed(g.op)));
-          for (uint32_t i = 0; i < RA_BITS; i++) gout[gi].push_back(wpt(g.row, ra_wire_bit(i, g.op)));
+          gin.push(wpt(g.row, ra_wire_index(g.op)));
+          for (uint32_t i = 0; i < RA_VEC; i++) gin.push(wpt(g.row, ra_wire_item(i, g.op)));
+          gout.push(wpt(g.row, ra_wire_claimed(g.op)));
+          for (uint32_t i = 0; i < RA_BITS; i++) gout.push(wpt(g.row, ra_wire_bit(i, g.op)));
           break;
         default: {
           std::vector<std::pair<uint32_t, uint32_t>> rd, wr;
           gen_row_wires(g.kind, g.row, g.op, rd, wr);
-          for (auto &rc : rd) gin[gi].push_back(wpt(rc.first, rc.second));
-          for (auto &rc : wr) gout[gi].push_back(wpt(rc.first, rc.second));
+          for (auto &rc : rd) gin.push(wpt(rc.first, rc.second));
+          for (auto &rc : wr) gout.push(wpt(rc.first, rc.second));
           break;
         }
       }
-      std::sort(gin[gi].begin(), gin[gi].end());
-      gin[gi].erase(std::unique(gin[gi].begin(), gin[gi].end()), gin[gi].end());
+      gin.close_unique();
+      gout.close();
     }
     // value slots: only partitions some generator or input sets; slot 0 is the
     // never-set zero slot shared by everything else
@@ -559,18 +598,22 @@ CircuitData CircuitBuilder::build() {
       if (!sid[p]) sid[p] = nslots++;
     };
     for (Target t : inputs_) take(pt(t));
-    for (auto &o : gout)
-      for (uint32_t p : o) take(p);
+    for (uint32_t p : gout.val) take(p);
     cd.num_slots = nslots;
-    for (auto &v : gin)
-      for (auto &p : v) p = sid[p];
-    for (auto &v : gout)
-      for (auto &p : v) p = sid[p];
-    std::vector<std::vector<uint32_t>> watchers(nslots);
-    std::vector<uint32_t> remaining(gens_.size());
-    for (size_t gi = 0; gi < gens_.size(); gi++) {
-      remaining[gi] = (uint32_t)gin[gi].size();
-      for (uint32_t s : gin[gi]) watchers[s].push_back((uint32_t)gi);
+    for (auto &p : gin.val) p = sid[p];
+    for (auto &p : gout.val) p = sid[p];
+    // watchers of slot s: woff[s] .. woff[s + 1] of wgen, generators in order
+    std::vector<uint32_t> remaining(gens_.size()), woff, wgen;
+    {
+      std::vector<uint32_t> wpos;
+      group_by_key(gin.val, nslots, woff, wpos);
+      std::vector<uint32_t> gen_of(gin.val.size());
+      for (size_t gi = 0; gi < gens_.size(); gi++) {
+        remaining[gi] = gin.off[gi + 1] - gin.off[gi];
+        for (uint32_t k = gin.off[gi]; k < gin.off[gi + 1]; k++) gen_of[k] = (uint32_t)gi;
+      }
+      wgen.resize(wpos.size());
+      for (size_t k = 0; k < wpos.size(); k++) wgen[k] = gen_of[wpos[k]];
     }
     std::vector<uint8_t> known(nslots, 0);
     std::vector<uint32_t> queue;
@@ -594,8 +637,8 @@ CircuitData CircuitBuilder::build() {
       }
       if (qh == queue.size()) break;
       uint32_t s = queue[qh++];
-      for (uint32_t gi : watchers[s])
-        if (--remaining[gi] == 0) ready.push_back(gi);
+      for (uint32_t k = woff[s]; k < woff[s + 1]; k++)
+        if (--remaining[wgen[k]] == 0) ready.push_back(wgen[k]);
     }
     if (cd.schedule.size() != gens_.size())
       throw std::runtime_error("witness generation cannot be scheduled: " +
@@ -672,10 +715,12 @@ CircuitData CircuitBuilder::build() {
         }
       }
       const size_t ng = cd.schedule.size();
-      std::vector<std::vector<uint32_t>> rds(ng), wrs(ng);
+      Rows rds, wrs;  // per generator: the slots it reads / writes
+      std::vector<uint32_t> rd, wr;
       for (size_t i = 0; i < ng; i++) {
         const Gen &g = cd.schedule[i];
-        std::vector<uint32_t> &rd = rds[i], &wr = wrs[i];
+        rd.clear();
+        wr.clear();
         switch (g.kind) {
           case GEN_CONSTANT: wr = {g.s[0], g.s[1]}; break;
           case GEN_ARITH: rd = {g.s[0], g.s[1], g.s[2]}; wr = {g.s[3]}; break;
@@ -712,6 +757,10 @@ CircuitData CircuitBuilder::build() {
             break;
           }
         }
+        for (uint32_t v : rd) rds.push(v);
+        rds.close();
+        for (uint32_t v : wr) wrs.push(v);
+        wrs.close();
       }
       // host chains (CircuitData::host_gens): forward, the Poseidon (and
       // constant) generators computable from inputs alone with their chain

@@ -16,6 +16,7 @@
 #include <stdint.h>
 #include <map>
 #include <string>
+#include <tuple>
 #include <unordered_map>
 #include <vector>
 
@@ -361,7 +362,16 @@ class CircuitBuilder {
   std::unordered_map<F, Target> const_to_target_;
   std::unordered_map<uint32_t, F> target_to_const_;
   std::map<std::pair<F, F>, std::pair<uint32_t, uint32_t>> arith_open_;  // (c0,c1) -> (row, next op)
-  std::map<std::tuple<F, F, uint32_t, uint32_t, uint32_t>, Target> arith_cache_;
+  using ArithKey = std::tuple<F, F, uint32_t, uint32_t, uint32_t>;
+  struct ArithKeyHash {
+    size_t operator()(const ArithKey &k) const {
+      uint64_t h = std::get<0>(k) * 0x9E3779B97F4A7C15ull ^ std::get<1>(k);
+      h = (h ^ (h >> 29)) * 0xBF58476D1CE4E5B9ull ^ std::get<2>(k);
+      h = (h ^ (h >> 31)) * 0x94D049BB133111EBull ^ ((uint64_t)std::get<3>(k) << 32 | std::get<4>(k));
+      return (size_t)(h ^ (h >> 32));
+    }
+  };
+  std::unordered_map<ArithKey, Target, ArithKeyHash> arith_cache_;  // find/insert only (no iteration)
   std::map<std::pair<F, F>, std::pair<uint32_t, uint32_t>> ae_open_;  // ArithmeticExtensionGate slots
   std::map<F, std::pair<uint32_t, uint32_t>> me_open_;                 // MulExtensionGate slots
   std::map<std::tuple<F, F, uint32_t, uint32_t, uint32_t, uint32_t, uint32_t, uint32_t>, ExtT> ext_cache_;
