@@ -490,38 +490,40 @@ CircuitData CircuitBuilder::build() {
   auto tindex = [&](Target t) -> uint32_t { return t.is_virtual() ? (uint32_t)(nwires + (t.v & ~Target::VIRT)) : t.row() * W + t.col(); };
   UF uf(nwires + nvirt_);
   for (auto &cp : copies_) uf.unite(tindex(cp.first), tindex(cp.second));
-  // partition id per target (dense, in target-index order of first member)
-  std::vector<uint32_t> part_of_rep(nwires + nvirt_, 0xFFFFFFFFu);
+  // partition id per target (dense, in target-index order of first member).
+  // Every parent index is below its child's (unite hangs the larger root
+  // under the smaller, find halves paths), so a set's root is its first
+  // member and one ascending pass labels every target from its parent's label
   uint32_t nparts = 0;
   std::vector<uint32_t> part(nwires + nvirt_);
-  for (size_t i = 0; i < nwires + nvirt_; i++) {
-    uint32_t r = uf.find((uint32_t)i);
-    if (part_of_rep[r] == 0xFFFFFFFFu) part_of_rep[r] = nparts++;
-    part[i] = part_of_rep[r];
-  }
+  for (size_t i = 0; i < nwires + nvirt_; i++) part[i] = uf.p[i] == i ? nparts++ : part[uf.p[i]];
   // ---- sigma polynomials: each partition's routed wires form a cycle
   {
-    // each partition's routed wires in (row, col) order
-    std::vector<uint32_t> mkeys((size_t)n * R), moff, midx;
-    for (uint32_t row = 0; row < n; row++)
-      for (uint32_t col = 0; col < R; col++) mkeys[(size_t)row * R + col] = part[row * W + col];
-    group_by_key(mkeys, nparts, moff, midx);
+    // each partition's routed wires, in (row, col) order, form a cycle: the
+    // successor of routed wire k = row * R + col is the partition's next
+    // member, the last member's its first (one backward pass)
+    const size_t nk = (size_t)n * R;
+    std::vector<uint32_t> succ(nk), first(nparts, UINT32_MAX);
+    for (size_t k = nk; k-- > 0;) {
+      const uint32_t p = part[(k / R) * W + k % R];
+      succ[k] = first[p];
+      first[p] = (uint32_t)k;
+    }
+    for (size_t k = 0; k < nk; k++)
+      if (succ[k] == UINT32_MAX) succ[k] = first[part[(k / R) * W + k % R]];
     const uint64_t w = gl::root_of_unity(cd.degree_bits);
     std::vector<F> wpow(n);
     wpow[0] = 1;
     for (uint32_t i = 1; i < n; i++) wpow[i] = gl::mul(wpow[i - 1], w);
     cd.constants_sigmas.assign((size_t)(cd.num_constants + R) * n, 0);
     F *sig = cd.constants_sigmas.data() + (size_t)cd.num_constants * n;
-    auto wire_of = [&](uint32_t k) { return (k / R) * W + k % R; };  // mkeys index -> row * W + col
-    for (size_t p = 0; p < nparts; p++) {
-      const uint32_t *m = midx.data() + moff[p];
-      const size_t msz = moff[p + 1] - moff[p];
-      for (size_t i = 0; i < msz; i++) {
-        uint32_t src = wire_of(m[i]), dst = wire_of(m[(i + 1) % msz]);
-        uint32_t srow = src / W, scol = src % W, drow = dst / W, dcol = dst % W;
-        sig[(size_t)scol * n + srow] = gl::mul(cd.k_is[dcol], wpow[drow]);
+    // sigma_col[row] = k_dcol * w^drow of the successor, column by column
+    // (sequential stores instead of one scattered store per wire)
+    for (uint32_t col = 0; col < R; col++)
+      for (uint32_t row = 0; row < n; row++) {
+        const uint32_t d = succ[(size_t)row * R + col];
+        sig[(size_t)col * n + row] = gl::mul(cd.k_is[d % R], wpow[d / R]);
       }
-    }
     // selectors + gate constants
     for (uint32_t row = 0; row < n; row++) {
       const GateInst &gi = rows_[row];
@@ -645,12 +647,13 @@ CircuitData CircuitBuilder::build() {
                                std::to_string(gens_.size() - cd.schedule.size()) + " generators never become ready");
     cd.wire_slot.resize(nwires);
     cd.wire_slot_cm.resize(nwires);
-    for (uint32_t row = 0; row < n; row++)
-      for (uint32_t col = 0; col < W; col++) {
-        const uint32_t s = sid[part[(size_t)row * W + col]];
-        cd.wire_slot[(size_t)row * W + col] = s;
-        cd.wire_slot_cm[(size_t)col * n + row] = s;
-      }
+    for (size_t i = 0; i < nwires; i++) cd.wire_slot[i] = sid[part[i]];
+    // the column-major copy by 64-row tiles (each column's 64 stores contiguous)
+    for (uint32_t r0 = 0; r0 < n; r0 += 64) {
+      const uint32_t r1 = std::min<uint32_t>(n, r0 + 64);
+      for (uint32_t col = 0; col < W; col++)
+        for (uint32_t row = r0; row < r1; row++) cd.wire_slot_cm[(size_t)col * n + row] = cd.wire_slot[(size_t)row * W + col];
+    }
     cd.virt_slot.resize(nvirt_);
     for (uint32_t v = 0; v < nvirt_; v++) cd.virt_slot[v] = sid[part[nwires + v]];
     {
