@@ -1000,15 +1000,20 @@ int gen_witness_batch(qp_prover *P, uint32_t nb) {
   // 16-lane row
   a.row = qpk::path_opt("wit_row", 1) != 0;
   // a launch per dependency level over the whole batch (default for small
-  // aggregation batches: their 55 levels are mostly one permutation deep, and
-  // one workgroup per proof leaves each level at a one-lane permutation's
-  // latency) or one workgroup per proof (the leaf circuits, large batches);
-  // path hook wit_mode=0|1 forces one
+  // batches: one workgroup per proof leaves each level at a one-lane
+  // permutation's latency) or one workgroup per proof (large batches, and the
+  // voting circuit); path hook wit_mode=0|1 forces one
   const long wmode = qpk::path_opt("wit_mode", -1);
   // (measured: one aggregation proof 11.0 -> 9.4 ms, witness 2.9 -> 1.3 ms;
   // at 32 proofs per launch 3.78 vs 3.88 ms for one workgroup per proof,
-  // profiles/r05_ab_witness_levels.log)
-  const bool by_level = wmode >= 0 ? wmode == 1 : P->circuit->kind == qp_circuit::AGGREGATION && nb <= 24;
+  // profiles/r05_ab_witness_levels.log.  Wormhole: witness 3.2-3.6 -> 1.6-2.2
+  // ms per call at 1-32 proofs, one proof 8.5 -> 6.8 ms; the 3-prover
+  // headline neutral either way; voting at 171 proofs 4 % slower by level:
+  // profiles/r06_wit_modes_by_batch.log, r06_ab_wit_levels.log)
+  const auto kind = P->circuit->kind;
+  const bool by_level = wmode >= 0 ? wmode == 1
+                                   : (kind == qp_circuit::AGGREGATION && nb <= 24) ||
+                                         (kind == qp_circuit::WORMHOLE && nb <= 32);
   if (by_level) {
     const auto &lo = P->circuit->cd.level_off;
     const auto &lp = P->circuit->cd.level_pos;

@@ -44,6 +44,20 @@ def test_device_witness_matches_host_witness(env):
     assert dev[3] == cpu
 
 
+def test_device_witness_forms_agree(env, monkeypatch):
+    """The two device witness forms -- a launch per dependency level (the
+    default up to 32 Wormhole proofs) and one workgroup per proof (larger
+    batches; QPGPU_PATHS wit_mode=0 forces it) -- prove the same bytes."""
+    from qp_wormhole.synthetic import synthetic_inputs
+    ctx, circ, prover = env
+    inputs = [WI.test_inputs()] + [synthetic_inputs(k, d) for k, d in ((31, 3), (32, 12))]
+    by_level = prover.prove_inputs(inputs)
+    monkeypatch.setenv("QPGPU_PATHS", "wit_mode=0")
+    per_proof = prover.prove_inputs(inputs)
+    monkeypatch.delenv("QPGPU_PATHS")
+    assert by_level == per_proof
+
+
 def test_device_witness_conflict_is_reported(env):
     """storage_proof_tests.rs:30-100 / nullifier_tests.rs:38-48: inconsistent
     inputs make generation fail with "set twice with different values"."""

@@ -111,6 +111,23 @@ for s in "$@"; do
              step pa_new_$r 300 python -u tools/agg_subtree.py 256 2 || exit $?
            done
            step pa_bench 300 python -u bench.py --steps 5 --cpu-sample 0 --ref-shapes 0 ;;
+    lattrace) step lat_plain 120 python -u tools/latency_trace.py 5 &&
+              step prof_lat 300 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/prof_lat -o run -- python3 tools/latency_trace.py 5 &&
+              step lat_ksum 120 python3 tools/kernel_summary.py gpurun_out/prof_lat/run_kernel_trace.csv gpurun_out/lat_kernel_summary.json "one proof at a time, 5 timed" &&
+              step lat_trace 120 python3 tools/agg_trace.py gpurun_out/prof_lat/run_kernel_trace.csv gpurun_out/lat_trace.json 1 ;;
+    latwit) for r in 1 2; do
+              step lw_def_$r 120 python -u tools/latency_trace.py 8 &&
+              step lw_lvl_$r 120 env QPGPU_PATHS=wit_mode=1 python -u tools/latency_trace.py 8 &&
+              step lw_hc16_$r 120 env QPGPU_PATHS=host_chain=16 python -u tools/latency_trace.py 8 &&
+              step lw_lvl_hc16_$r 120 env QPGPU_PATHS=wit_mode=1,host_chain=16 python -u tools/latency_trace.py 8 &&
+              step lw_lvl_hc8_$r 120 env QPGPU_PATHS=wit_mode=1,host_chain=8 python -u tools/latency_trace.py 8 || exit $?
+            done ;;
+    witab) for r in 1 2; do
+             step wa_w_def_$r 300 python -u bench.py --steps 5 --cpu-sample 0 --ref-shapes 0 --configs3 0 --agg-leaves 0 &&
+             step wa_w_lvl_$r 300 env QPGPU_PATHS=wit_mode=1 python -u bench.py --steps 5 --cpu-sample 0 --ref-shapes 0 --configs3 0 --agg-leaves 0 &&
+             step wa_v_def_$r 300 python -u bench.py --circuit voting --steps 5 --cpu-sample 0 --ref-shapes 0 &&
+             step wa_v_lvl_$r 300 env QPGPU_PATHS=wit_mode=1 python -u bench.py --circuit voting --steps 5 --cpu-sample 0 --ref-shapes 0 || exit $?
+           done ;;
     check) step pytest_gpu 900 python -u -m pytest tests -m gpu -x -v --timeout 400 --timeout-method thread &&
            step smoke 300 python -c "import __graft_entry__ as g; g.smoke()" &&
            step bench 900 python -u bench.py ;;
