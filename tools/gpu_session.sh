@@ -128,6 +128,11 @@ for s in "$@"; do
              step wa_v_def_$r 300 python -u bench.py --circuit voting --steps 5 --cpu-sample 0 --ref-shapes 0 &&
              step wa_v_lvl_$r 300 env QPGPU_PATHS=wit_mode=1 python -u bench.py --circuit voting --steps 5 --cpu-sample 0 --ref-shapes 0 || exit $?
            done ;;
+    graphwit) step gw_tests 600 python -u -m pytest tests/test_gpu_witness.py tests/test_gpu_aggregation.py tests/test_gpu_reference_proof.py -x -q --timeout 400 --timeout-method thread &&
+              step gw_lat 120 python -u tools/latency_trace.py 8 &&
+              step gw_modes 400 python -u tools/wit_modes.py 1 4 16 32 &&
+              step gw_agg 300 python -u tools/agg_subtree.py 256 2 &&
+              step gw_afc 300 python -u tools/agg_first_call.py ;;
     check) step pytest_gpu 900 python -u -m pytest tests -m gpu -x -v --timeout 400 --timeout-method thread &&
            step smoke 300 python -c "import __graft_entry__ as g; g.smoke()" &&
            step bench 900 python -u bench.py ;;
