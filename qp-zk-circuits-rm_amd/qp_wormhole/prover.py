@@ -44,6 +44,7 @@ class Prover:
         lib().qp_prover_proof_size(self.h, ctypes.byref(ln))
         self.proof_size = ln.value
         self._out = self._mv = self._lens = None
+        self._lock = threading.Lock()  # one prove call at a time (the device buffers and the output rows)
 
     def _out_buffers(self, nb):
         """The output rows ([nb][proof_size]) and lengths the prove calls write:
@@ -62,6 +63,13 @@ class Prover:
         mv, ps, lens = self._mv, self.proof_size, self._lens
         return [mv[i * ps:i * ps + lens[i]].tobytes() for i in range(nb)]
 
+    def _prove(self, nb, what, call):
+        """call(out, lens) -> status for nb proofs, under the prover's lock."""
+        with self._lock:
+            out, lens = self._out_buffers(nb)
+            self.ctx.check(call(out, lens), what)
+            return self._proofs(nb)
+
     def verifier_data(self):
         ln = ctypes.c_size_t()
         lib().qp_prover_verifier_data(self.h, None, 0, ctypes.byref(ln))
@@ -72,9 +80,8 @@ class Prover:
     def prove_witnesses(self, witnesses):
         nb = len(witnesses)
         arr = (ctypes.c_void_p * nb)(*[w.h.value for w in witnesses])
-        out, lens = self._out_buffers(nb)
-        self.ctx.check(lib().qp_prover_prove(self.h, arr, nb, out, self.proof_size, lens), "qp_prover_prove")
-        return self._proofs(nb)
+        return self._prove(nb, "qp_prover_prove",
+                           lambda out, lens: lib().qp_prover_prove(self.h, arr, nb, out, self.proof_size, lens))
 
     def inputs_array(self, inputs):
         """CircuitInputs / VoteCircuitData list -> contiguous C-ABI struct array."""
@@ -84,12 +91,11 @@ class Prover:
         return arr
 
     def prove_inputs_array(self, arr, nb):
-        out, lens = self._out_buffers(nb)
         fn = lib().qp_prover_prove_voting_inputs if self.circuit.kind == "voting" else \
             lib().qp_prover_prove_wormhole_inputs
-        self.ctx.check(fn(self.h, ctypes.cast(arr, ctypes.c_void_p), nb, out, self.proof_size, lens),
-                       "qp_prover_prove_inputs")
-        return self._proofs(nb)
+        return self._prove(nb, "qp_prover_prove_inputs",
+                           lambda out, lens: fn(self.h, ctypes.cast(arr, ctypes.c_void_p), nb, out, self.proof_size,
+                                                lens))
 
     def prove_inputs(self, inputs):
         """End to end: commit(inputs) + prove() for a list of CircuitInputs (Wormhole)
@@ -128,27 +134,24 @@ class Prover:
             arr[i].proofs, arr[i].lens, arr[i].nproofs = ctypes.cast(pa, ctypes.c_void_p), \
                 ctypes.cast(la, ctypes.c_void_p), len(ps)
             arr[i].zk_randomness = ctypes.cast(zp, ctypes.c_void_p) if zp else None
-        out, lens = self._out_buffers(nb)
-        self.ctx.check(lib().qp_prover_prove_aggregation(self.h, ctypes.cast(arr, ctypes.c_void_p), nb, out,
-                                                         self.proof_size, lens), "qp_prover_prove_aggregation")
-        return self._proofs(nb)
+        return self._prove(nb, "qp_prover_prove_aggregation",
+                           lambda out, lens: lib().qp_prover_prove_aggregation(
+                               self.h, ctypes.cast(arr, ctypes.c_void_p), nb, out, self.proof_size, lens))
 
     def prove_wires(self, wires, pis):
         wires = np.ascontiguousarray(wires, dtype=np.uint64)
         pis = np.ascontiguousarray(pis, dtype=np.uint64)
         nb = wires.shape[0]
-        out, lens = self._out_buffers(nb)
-        self.ctx.check(lib().qp_prover_prove_wires(self.h, wires, pis, nb, out, self.proof_size, lens),
-                       "qp_prover_prove_wires")
-        return self._proofs(nb)
+        return self._prove(nb, "qp_prover_prove_wires",
+                           lambda out, lens: lib().qp_prover_prove_wires(self.h, wires, pis, nb, out,
+                                                                          self.proof_size, lens))
 
     def prove_wires_dev(self, d_wires_ptr, pis, nproofs):
         """wires already resident on the device (device pointer [nproofs][W][n])."""
         pis = np.ascontiguousarray(pis, dtype=np.uint64)
-        out, lens = self._out_buffers(nproofs)
-        self.ctx.check(lib().qp_prover_prove_wires_dev(self.h, d_wires_ptr, pis, nproofs, out, self.proof_size, lens),
-                       "qp_prover_prove_wires_dev")
-        return self._proofs(nproofs)
+        return self._prove(nproofs, "qp_prover_prove_wires_dev",
+                           lambda out, lens: lib().qp_prover_prove_wires_dev(self.h, d_wires_ptr, pis, nproofs, out,
+                                                                              self.proof_size, lens))
 
     def set_timing(self, enable=True):
         lib().qp_prover_set_timing(self.h, int(enable))
