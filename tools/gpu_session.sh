@@ -133,6 +133,21 @@ for s in "$@"; do
               step gw_modes 400 python -u tools/wit_modes.py 1 4 16 32 &&
               step gw_agg 300 python -u tools/agg_subtree.py 256 2 &&
               step gw_afc 300 python -u tools/agg_first_call.py ;;
+    q1rpm) V=qp-zk-circuits-rm_amd/qp_wormhole/variants/libqpgpu_q1rpm.so
+           step qp_test 300 env QPGPU_LIB=$V python -u -m pytest tests/test_gpu_reference_proof.py tests/test_gpu_prover.py -x -q --timeout 200 --timeout-method thread &&
+           for r in 1 2; do
+             step qp_def_$r 300 python -u bench.py --steps 5 --cpu-sample 0 --ref-shapes 0 --configs3 0 --agg-leaves 0 &&
+             step qp_pm_$r 300 env QPGPU_LIB=$V python -u bench.py --steps 5 --cpu-sample 0 --ref-shapes 0 --configs3 0 --agg-leaves 0 || exit $?
+           done &&
+           step qp_pmc_def 300 rocprofv3 --pmc FETCH_SIZE --kernel-include-regex k_quotient_1r --output-format csv -d gpurun_out/qp_pmc_def -o run -- python3 bench.py --steps 1 --warmup 1 --cpu-sample 0 --provers 1 --batch 128 --configs3 0 --ref-shapes 0 &&
+           step qp_pmc_pm 300 env QPGPU_LIB=$V rocprofv3 --pmc FETCH_SIZE --kernel-include-regex k_quotient_1r --output-format csv -d gpurun_out/qp_pmc_pm -o run -- python3 bench.py --steps 1 --warmup 1 --cpu-sample 0 --provers 1 --batch 128 --configs3 0 --ref-shapes 0 ;;
+    qppm) V=qp-zk-circuits-rm_amd/qp_wormhole/variants/libqpgpu_qparts_pm.so
+          step qpp_test 600 env QPGPU_LIB=$V python -u -m pytest tests/test_gpu_aggregation.py tests/test_gpu_seams.py tests/test_gpu_prover.py -x -q --timeout 400 --timeout-method thread &&
+          step qpp_test_def 300 python -u -m pytest tests/test_gpu_reference_proof.py tests/test_gpu_prover.py tests/test_gpu_seams.py -x -q --timeout 300 --timeout-method thread &&
+          for r in 1 2; do
+            step qpp_def_$r 300 python -u tools/agg_subtree.py 256 2 &&
+            step qpp_pm_$r 300 env QPGPU_LIB=$V python -u tools/agg_subtree.py 256 2 || exit $?
+          done ;;
     check) step pytest_gpu 900 python -u -m pytest tests -m gpu -x -v --timeout 400 --timeout-method thread &&
            step smoke 300 python -c "import __graft_entry__ as g; g.smoke()" &&
            step bench 900 python -u bench.py ;;
