@@ -148,6 +148,11 @@ for s in "$@"; do
             step qpp_def_$r 300 python -u tools/agg_subtree.py 256 2 &&
             step qpp_pm_$r 300 env QPGPU_LIB=$V python -u tools/agg_subtree.py 256 2 || exit $?
           done ;;
+    prevab) V=qp-zk-circuits-rm_amd/qp_wormhole/variants/libqpgpu_prev.so
+            for r in 1 2 3; do
+              step pv_new_$r 300 python -u bench.py --steps 10 --cpu-sample 0 --ref-shapes 0 --configs3 0 --agg-leaves 0 &&
+              step pv_old_$r 300 env QPGPU_LIB=$V python -u bench.py --steps 10 --cpu-sample 0 --ref-shapes 0 --configs3 0 --agg-leaves 0 || exit $?
+            done ;;
     check) step pytest_gpu 900 python -u -m pytest tests -m gpu -x -v --timeout 400 --timeout-method thread &&
            step smoke 300 python -c "import __graft_entry__ as g; g.smoke()" &&
            step bench 900 python -u bench.py ;;
