@@ -153,6 +153,12 @@ for s in "$@"; do
               step pv_new_$r 300 python -u bench.py --steps 10 --cpu-sample 0 --ref-shapes 0 --configs3 0 --agg-leaves 0 &&
               step pv_old_$r 300 env QPGPU_LIB=$V python -u bench.py --steps 10 --cpu-sample 0 --ref-shapes 0 --configs3 0 --agg-leaves 0 || exit $?
             done ;;
+    pm2) V=qp-zk-circuits-rm_amd/qp_wormhole/variants/libqpgpu_pm2.so
+         step pm2_test 300 env QPGPU_LIB=$V python -u -m pytest tests/test_gpu_reference_proof.py tests/test_gpu_prover.py tests/test_gpu_witness.py -x -q --timeout 300 --timeout-method thread &&
+         for r in 1 2 3; do
+           step pm2_def_$r 300 python -u bench.py --steps 10 --cpu-sample 0 --ref-shapes 0 --configs3 0 --agg-leaves 0 &&
+           step pm2_new_$r 300 env QPGPU_LIB=$V python -u bench.py --steps 10 --cpu-sample 0 --ref-shapes 0 --configs3 0 --agg-leaves 0 || exit $?
+         done ;;
     check) step pytest_gpu 900 python -u -m pytest tests -m gpu -x -v --timeout 400 --timeout-method thread &&
            step smoke 300 python -c "import __graft_entry__ as g; g.smoke()" &&
            step bench 900 python -u bench.py ;;
