@@ -1,8 +1,8 @@
-"""Soak check: many Wormhole batches through the production path (three provers
-on their own streams and threads, as bench.py), each step's inputs a fresh
+"""Soak check: many Wormhole (or voting) batches through the production path
+(three provers -- six for voting -- on their own streams and threads, as bench.py), each step's inputs a fresh
 seeded set, and every proof checked by the CPU oracle verifier on a host
 thread pool.  A rare kernel or scheduling race would show up as a proof that
-does not verify.  Usage: python tools/soak.py [steps] [batch]"""
+does not verify.  Usage: python tools/soak.py [steps] [batch] [wormhole|voting]"""
 import concurrent.futures
 import json
 import os
@@ -23,8 +23,9 @@ def main():
     from oracle_lib import lib as olib
     steps = int(sys.argv[1]) if len(sys.argv) > 1 else 8
     B = int(sys.argv[2]) if len(sys.argv) > 2 else 256
-    NP = 3
-    circ = qp_wormhole.Circuit.wormhole(zero_knowledge=False)
+    voting = len(sys.argv) > 3 and sys.argv[3] == "voting"
+    NP = 6 if voting else 3  # as bench.py
+    circ = qp_wormhole.Circuit.voting() if voting else qp_wormhole.Circuit.wormhole(zero_knowledge=False)
     per = [B // NP + (1 if i < B % NP else 0) for i in range(NP)]
     provers = [qp_wormhole.Prover(qp_wormhole.Context(0), circ, max_batch=per[i]) for i in range(NP)]
     vd = provers[0].verifier_data()
@@ -53,7 +54,7 @@ def main():
     for key, f in futs:
         if f.result() != 0:
             bad.append(key)
-    print(json.dumps({"steps": steps, "batch": B, "proofs": steps * B, "verified": steps * B - len(bad),
+    print(json.dumps({"circuit": circ.kind, "steps": steps, "batch": B, "proofs": steps * B, "verified": steps * B - len(bad),
                       "failed": bad[:20], "seconds": time.perf_counter() - t0}))
     sys.exit(1 if bad else 0)
 
